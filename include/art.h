@@ -1,0 +1,208 @@
+/*
+ * art.h -- C ABI of libart.so, the MI355X (gfx950) engine for the hot path of
+ * SamWitte/Adiabatic_RayTracer: the per-ray Hamiltonian ODE of a photon/axion
+ * segment around a neutron star (Goldreich-Julian plasma, rotating dipole,
+ * Schwarzschild metric), its Vern6/RK4 integration, resonance detection and the
+ * conversion probability at each crossing.
+ *
+ * Every entry point replaces a reference interface (file:line under
+ * /root/reference/src):
+ *
+ *   art_propagate_host / _device   RT.propagate              RayTracer.jl:171-452
+ *       (callers MainRunner.jl:179-182 photon, :187-190 axion)
+ *   art_get_prob_nonad_host/_dev   get_Prob_nonAD            MainRunner.jl:67-124
+ *       (-> RT.conversion_prob RayTracer.jl:1405-1473; callers MainRunner.jl:134,265)
+ *   art_sample_conversion_points_* RT.find_samples_new + k_norm_Cart
+ *                                  RayTracer.jl:1480-1653, MainRunner.jl:463-529
+ *   art_find_conversion_surface    RT.Find_Conversion_Surface RayTracer.jl:1250-1263
+ *   art_flux_histogram_device      plot/flux.py:38-48 (binned flux, reduced over ranks)
+ *   art_eval_*_device              pointwise physics (func!, func_axion!, hamiltonian,
+ *                                  GJ_Model_ωp_vecSPH, condition) for parity tests
+ *
+ * Conventions
+ *   - All arrays are caller-owned. Position/momentum arrays are structure-of-arrays,
+ *     exactly the memory of a Julia column-major N x 3 Matrix{Float64}:
+ *     x[0..n) = x-column, x[n..2n) = y-column, x[2n..3n) = z-column.
+ *   - *_host entry points take host pointers and do H2D/kernel/D2H on the library's
+ *     own HIP stream (a Julia ccall passes Vector/Matrix pointers straight through).
+ *     *_device entry points take device (HBM) pointers plus a hipStream_t passed as
+ *     void* (NULL = the library stream); they are asynchronous on that stream.
+ *   - Return 0 on success or a negative ART_E* code; art_last_error() describes it.
+ *   - Thread safety: calls are serialized by an internal mutex; one device per call
+ *     (art_set_device).
+ */
+#ifndef ART_H
+#define ART_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ART_ABI_VERSION 1
+
+/* error codes */
+#define ART_OK 0
+#define ART_E_INVALID (-1)     /* bad argument / unsupported option */
+#define ART_E_HIP (-2)         /* HIP runtime error */
+#define ART_E_NOMEM (-3)       /* device allocation failed */
+#define ART_E_UNSUPPORTED (-4) /* melrose=0 (dead code at the reference's fixed flags) */
+
+/* integrators */
+#define ART_VERN6 0 /* adaptive Verner 6(5), the reference's Vern6() (RayTracer.jl:383) */
+#define ART_RK4 1   /* fixed-step classical RK4 in ln t (BASELINE config 1) */
+
+/* per-ray segment status (the reference's sol.retcode, refined) */
+#define ART_STATUS_SUCCESS 0    /* reached ln_t_end                      (:Success)    */
+#define ART_STATUS_CROSSING 1   /* terminate! after max_crossings         (:Terminated) */
+#define ART_STATUS_HIT_NS 2     /* photon r < 1.01 rNS (cb_r, :352-368)   (:Terminated) */
+#define ART_STATUS_MAXITERS 3   /* maxiters step attempts                 (:MaxIters)   */
+#define ART_STATUS_NONFINITE 4  /* NaN/Inf in state or error estimate     (:Unstable)   */
+
+/* species (RT.node.species; MainRunner.jl:175-191) */
+#define ART_AXION 0
+#define ART_PHOTON 1
+
+typedef struct art_params {
+  /* physics: Gen_Samples.jl:139-170, Mvars of MainRunner.jl:177-178,185-186 */
+  double theta_m;   /* θm misalignment angle [rad]                                  */
+  double omega_pul; /* ωPul rotation frequency [1/s]                                */
+  double B0;        /* surface dipole field [G]                                     */
+  double rNS;       /* neutron-star radius [km]                                     */
+  double mass_ns;   /* Mass_NS [solar masses]; get_Prob_nonAD always uses this GR   */
+                    /* mass, even when flat != 0 (MainRunner.jl:75, global)         */
+  double mass_a;    /* axion mass [eV]                                              */
+  double g_agg;     /* axion-photon coupling Ax_g [1/GeV]                          */
+  double bndry_lyr; /* boundary-layer index; <= 0 disables (Gen_Samples.jl:130)    */
+  /* numerics: NumerP = [ln_tstart, ln_tend, ode_err] (MainRunner.jl:411-413),       */
+  /* solve(...) keywords RayTracer.jl:383-384                                        */
+  double ln_t_end;  /* log(1/ωPul)                                                  */
+  double abstol;    /* ode_err = 1e-6                                               */
+  double reltol;    /* 1e-7                                                         */
+  double dtmin;     /* 1e-13 with force_dtmin = true                                */
+  int64_t maxiters; /* 1e5 step attempts                                            */
+  int32_t flat;     /* 1: Mass_NS -> 0 in the ray equations (RayTracer.jl:77,187)   */
+  int32_t isotropic;/* 1: k_par -> 0                                                */
+  int32_t melrose;  /* must be 1 (Gen_Samples.jl:167)                               */
+  int32_t integrator;    /* ART_VERN6 or ART_RK4                                    */
+  int32_t n_fixed;       /* RK4: steps per segment                                  */
+  int32_t interp_points; /* ContinuousCallback interp_points (RayTracer.jl:358 = 50)*/
+} art_params;
+
+/* Outputs of one batch of segments (the 14-tuple of RayTracer.jl:448, per ray). */
+typedef struct art_segment_out {
+  double* x_end;     /* 3n  final Cartesian position [km]       (x_reshaped[:, :, end]) */
+  double* k_end;     /* 3n  final Cartesian momentum [eV]       (v_reshaped[:, :, end]) */
+  double* u7_end;    /* n   final u[7] = erg*Δω                 (dt[:, end], :431)      */
+  double* tau_end;   /* n   final ln t                          (times[end], :444)      */
+  int32_t* status;   /* n   ART_STATUS_*                                               */
+  int32_t* n_accept; /* n   accepted steps                                             */
+  int32_t* n_reject; /* n   rejected steps                                             */
+} art_segment_out;
+
+/* Resonance crossings (xc..Δωc of RayTracer.jl:325-342), layout [(c*cap + j)*n + i]
+ * for component c, crossing j < capacity, ray i. */
+typedef struct art_crossing_buf {
+  int32_t capacity; /* crossings stored per ray (1 for forward trees)               */
+  int32_t* count;   /* n  crossings recorded (> capacity means overflow)            */
+  double* pos;      /* 3*cap*n  xc, yc, zc [km]                                     */
+  double* k;        /* 3*cap*n  kxc, kyc, kzc [eV]                                  */
+  double* t;        /* cap*n    tc = exp(τ) [s]                                     */
+  double* dw;       /* cap*n    Δωc = u7/erg                                        */
+  double* p_nonad;  /* cap*n    get_Prob_nonAD at the crossing, Nc = 1 semantics   */
+} art_crossing_buf;
+
+/* ---- library / device ---- */
+int art_abi_version(void);
+const char* art_last_error(void);
+int art_device_count(int32_t* count);
+int art_set_device(int32_t device);
+int art_synchronize(void);
+/* Duration [ms] of the last propagate kernel, from HIP events recorded on the stream
+ * the kernel ran on. */
+double art_last_kernel_ms(void);
+/* The Vern6 tableau the kernel uses: c[9], A[81] row-major, b[9], bhat[9]. */
+int art_vern6_tableau(double* c, double* A, double* b, double* bhat);
+
+/* ---- RT.Find_Conversion_Surface (RayTracer.jl:1250-1263), pure host math ---- */
+double art_find_conversion_surface(const art_params* p);
+
+/* ---- RT.propagate for a batch of n segments (RayTracer.jl:171-452) ----
+ * x0, k0   : 3n Cartesian start position [km] / momentum (rescaled onto the axion
+ *            mass shell in-kernel exactly as k_norm_Cart, RayTracer.jl:179-186)
+ * erg      : n  Mvars erg (erg_inf_ini) [eV]
+ * dw       : n  Δω (u0[7] = erg*Δω, RayTracer.jl:216)
+ * ln_t0    : n  NumerP[1] = log(max(event.t, e^-30)) (MainRunner.jl:166)
+ * species  : n  ART_PHOTON (func!) or ART_AXION (func_axion!)
+ * max_crossings : terminate! once this many crossings are recorded (RayTracer.jl:346);
+ *            <= 0 means "stop at the first new crossing" exactly like the reference's
+ *            splittings_cutoff = -1 (MainRunner.jl:128).
+ * xc may be NULL when crossings are not wanted (the segment still stops on them). */
+int art_propagate_host(const art_params* p, int64_t n, const double* x0, const double* k0,
+                       const double* erg, const double* dw, const double* ln_t0,
+                       const int8_t* species, int32_t max_crossings,
+                       art_segment_out* out, art_crossing_buf* xc);
+int art_propagate_device(const art_params* p, int64_t n, const double* x0, const double* k0,
+                         const double* erg, const double* dw, const double* ln_t0,
+                         const int8_t* species, int32_t max_crossings,
+                         art_segment_out* out, art_crossing_buf* xc, void* stream);
+
+/* ---- get_Prob_nonAD (MainRunner.jl:67-124) ----
+ * One call of the reference per group: group g covers crossings
+ * [group_start[g], group_start[g+1]) and reproduces the reference's column-major
+ * linear indexing of ksphere/Bsphere inside conversion_prob (RayTracer.jl:1432-1443)
+ * for groups with more than one crossing. group_start == NULL means n_groups == nc
+ * groups of one crossing each (forward-tree semantics).
+ * pos, kpos: 3nc Cartesian; erg_eff: nc = erg_inf_ini .* abs.(Δωc). out: nc P_nonAD. */
+int art_get_prob_nonad_host(const art_params* p, int64_t nc, const double* pos,
+                            const double* kpos, const double* erg_eff,
+                            int64_t n_groups, const int64_t* group_start, double* out);
+int art_get_prob_nonad_device(const art_params* p, int64_t nc, const double* pos,
+                              const double* kpos, const double* erg_eff,
+                              int64_t n_groups, const int64_t* group_start, double* out,
+                              void* stream);
+
+/* ---- conversion-surface sampler (find_samples_new, RayTracer.jl:1480-1653) ----
+ * Draws one accepted sample per ray i in [0, n) with a Philox4x32-10 stream keyed by
+ * (seed, ray_offset + i): attempts are repeated until accepted (MainRunner.jl:463-495).
+ * Outputs (n or 3n, SoA): x [km], k_init (k_norm_Cart onto the axion shell, :529),
+ * erg_inf_ini [eV] (:526), vifty = vIfty/c (unitless, :1651), weights (# crossings on
+ * the accepted line, :1636), attempts (# find_samples_new calls, feeds f_inx :469). */
+int art_sample_conversion_points_host(const art_params* p, double max_r, uint64_t seed,
+                                      int64_t ray_offset, int64_t n, double* x, double* k_init,
+                                      double* erg_inf, double* vifty, int32_t* weights,
+                                      int32_t* attempts);
+int art_sample_conversion_points_device(const art_params* p, double max_r, uint64_t seed,
+                                        int64_t ray_offset, int64_t n, double* x,
+                                        double* k_init, double* erg_inf, double* vifty,
+                                        int32_t* weights, int32_t* attempts, void* stream);
+
+/* ---- binned flux (plot/flux.py:38-48): histogram of the final momentum azimuth
+ * φf = atan2(ky, kx) over [-π, π) in nbins bins, separately for axions (row 0) and
+ * photons (row 1), weight w[i] (NULL = 1), only rays with status SUCCESS whose final
+ * radius exceeds 1.1 rNS (is_final, MainRunner.jl:207-209). hist (2*nbins, device,
+ * float64) is ACCUMULATED into (zero it first). */
+int art_flux_histogram_device(const art_params* p, int64_t n, const double* x_end,
+                              const double* k_end, const int32_t* status,
+                              const int8_t* species, const double* w, int32_t nbins,
+                              double* hist, void* stream);
+
+/* ---- pointwise physics on device, for parity tests (u: 7n SoA r,θ,φ,w_r,w_θ,w_φ,u7) */
+/* func!/func_axion! (RayTracer.jl:71-123): du (7n) */
+int art_eval_rhs_device(const art_params* p, int64_t n, const double* u, const double* tau,
+                        const double* erg, const int8_t* species, double* du, void* stream);
+/* hamiltonian (RayTracer.jl:530-556) at spherical x (3n), covariant k (3n), time T (n),
+ * energy E (n): H (n), dH/dx (3n), dH/dk (3n), dH/dT (n). bndry_lyr applies to all. */
+int art_eval_hamiltonian_device(const art_params* p, int64_t n, const double* x,
+                                const double* k, const double* T, const double* E,
+                                double* H, double* dHdx, double* dHdk, double* dHdT,
+                                void* stream);
+/* resonance condition (RayTracer.jl:254-298): value (n) */
+int art_eval_condition_device(const art_params* p, int64_t n, const double* u,
+                              const double* tau, double* out, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ART_H */
