@@ -1,0 +1,425 @@
+// art_capi.cpp -- the extern "C" boundary of libart.so (declared in include/art.h).
+//
+// Host-pointer entry points (what a Julia ccall passes) stage through pooled device
+// buffers on the library's own HIP stream; device-pointer entry points run
+// asynchronously on the caller's stream. No torch types cross this boundary.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/art.h"
+#include "art_core.h"
+#include "art_internal.h"
+
+
+namespace {
+
+std::mutex g_mu;
+thread_local std::string g_err;
+double g_last_ms = 0.0;
+unsigned long long g_last_stats[art::N_STATS] = {0};
+int g_last_grid = 0;
+
+struct DeviceCtx {
+  int device = -1;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  unsigned long long* scratch = nullptr;  // [0] queue head, [1..N_STATS] statistics
+  std::vector<std::pair<void*, size_t>> pool;  // host-entry staging buffers (grow-only)
+};
+std::vector<DeviceCtx> g_ctx;
+
+int fail(int code, const char* fmt, const char* a = "", const char* b = "") {
+  char buf[512];
+  std::snprintf(buf, sizeof buf, fmt, a, b);
+  g_err = buf;
+  return code;
+}
+
+#define HIP_OK(expr)                                                                       \
+  do {                                                                                     \
+    hipError_t e_ = (expr);                                                                \
+    if (e_ != hipSuccess) return fail(ART_E_HIP, "%s: %s", #expr, hipGetErrorString(e_)); \
+  } while (0)
+
+int current_ctx(DeviceCtx** out) {
+  int dev = 0;
+  HIP_OK(hipGetDevice(&dev));
+  if ((int)g_ctx.size() <= dev) g_ctx.resize(dev + 1);
+  DeviceCtx& c = g_ctx[dev];
+  if (c.device < 0) {
+    c.device = dev;
+    HIP_OK(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking));
+    HIP_OK(hipEventCreate(&c.ev0));
+    HIP_OK(hipEventCreate(&c.ev1));
+    HIP_OK(hipMalloc(&c.scratch, sizeof(unsigned long long) * (1 + art::N_STATS)));
+  }
+  *out = &c;
+  return ART_OK;
+}
+
+int pool_get(DeviceCtx* c, size_t slot, size_t bytes, void** p) {
+  if (c->pool.size() <= slot) c->pool.resize(slot + 1, {nullptr, 0});
+  auto& e = c->pool[slot];
+  if (e.second < bytes) {
+    if (e.first) HIP_OK(hipFree(e.first));
+    e.first = nullptr;
+    e.second = 0;
+    if (hipMalloc(&e.first, bytes) != hipSuccess) return fail(ART_E_NOMEM, "hipMalloc of %s bytes failed", std::to_string(bytes).c_str());
+    e.second = bytes;
+  }
+  *p = e.first;
+  return ART_OK;
+}
+
+int validate(const art_params* p) {
+  if (!p) return fail(ART_E_INVALID, "params is NULL");
+  if (!p->melrose) return fail(ART_E_UNSUPPORTED, "melrose=0 (Ctheta_B_sphere form) is not supported; the reference hard-codes melrose=true (Gen_Samples.jl:167)");
+  if (p->integrator != ART_VERN6 && p->integrator != ART_RK4) return fail(ART_E_INVALID, "unknown integrator");
+  if (p->integrator == ART_RK4 && p->n_fixed < 1) return fail(ART_E_INVALID, "RK4 needs n_fixed >= 1");
+  if (!(p->rNS > 0) || !(p->mass_a > 0) || !(p->omega_pul != 0)) return fail(ART_E_INVALID, "rNS, mass_a must be > 0 and omega_pul != 0");
+  if (!(p->abstol > 0) || !(p->reltol >= 0)) return fail(ART_E_INVALID, "bad tolerances");
+  if (p->maxiters < 1) return fail(ART_E_INVALID, "maxiters must be >= 1");
+  return ART_OK;
+}
+
+hipStream_t pick(DeviceCtx* c, void* stream) { return stream ? (hipStream_t)stream : c->stream; }
+
+int propagate_device_impl(const art_params* p, int64_t n, const double* x0, const double* k0, const double* erg,
+                          const double* dw, const double* ln_t0, const int8_t* species, int32_t max_crossings,
+                          art_segment_out* out, art_crossing_buf* xc, void* stream) {
+  int rc = validate(p);
+  if (rc) return rc;
+  if (n < 0 || n > 2147483647LL) return fail(ART_E_INVALID, "n must be in [0, 2^31)");
+  if (!out || !out->x_end || !out->k_end || !out->u7_end || !out->tau_end || !out->status || !out->n_accept || !out->n_reject)
+    return fail(ART_E_INVALID, "segment output buffers must be non-NULL");
+  if (n == 0) return ART_OK;
+  if (!x0 || !k0 || !erg || !dw || !ln_t0 || !species) return fail(ART_E_INVALID, "input buffers must be non-NULL");
+  DeviceCtx* c;
+  if ((rc = current_ctx(&c))) return rc;
+  hipStream_t s = pick(c, stream);
+  art::KParams K = art::make_kparams(*p);
+  art::SegIn in{x0, k0, erg, dw, ln_t0, species};
+  art::SegOut so{out->x_end, out->k_end, out->u7_end, out->tau_end, out->status, out->n_accept, out->n_reject,
+                 0, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+  if (xc && xc->count) {
+    if (xc->capacity < 1 || !xc->pos || !xc->k || !xc->t || !xc->dw || !xc->p_nonad)
+      return fail(ART_E_INVALID, "crossing buffer incomplete");
+    so.cap = xc->capacity;
+    so.xcount = xc->count;
+    so.xpos = xc->pos; so.xk = xc->k; so.xt = xc->t; so.xdw = xc->dw; so.xp = xc->p_nonad;
+  }
+  HIP_OK(hipMemsetAsync(c->scratch, 0, sizeof(unsigned long long) * (1 + art::N_STATS), s));
+  HIP_OK(hipEventRecord(c->ev0, s));
+  HIP_OK(art::launch_propagate(K, n, in, so, max_crossings, c->scratch, c->scratch + 1, s, &g_last_grid));
+  HIP_OK(hipEventRecord(c->ev1, s));
+  return ART_OK;
+}
+
+int finish_timing(DeviceCtx* c) {
+  HIP_OK(hipEventSynchronize(c->ev1));
+  float ms = 0.f;
+  HIP_OK(hipEventElapsedTime(&ms, c->ev0, c->ev1));
+  g_last_ms = ms;
+  HIP_OK(hipMemcpy(g_last_stats, c->scratch + 1, sizeof(g_last_stats), hipMemcpyDeviceToHost));
+  return ART_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int art_abi_version(void) { return ART_ABI_VERSION; }
+const char* art_last_error(void) { return g_err.c_str(); }
+
+int art_device_count(int32_t* count) {
+  int n = 0;
+  HIP_OK(hipGetDeviceCount(&n));
+  if (count) *count = n;
+  return ART_OK;
+}
+
+int art_set_device(int32_t device) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  HIP_OK(hipSetDevice(device));
+  return ART_OK;
+}
+
+int art_synchronize(void) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  DeviceCtx* c;
+  int rc = current_ctx(&c);
+  if (rc) return rc;
+  HIP_OK(hipStreamSynchronize(c->stream));
+  HIP_OK(hipDeviceSynchronize());
+  return finish_timing(c);
+}
+
+double art_last_kernel_ms(void) { return g_last_ms; }
+
+// Statistics of the last propagate launch (after art_synchronize / a host entry point):
+// [attempts, accepted, root re-steps, scan condition evals, interpolant-root evals, rays,
+//  init RHS evals, reserved]; grid = persistent grid size.
+int art_last_stats(uint64_t* stats, int32_t* grid) {
+  for (int i = 0; i < art::N_STATS; ++i) stats[i] = g_last_stats[i];
+  if (grid) *grid = g_last_grid;
+  return ART_OK;
+}
+
+int art_vern6_tableau(double* c, double* A, double* b, double* bhat) {
+  using V = art::Vern6;
+  const double cc[9] = {0.0, V::c2, V::c3, V::c4, V::c5, V::c6, V::c7, 1.0, 1.0};
+  double AA[9][9] = {{0}};
+  AA[1][0] = V::a21;
+  AA[2][0] = V::a31; AA[2][1] = V::a32;
+  AA[3][0] = V::a41; AA[3][2] = V::a43;
+  AA[4][0] = V::a51; AA[4][2] = V::a53; AA[4][3] = V::a54;
+  AA[5][0] = V::a61; AA[5][2] = V::a63; AA[5][3] = V::a64; AA[5][4] = V::a65;
+  AA[6][0] = V::a71; AA[6][2] = V::a73; AA[6][3] = V::a74; AA[6][4] = V::a75; AA[6][5] = V::a76;
+  AA[7][0] = V::a81; AA[7][2] = V::a83; AA[7][3] = V::a84; AA[7][4] = V::a85; AA[7][5] = V::a86; AA[7][6] = V::a87;
+  AA[8][0] = V::a91; AA[8][3] = V::a94; AA[8][4] = V::a95; AA[8][5] = V::a96; AA[8][6] = V::a97; AA[8][7] = V::a98;
+  const double bh[9] = {V::bh1, 0, 0, V::bh4, V::bh5, V::bh6, 0, V::bh8, V::bh9};
+  for (int i = 0; i < 9; ++i) {
+    c[i] = cc[i];
+    b[i] = AA[8][i];
+    bhat[i] = bh[i];
+    for (int j = 0; j < 9; ++j) A[9 * i + j] = AA[i][j];
+  }
+  return ART_OK;
+}
+
+double art_find_conversion_surface(const art_params* p) {
+  // Find_Conversion_Surface (RayTracer.jl:1250-1263) with fix_time = 0: ωp at the surface
+  // point in the plane of the magnetic axis, then rNS (ωp/m_a)^(2/3) * 1.01.
+  const double th = p->theta_m < art::PI / 2.0 ? p->theta_m / 2.0 : (p->theta_m + art::PI) / 2.0;
+  const double x[3] = {p->rNS * std::sin(th), 0.0, p->rNS * std::cos(th)};
+  const double r = std::sqrt(x[0] * x[0] + x[1] * x[1] + x[2] * x[2]);
+  const double ph = std::atan2(x[1], x[0]);
+  const double t = std::acos(x[2] / r);
+  const double psi = ph;
+  const double Bn = p->B0 * std::pow(p->rNS / r, 3) / 2.0;
+  const double Br = 2.0 * Bn * (std::cos(p->theta_m) * std::cos(t) + std::sin(p->theta_m) * std::sin(t) * std::cos(psi));
+  const double Bt = Bn * (std::cos(p->theta_m) * std::sin(t) - std::sin(p->theta_m) * std::cos(t) * std::cos(psi));
+  const double Bz = Br * std::cos(t) - Bt * std::sin(t);
+  const double ne = std::fabs(2.0 * p->omega_pul * Bz / std::sqrt(4 * art::PI / 137) * 1.95e-2 * art::HBAR);
+  const double wp = std::sqrt(4 * art::PI * ne / 137 / 5.0e5);
+  return p->rNS * std::pow(wp / p->mass_a, 2.0 / 3.0) * 1.01;
+}
+
+int art_propagate_device(const art_params* p, int64_t n, const double* x0, const double* k0, const double* erg,
+                         const double* dw, const double* ln_t0, const int8_t* species, int32_t max_crossings,
+                         art_segment_out* out, art_crossing_buf* xc, void* stream) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  return propagate_device_impl(p, n, x0, k0, erg, dw, ln_t0, species, max_crossings, out, xc, stream);
+}
+
+int art_propagate_host(const art_params* p, int64_t n, const double* x0, const double* k0, const double* erg,
+                       const double* dw, const double* ln_t0, const int8_t* species, int32_t max_crossings,
+                       art_segment_out* out, art_crossing_buf* xc) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  int rc = validate(p);
+  if (rc) return rc;
+  if (n == 0) return ART_OK;
+  DeviceCtx* c;
+  if ((rc = current_ctx(&c))) return rc;
+  const int cap = (xc && xc->count) ? xc->capacity : 0;
+  const size_t nd = (size_t)n;
+  // staging layout: inputs 3n+3n+n+n+n doubles + n int8; outputs 3n+3n+n+n doubles + 3n int32 (+ crossings)
+  void *din, *dout, *dxc = nullptr;
+  const size_t in_bytes = nd * 9 * sizeof(double) + nd;
+  const size_t out_bytes = nd * 8 * sizeof(double) + nd * 3 * sizeof(int32_t);
+  const size_t cnt_bytes = ((nd * sizeof(int32_t) + 15) / 16) * 16;
+  const size_t xc_bytes = cap ? cnt_bytes + (size_t)cap * nd * 9 * sizeof(double) : 0;
+  if ((rc = pool_get(c, 0, in_bytes, &din))) return rc;
+  if ((rc = pool_get(c, 1, out_bytes, &dout))) return rc;
+  if (cap && (rc = pool_get(c, 2, xc_bytes, &dxc))) return rc;
+  double* di = (double*)din;
+  hipStream_t s = c->stream;
+  HIP_OK(hipMemcpyAsync(di, x0, nd * 3 * sizeof(double), hipMemcpyHostToDevice, s));
+  HIP_OK(hipMemcpyAsync(di + 3 * nd, k0, nd * 3 * sizeof(double), hipMemcpyHostToDevice, s));
+  HIP_OK(hipMemcpyAsync(di + 6 * nd, erg, nd * sizeof(double), hipMemcpyHostToDevice, s));
+  HIP_OK(hipMemcpyAsync(di + 7 * nd, dw, nd * sizeof(double), hipMemcpyHostToDevice, s));
+  HIP_OK(hipMemcpyAsync(di + 8 * nd, ln_t0, nd * sizeof(double), hipMemcpyHostToDevice, s));
+  HIP_OK(hipMemcpyAsync((int8_t*)(di + 9 * nd), species, nd, hipMemcpyHostToDevice, s));
+  double* dd = (double*)dout;
+  int32_t* di32 = (int32_t*)(dd + 8 * nd);
+  art_segment_out dso{dd, dd + 3 * nd, dd + 6 * nd, dd + 7 * nd, di32, di32 + nd, di32 + 2 * nd};
+  art_crossing_buf dxb{};
+  art_crossing_buf* dxbp = nullptr;
+  if (cap) {
+    int32_t* cnt = (int32_t*)dxc;
+    double* xd = (double*)((char*)dxc + cnt_bytes);
+    dxb = art_crossing_buf{cap, cnt, xd, xd + 3 * cap * nd, xd + 6 * cap * nd, xd + 7 * cap * nd, xd + 8 * cap * nd};
+    dxbp = &dxb;
+  }
+  rc = propagate_device_impl(p, n, di, di + 3 * nd, di + 6 * nd, di + 7 * nd, di + 8 * nd, (const int8_t*)(di + 9 * nd),
+                             max_crossings, &dso, dxbp, s);
+  if (rc) return rc;
+  HIP_OK(hipMemcpyAsync(out->x_end, dso.x_end, nd * 3 * sizeof(double), hipMemcpyDeviceToHost, s));
+  HIP_OK(hipMemcpyAsync(out->k_end, dso.k_end, nd * 3 * sizeof(double), hipMemcpyDeviceToHost, s));
+  HIP_OK(hipMemcpyAsync(out->u7_end, dso.u7_end, nd * sizeof(double), hipMemcpyDeviceToHost, s));
+  HIP_OK(hipMemcpyAsync(out->tau_end, dso.tau_end, nd * sizeof(double), hipMemcpyDeviceToHost, s));
+  HIP_OK(hipMemcpyAsync(out->status, dso.status, nd * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+  HIP_OK(hipMemcpyAsync(out->n_accept, dso.n_accept, nd * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+  HIP_OK(hipMemcpyAsync(out->n_reject, dso.n_reject, nd * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+  if (cap) {
+    HIP_OK(hipMemcpyAsync(xc->count, dxb.count, nd * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    HIP_OK(hipMemcpyAsync(xc->pos, dxb.pos, (size_t)cap * nd * 3 * sizeof(double), hipMemcpyDeviceToHost, s));
+    HIP_OK(hipMemcpyAsync(xc->k, dxb.k, (size_t)cap * nd * 3 * sizeof(double), hipMemcpyDeviceToHost, s));
+    HIP_OK(hipMemcpyAsync(xc->t, dxb.t, (size_t)cap * nd * sizeof(double), hipMemcpyDeviceToHost, s));
+    HIP_OK(hipMemcpyAsync(xc->dw, dxb.dw, (size_t)cap * nd * sizeof(double), hipMemcpyDeviceToHost, s));
+    HIP_OK(hipMemcpyAsync(xc->p_nonad, dxb.p_nonad, (size_t)cap * nd * sizeof(double), hipMemcpyDeviceToHost, s));
+  }
+  HIP_OK(hipStreamSynchronize(s));
+  return finish_timing(c);
+}
+
+int art_get_prob_nonad_device(const art_params* p, int64_t nc, const double* pos, const double* kpos,
+                              const double* erg_eff, int64_t n_groups, const int64_t* group_start, double* out,
+                              void* stream) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  int rc = validate(p);
+  if (rc) return rc;
+  if (nc == 0) return ART_OK;
+  if (!pos || !kpos || !erg_eff || !out) return fail(ART_E_INVALID, "NULL buffer");
+  if (!group_start) n_groups = nc;
+  DeviceCtx* c;
+  if ((rc = current_ctx(&c))) return rc;
+  HIP_OK(art::launch_prob(art::make_kparams(*p), nc, pos, kpos, erg_eff, n_groups, group_start, out, pick(c, stream)));
+  return ART_OK;
+}
+
+int art_get_prob_nonad_host(const art_params* p, int64_t nc, const double* pos, const double* kpos,
+                            const double* erg_eff, int64_t n_groups, const int64_t* group_start, double* out) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  int rc = validate(p);
+  if (rc) return rc;
+  if (nc == 0) return ART_OK;
+  if (!group_start) n_groups = nc;
+  if (group_start) {  // groups must tile [0, nc)
+    if (group_start[0] != 0 || group_start[n_groups] != nc) return fail(ART_E_INVALID, "group_start must span [0, nc]");
+    for (int64_t g = 0; g < n_groups; ++g)
+      if (group_start[g + 1] <= group_start[g]) return fail(ART_E_INVALID, "empty or unsorted group");
+  }
+  DeviceCtx* c;
+  if ((rc = current_ctx(&c))) return rc;
+  void* d;
+  const size_t nd = (size_t)nc;
+  const size_t bytes = nd * 8 * sizeof(double) + (size_t)(n_groups + 1) * sizeof(int64_t);
+  if ((rc = pool_get(c, 3, bytes, &d))) return rc;
+  double* dd = (double*)d;
+  int64_t* dg = group_start ? (int64_t*)(dd + 8 * nd) : nullptr;
+  hipStream_t s = c->stream;
+  HIP_OK(hipMemcpyAsync(dd, pos, nd * 3 * sizeof(double), hipMemcpyHostToDevice, s));
+  HIP_OK(hipMemcpyAsync(dd + 3 * nd, kpos, nd * 3 * sizeof(double), hipMemcpyHostToDevice, s));
+  HIP_OK(hipMemcpyAsync(dd + 6 * nd, erg_eff, nd * sizeof(double), hipMemcpyHostToDevice, s));
+  if (dg) HIP_OK(hipMemcpyAsync(dg, group_start, (size_t)(n_groups + 1) * sizeof(int64_t), hipMemcpyHostToDevice, s));
+  HIP_OK(art::launch_prob(art::make_kparams(*p), nc, dd, dd + 3 * nd, dd + 6 * nd, n_groups, dg, dd + 7 * nd, s));
+  HIP_OK(hipMemcpyAsync(out, dd + 7 * nd, nd * sizeof(double), hipMemcpyDeviceToHost, s));
+  HIP_OK(hipStreamSynchronize(s));
+  return ART_OK;
+}
+
+int art_sample_conversion_points_device(const art_params* p, double max_r, uint64_t seed, int64_t ray_offset,
+                                        int64_t n, double* x, double* k_init, double* erg_inf, double* vifty,
+                                        int32_t* weights, int32_t* attempts, void* stream) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  int rc = validate(p);
+  if (rc) return rc;
+  if (n == 0) return ART_OK;
+  if (n > 2147483647LL) return fail(ART_E_INVALID, "n must be < 2^31");
+  if (!(max_r > p->rNS)) return fail(ART_E_INVALID, "max_r must exceed rNS (MainRunner.jl:389-396 quits otherwise)");
+  DeviceCtx* c;
+  if ((rc = current_ctx(&c))) return rc;
+  hipStream_t s = pick(c, stream);
+  HIP_OK(hipMemsetAsync(c->scratch, 0, sizeof(unsigned long long), s));
+  HIP_OK(art::launch_sample(art::make_kparams(*p), max_r, seed, ray_offset, n, x, k_init, erg_inf, vifty, weights,
+                            attempts, c->scratch, s));
+  return ART_OK;
+}
+
+int art_sample_conversion_points_host(const art_params* p, double max_r, uint64_t seed, int64_t ray_offset, int64_t n,
+                                      double* x, double* k_init, double* erg_inf, double* vifty, int32_t* weights,
+                                      int32_t* attempts) {
+  int rc;
+  DeviceCtx* c;
+  void* d;
+  const size_t nd = (size_t)n;
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if ((rc = current_ctx(&c))) return rc;
+    if ((rc = pool_get(c, 4, nd * 10 * sizeof(double) + nd * 2 * sizeof(int32_t), &d))) return rc;
+  }
+  double* dd = (double*)d;
+  int32_t* di = (int32_t*)(dd + 10 * nd);
+  if ((rc = art_sample_conversion_points_device(p, max_r, seed, ray_offset, n, dd, dd + 3 * nd, dd + 6 * nd, dd + 7 * nd,
+                                                di, di + nd, c->stream)))
+    return rc;
+  std::lock_guard<std::mutex> lk(g_mu);
+  hipStream_t s = c->stream;
+  HIP_OK(hipMemcpyAsync(x, dd, nd * 3 * sizeof(double), hipMemcpyDeviceToHost, s));
+  HIP_OK(hipMemcpyAsync(k_init, dd + 3 * nd, nd * 3 * sizeof(double), hipMemcpyDeviceToHost, s));
+  HIP_OK(hipMemcpyAsync(erg_inf, dd + 6 * nd, nd * sizeof(double), hipMemcpyDeviceToHost, s));
+  HIP_OK(hipMemcpyAsync(vifty, dd + 7 * nd, nd * 3 * sizeof(double), hipMemcpyDeviceToHost, s));
+  HIP_OK(hipMemcpyAsync(weights, di, nd * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+  HIP_OK(hipMemcpyAsync(attempts, di + nd, nd * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+  HIP_OK(hipStreamSynchronize(s));
+  return ART_OK;
+}
+
+int art_flux_histogram_device(const art_params* p, int64_t n, const double* x_end, const double* k_end,
+                              const int32_t* status, const int8_t* species, const double* w, int32_t nbins,
+                              double* hist, void* stream) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  int rc = validate(p);
+  if (rc) return rc;
+  if (nbins < 1 || nbins > 4096) return fail(ART_E_INVALID, "nbins must be in [1, 4096]");
+  if (n == 0) return ART_OK;
+  DeviceCtx* c;
+  if ((rc = current_ctx(&c))) return rc;
+  HIP_OK(art::launch_flux(art::make_kparams(*p), n, x_end, k_end, status, species, w, nbins, hist, pick(c, stream)));
+  return ART_OK;
+}
+
+int art_eval_rhs_device(const art_params* p, int64_t n, const double* u, const double* tau, const double* erg,
+                        const int8_t* species, double* du, void* stream) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  int rc = validate(p);
+  if (rc) return rc;
+  if (n == 0) return ART_OK;
+  DeviceCtx* c;
+  if ((rc = current_ctx(&c))) return rc;
+  HIP_OK(art::launch_eval_rhs(art::make_kparams(*p), n, u, tau, erg, species, du, pick(c, stream)));
+  return ART_OK;
+}
+
+int art_eval_hamiltonian_device(const art_params* p, int64_t n, const double* x, const double* k, const double* T,
+                                const double* E, double* H, double* dHdx, double* dHdk, double* dHdT, void* stream) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  int rc = validate(p);
+  if (rc) return rc;
+  if (n == 0) return ART_OK;
+  DeviceCtx* c;
+  if ((rc = current_ctx(&c))) return rc;
+  HIP_OK(art::launch_eval_hamiltonian(art::make_kparams(*p), n, x, k, T, E, H, dHdx, dHdk, dHdT, pick(c, stream)));
+  return ART_OK;
+}
+
+int art_eval_condition_device(const art_params* p, int64_t n, const double* u, const double* tau, double* out,
+                              void* stream) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  int rc = validate(p);
+  if (rc) return rc;
+  if (n == 0) return ART_OK;
+  DeviceCtx* c;
+  if ((rc = current_ctx(&c))) return rc;
+  HIP_OK(art::launch_eval_condition(art::make_kparams(*p), n, u, tau, out, pick(c, stream)));
+  return ART_OK;
+}
+
+}  // extern "C"

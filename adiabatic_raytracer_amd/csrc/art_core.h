@@ -1,0 +1,788 @@
+// art_core.h -- physics of the adiabatic axion<->photon ray-tracing hot path for CDNA4.
+//
+// Every function restates a reference function of SamWitte/Adiabatic_RayTracer
+// (file:line under /root/reference/src). Gradients that the reference takes with
+// ForwardDiff dual numbers (RayTracer.jl:21,24,84-88,1427-1432) are HAND-DERIVED here:
+// one fused pass yields H's 7 partial derivatives with ~5x fewer operations than the
+// reference's three dual-number passes, and no transcendental is evaluated twice.
+//
+// Everything is templated on the scalar type T so the same source compiles
+//   * as T = double in the gfx950 kernels (art_kernels.hip), and
+//   * as an op-counting type on the host (tools/count_flops.cpp) -- the
+//     "instrumented restatement" that fixes the algorithmic FLOPs per ray-step.
+// Branch conditions compare T against doubles, so the counting type carries a value.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/art.h"
+
+namespace art {
+
+// Constants.jl:3-5
+constexpr double C_KM = 2.99792e5;
+constexpr double HBAR = 6.582119e-16;
+constexpr double GNEW = 132712000000.0;
+constexpr double PI = 3.141592653589793;
+
+// ---- scalar math for T = double (the op-counting type provides its own overloads) ----
+__host__ __device__ inline double msqrt(double x) { return sqrt(x); }
+__host__ __device__ inline double mexp(double x) { return exp(x); }
+__host__ __device__ inline double mabs(double x) { return fabs(x); }
+__host__ __device__ inline double msign(double x) { return copysign(1.0, x); }  // ForwardDiff abs: signbit
+// sin and cos together: FMA Cody-Waite reduction by π/2 (3 parts) + the fdlibm kernels on
+// [-π/4, π/4]; <= 1 ulp against glibc for |x| <= 200 (tests/test_corecheck.py). The ray's
+// angles θ and ψ = φ - ωt stay small, so the large-argument (Payne-Hanek) path that
+// ocml's sincos carries -- ~200 instructions of code per call site -- is never needed.
+__host__ __device__ inline void msincos(double x, double& s, double& c) {
+  const double n = rint(x * 0.63661977236758134308);
+  double r = fma(-n, 1.5707963267948966, x);
+  r = fma(-n, 6.123233995736766e-17, r);
+  r = fma(-n, -1.4973849048591698e-33, r);
+  const double z = r * r;
+  const double ps = 8.33333333332248946124e-03 +
+                    z * (-1.98412698298579493134e-04 +
+                         z * (2.75573137070700676789e-06 + z * (-2.50507602534068634195e-08 + z * 1.58969099521155010221e-10)));
+  const double sr = r + r * z * (-1.66666666666666324348e-01 + z * ps);
+  const double pc =
+      z * (4.16666666666666019037e-02 +
+           z * (-1.38888888888741095749e-03 +
+                z * (2.48015872894767294178e-05 +
+                     z * (-2.75573143513906633035e-07 + z * (2.08757232129817482790e-09 + z * -1.13596475577881948265e-11)))));
+  const double hz = 0.5 * z, w = 1.0 - hz;
+  const double cr = w + (((1.0 - w) - hz) + z * pc);
+  const int q = ((int)n) & 3;
+  const double ss = (q & 1) ? cr : sr;
+  const double cc = (q & 1) ? sr : cr;
+  s = (q & 2) ? -ss : ss;
+  c = ((q + 1) & 2) ? -cc : cc;
+}
+__host__ __device__ inline double msin(double x) { return sin(x); }
+__host__ __device__ inline double mcos(double x) { return cos(x); }
+__host__ __device__ inline double macos(double x) { return acos(x); }
+__host__ __device__ inline double matan2(double y, double x) { return atan2(y, x); }
+__host__ __device__ inline double mpow(double x, double p) { return pow(x, p); }
+__host__ __device__ inline bool misnan(double x) { return isnan(x); }
+__host__ __device__ inline double mmax(double a, double b) { return a > b ? a : b; }
+
+// Kernel-side parameters: art_params plus derived constants, passed by value (kernarg ->
+// SGPRs: the NS parameters are wave-uniform scalars, never per-lane data).
+struct KParams {
+  double cm, sm;          // cos θm, sin θm
+  double omega;           // ωPul
+  double Bn_coef;         // B0 rNS^3 / 2  (B_n = Bn_coef / r^3, RayTracer.jl:1143)
+  double rNS, rNS101;     // rNS, 1.01 rNS
+  double rs_gr, rs_eff;   // 2 GNew M / c^2 (GR); flat ? 0 : rs_gr
+  double wp2_coef;        // ωp^2 = wp2_coef |Bz| (RayTracer.jl:1153-1154)
+  double mass_a, mass_a2; // m_a, m_a^2
+  double g_agg;
+  double bndry_lyr, pole_val, rmax, rmax_def;  // boundary layer (RayTracer.jl:1155-1162)
+  double GM_c2;           // GNew M / c^2 (Cristoffel, get_Prob_nonAD erg_ax)
+  double ln_t_end, abstol, reltol, dtmin;
+  int64_t maxiters;
+  int32_t flat, isotropic, integrator, n_fixed, interp_points, pad;
+};
+
+inline KParams make_kparams(const art_params& p) {
+  KParams k{};
+  k.cm = cos(p.theta_m);
+  k.sm = sin(p.theta_m);
+  k.omega = p.omega_pul;
+  k.Bn_coef = 0.5 * p.B0 * p.rNS * p.rNS * p.rNS;
+  k.rNS = p.rNS;
+  k.rNS101 = p.rNS * 1.01;
+  k.rs_gr = 2.0 * GNEW * p.mass_ns / (C_KM * C_KM);
+  k.rs_eff = p.flat ? 0.0 : k.rs_gr;
+  const double ne_coef = fabs(2.0 * p.omega_pul / sqrt(4.0 * PI / 137.0) * 1.95e-2 * HBAR);
+  k.wp2_coef = 4.0 * PI * ne_coef / 137.0 / 5.0e5;
+  k.mass_a = p.mass_a;
+  k.mass_a2 = p.mass_a * p.mass_a;
+  k.g_agg = p.g_agg;
+  k.bndry_lyr = p.bndry_lyr;
+  const double ne_pole = fabs(2.0 * p.omega_pul * p.B0 / sqrt(4.0 * PI / 137.0) * 1.95e-2 * HBAR);
+  k.pole_val = sqrt(4.0 * PI * ne_pole / 137.0 / 5.0e5);
+  k.rmax = p.rNS * pow(k.pole_val / p.mass_a, 2.0 / 3.0);
+  k.rmax_def = p.rNS * pow(k.pole_val / 1e-5, 2.0 / 3.0);  // get_Prob_nonAD passes no Mass_a (:97)
+  k.GM_c2 = GNEW * p.mass_ns / (C_KM * C_KM);
+  k.ln_t_end = p.ln_t_end;
+  k.abstol = p.abstol;
+  k.reltol = p.reltol;
+  k.dtmin = p.dtmin;
+  k.maxiters = p.maxiters;
+  k.flat = p.flat;
+  k.isotropic = p.isotropic;
+  k.integrator = p.integrator;
+  k.n_fixed = p.n_fixed;
+  k.interp_points = p.interp_points < 2 ? 2 : p.interp_points;
+  return k;
+}
+
+// ---------------------------------------------------------------------------
+// g_schwartz (RayTracer.jl:455-501): g^tt, g^rr and d/dr. The interior patch is switched
+// on r <= 10 km, the keyword default that hot-path callers never override (:455).
+template <class T>
+__host__ __device__ inline void metric_tr(const T& r, double rs, T& gtt, T& grr) {
+  if (r <= 10.0) {
+    const T rsp = rs * (r * r * r) * 1e-3;  // rs (r/10)^3 (:463)
+    grr = 1.0 - r * r * rsp * 1e-3;
+    const T D = 3.0 * msqrt(1.0 - rsp * 0.1) - msqrt(grr);
+    gtt = -4.0 / (D * D);
+  } else {
+    grr = 1.0 - rs / r;
+    gtt = -1.0 / grr;
+  }
+}
+
+template <class T>
+__host__ __device__ inline void metric_tr_d(const T& r, double rs, T& gtt, T& grr, T& dgtt, T& dgrr) {
+  if (r <= 10.0) {
+    const T r2 = r * r;
+    const T rsp = rs * (r2 * r) * 1e-3;
+    grr = 1.0 - r2 * rsp * 1e-3;                  // 1 - rs r^5 / 1e6
+    dgrr = -5e-6 * rs * (r2 * r2);
+    const T S1 = msqrt(1.0 - rsp * 0.1);          // sqrt(1 - rs r^3 / 1e4)
+    const T dS1 = (-1.5e-4 * rs * r2) / S1;
+    const T S2 = msqrt(grr);
+    const T dS2 = 0.5 * dgrr / S2;
+    const T D = 3.0 * S1 - S2;
+    const T iD = 1.0 / D;
+    gtt = -4.0 * iD * iD;
+    dgtt = 8.0 * (3.0 * dS1 - dS2) * iD * iD * iD;
+  } else {
+    const T ir = 1.0 / r;
+    grr = 1.0 - rs * ir;
+    dgrr = rs * ir * ir;
+    const T ig = 1.0 / grr;
+    gtt = -ig;
+    dgtt = dgrr * ig * ig;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Rotating oblique dipole (RayTracer.jl:1142-1151): B = B_n (2 a1, a2, a3) with
+// a1 = cosθm cosθ + sinθm sinθ cosψ, a2 = cosθm sinθ - sinθm cosθ cosψ, a3 = sinθm sinψ,
+// ψ = φ - ωt, B_n = B0 (rNS/r)^3 / 2. The GJ density uses b = Bz/B_n = 2 a1 cosθ - a2 sinθ.
+template <class T>
+struct DipoleAng {
+  T a1, a2, a3;        // angular factors
+  T a1t, a1p, a2p, a3p;  // ∂θ a1, ∂φ a1, ∂φ a2, ∂φ a3  (∂θ a2 = a1, ∂θ a3 = 0)
+  T b, bt, bp;         // Bz/B_n and its θ, φ derivatives
+};
+
+template <class T>
+__host__ __device__ inline DipoleAng<T> dipole_ang(const KParams& P, const T& st, const T& ct, const T& sp,
+                                                   const T& cp) {
+  DipoleAng<T> d;
+  d.a1 = P.cm * ct + P.sm * st * cp;
+  d.a2 = P.cm * st - P.sm * ct * cp;
+  d.a3 = P.sm * sp;
+  d.a1t = P.sm * ct * cp - P.cm * st;
+  d.a1p = -P.sm * st * sp;
+  d.a2p = P.sm * ct * sp;
+  d.a3p = P.sm * cp;
+  d.b = 2.0 * d.a1 * ct - d.a2 * st;
+  d.bt = 2.0 * d.a1t * ct - 3.0 * d.a1 * st - d.a2 * ct;
+  d.bp = 2.0 * d.a1p * ct - d.a2p * st;
+  return d;
+}
+
+// Boundary-layer increment of ωp (RayTracer.jl:1158-1161), r >= rNS.
+template <class T>
+__host__ __device__ inline T layer_wp(const KParams& P, const T& r, double rmax) {
+  const T x = P.rNS / r;
+  return P.pole_val * x * msqrt(x) * mexp(-(r - rmax * P.bndry_lyr) / (0.1 * rmax));
+}
+
+// ---------------------------------------------------------------------------
+// func! (RayTracer.jl:71-91) with hamiltonian (:530-556, melrose=true), GJ_Model_ωp_vecSPH
+// (:1120-1170), K_par (:1044-1058), g_schwartz (:455-501), all partials hand-derived:
+//   H = ½[K + ωp²(1 - Q)],  K = g^tt E² + g^rr k_r² + g^θθ k_θ² + g^φφ k_φ²,
+//   Q = g^rr k∥²/E²,  k∥² = p²/β,  p = 2√g^rr k_r a1 + (k_θ a2 + k_φ a3/|sinθ|)/r,
+//   β = 4a1² + a2² + a3²  (|B|² = B_n² β, so B_n cancels from k∥),  ωp² = C |B_n b|.
+// du[1:3] = ∂H/∂k c t g^rr/E, du[4:6] = -∂H/∂x c t g^rr/(E erg), du[7] = ∂H/∂t t g^rr/E,
+// E = -u[7], k = w erg; rows 1..6 zeroed for r <= 1.01 rNS (:86); H is evaluated at the
+// radius clamped to rNS (:531) while the prefactor's g^rr uses the raw radius (:82).
+// bndry_lyr enters only the ∂t pass (:84-88).
+template <class T>
+__host__ __device__ inline void rhs_photon(const KParams& P, const T* u, const T& tau, double erg, T* du) {
+  const T t = mexp(tau);
+  const T r = u[0];
+  const T E = -u[6];
+  T gtt_u, grr_u;
+  metric_tr(r, P.rs_eff, gtt_u, grr_u);
+  const T rc = (r < P.rNS) ? T(P.rNS) : r;
+  T st, ct, sp, cp;
+  msincos(u[1], st, ct);
+  msincos(u[2] - P.omega * t, sp, cp);  // ψ = φ - ω (time0 + t), time0 = 0 (MainRunner.jl:177)
+  const T ir = 1.0 / rc;
+  const T ir2 = ir * ir;
+  const T iast = 1.0 / mabs(st);
+  const T sgn_st = msign(st);
+  const T kr = u[3] * erg, kt = u[4] * erg, kp = u[5] * erg;
+  const DipoleAng<T> d = dipole_ang(P, st, ct, sp, cp);
+  const T Bn = P.Bn_coef * ir2 * ir;
+  const T sgb = msign(d.b);
+  const T cB = P.wp2_coef * Bn;                 // ∂ωp² = cB sgn(b) ∂b, ωp² ∝ r^-3
+  const T wp2 = cB * mabs(d.b);
+  const T dwp2_r = -3.0 * wp2 * ir;
+  const T dwp2_t = cB * sgb * d.bt;
+  const T dwp2_p = cB * sgb * d.bp;
+  T gtt, grr, dgtt, dgrr;
+  metric_tr_d(rc, P.rs_eff, gtt, grr, dgtt, dgrr);
+  const T gpp = ir2 * iast * iast;
+  const T E2 = E * E;
+  const T iE2 = 1.0 / E2;
+  const T sq = msqrt(grr);
+  // k∥ part (vanishes for isotropic plasma, kpar = 0)
+  T Q = 0.0, Q_r = 0.0, Q_t = 0.0, Q_p = 0.0, Q_kr = 0.0, Q_kt = 0.0, Q_kp = 0.0;
+  if (!P.isotropic) {
+    const T pa = kt * d.a2 + kp * d.a3 * iast;
+    const T p = 2.0 * sq * kr * d.a1 + ir * pa;
+    const T ibeta = 1.0 / (4.0 * d.a1 * d.a1 + d.a2 * d.a2 + d.a3 * d.a3);
+    const T G = grr * p * ibeta * iE2;  // Q = G p
+    Q = G * p;
+    const T p_r = dgrr / sq * kr * d.a1 - ir2 * pa;
+    const T p_t = 2.0 * sq * kr * d.a1t + ir * (kt * d.a1 - kp * d.a3 * sgn_st * ct * iast * iast);
+    const T p_p = 2.0 * sq * kr * d.a1p + ir * (kt * d.a2p + kp * d.a3p * iast);
+    const T beta_t = 8.0 * d.a1 * d.a1t + 2.0 * d.a2 * d.a1;
+    const T beta_p = 8.0 * d.a1 * d.a1p + 2.0 * d.a2 * d.a2p + 2.0 * d.a3 * d.a3p;
+    Q_r = dgrr * p * p * ibeta * iE2 + 2.0 * G * p_r;
+    Q_t = 2.0 * G * p_t - Q * beta_t * ibeta;
+    Q_p = 2.0 * G * p_p - Q * beta_p * ibeta;
+    const T G2 = 2.0 * G;
+    Q_kr = G2 * 2.0 * sq * d.a1;
+    Q_kt = G2 * ir * d.a2;
+    Q_kp = G2 * ir * d.a3 * iast;
+  }
+  const T omQ = 1.0 - Q;
+  const T fac = C_KM * t * grr_u / E;
+  if (r <= P.rNS101) {
+    du[0] = 0.0; du[1] = 0.0; du[2] = 0.0; du[3] = 0.0; du[4] = 0.0; du[5] = 0.0;
+  } else {
+    const T ir3 = ir2 * ir;
+    const T H_r = 0.5 * (dgtt * E2 + dgrr * kr * kr - 2.0 * ir3 * (kt * kt + iast * iast * kp * kp) +
+                         dwp2_r * omQ - wp2 * Q_r);
+    const T H_t = 0.5 * (-2.0 * ct * ir2 * iast * iast / st * kp * kp + dwp2_t * omQ - wp2 * Q_t);
+    const T H_p = 0.5 * (dwp2_p * omQ - wp2 * Q_p);
+    const T fx = -fac / erg;
+    du[0] = (grr * kr - 0.5 * wp2 * Q_kr) * fac;
+    du[1] = (ir2 * kt - 0.5 * wp2 * Q_kt) * fac;
+    du[2] = (gpp * kp - 0.5 * wp2 * Q_kp) * fac;
+    du[3] = H_r * fx;
+    du[4] = H_t * fx;
+    du[5] = H_p * fx;
+  }
+  // ∂H/∂t = -ω ∂H/∂ψ (K is static); with a boundary layer ωp² -> (sqrt(ωp²) + L)²
+  T dwp2_T = -P.omega * dwp2_p;
+  T wp2_T = wp2;
+  if (P.bndry_lyr > 0.0) {
+    const T wgj = msqrt(wp2);
+    const T wtot = wgj + layer_wp(P, rc, P.rmax);
+    wp2_T = wtot * wtot;
+    dwp2_T = dwp2_T * (wtot / wgj);
+  }
+  const T H_T = 0.5 * (dwp2_T * omQ + wp2_T * P.omega * Q_p);
+  du[6] = H_T * t * grr_u / E;
+}
+
+// func_axion! (RayTracer.jl:95-123) with hamiltonian_axion (:632-640): H = K/2 at fixed
+// energy erg, no clamp, no NS cut, du[7] = 0.
+template <class T>
+__host__ __device__ inline void rhs_axion(const KParams& P, const T* u, const T& tau, double erg, T* du) {
+  const T t = mexp(tau);
+  const T r = u[0];
+  T st, ct;
+  msincos(u[1], st, ct);
+  T gtt, grr, dgtt, dgrr;
+  metric_tr_d(r, P.rs_eff, gtt, grr, dgtt, dgrr);
+  const T ir = 1.0 / r;
+  const T ir2 = ir * ir;
+  const T is2 = 1.0 / (st * st);
+  const T kr = u[3] * erg, kt = u[4] * erg, kp = u[5] * erg;
+  const T fac = C_KM * t * grr / erg;
+  const T fx = -fac / erg;
+  du[0] = grr * kr * fac;
+  du[1] = ir2 * kt * fac;
+  du[2] = ir2 * is2 * kp * fac;
+  du[3] = 0.5 * (dgtt * erg * erg + dgrr * kr * kr - 2.0 * ir2 * ir * (kt * kt + is2 * kp * kp)) * fx;
+  du[4] = 0.5 * (-2.0 * ct * ir2 * is2 / st * kp * kp) * fx;
+  du[5] = 0.0;
+  du[6] = 0.0;
+}
+
+template <class T>
+__host__ __device__ inline void rhs(const KParams& P, bool photon, const T* u, const T& tau, double erg, T* du) {
+  if (photon) rhs_photon(P, u, tau, erg, du);
+  else rhs_axion(P, u, tau, erg, du);
+}
+
+// hamiltonian value + all partials at (x, k, T, E) for parity tests (RayTracer.jl:530-556).
+// bndry_lyr is applied in all partials here (unlike func!, which applies it to ∂t only).
+template <class T>
+__host__ __device__ inline void hamiltonian_full(const KParams& P, const T* x, const T* k, const T& Tm, const T& E,
+                                                 T* H, T* dHdx, T* dHdk, T* dHdT) {
+  const T r = x[0];
+  const bool clamped = r < P.rNS;
+  const T rc = clamped ? T(P.rNS) : r;
+  T st, ct, sp, cp;
+  msincos(x[1], st, ct);
+  msincos(x[2] - P.omega * Tm, sp, cp);
+  const T ir = 1.0 / rc, ir2 = ir * ir, iast = 1.0 / mabs(st), sgn_st = msign(st);
+  const DipoleAng<T> d = dipole_ang(P, st, ct, sp, cp);
+  const T Bn = P.Bn_coef * ir2 * ir;
+  const T sgb = msign(d.b);
+  const T cB = P.wp2_coef * Bn;
+  T wp2 = cB * mabs(d.b);
+  T dwp2_r = -3.0 * wp2 * ir, dwp2_t = cB * sgb * d.bt, dwp2_p = cB * sgb * d.bp;
+  if (P.bndry_lyr > 0.0) {
+    const T wgj = msqrt(wp2);
+    const T L = layer_wp(P, rc, P.rmax);
+    const T wt = wgj + L;
+    const T dL_r = L * (-1.5 * ir - 1.0 / (0.1 * P.rmax));
+    const T s = wt / wgj;
+    dwp2_r = dwp2_r * s + 2.0 * wt * dL_r;
+    dwp2_t = dwp2_t * s;
+    dwp2_p = dwp2_p * s;
+    wp2 = wt * wt;
+  }
+  T gtt, grr, dgtt, dgrr;
+  metric_tr_d(rc, P.rs_eff, gtt, grr, dgtt, dgrr);
+  const T gpp = ir2 * iast * iast;
+  const T E2 = E * E, iE2 = 1.0 / E2, sq = msqrt(grr);
+  T Q = 0.0, Q_r = 0.0, Q_t = 0.0, Q_p = 0.0, Q_kr = 0.0, Q_kt = 0.0, Q_kp = 0.0;
+  if (!P.isotropic) {
+    const T pa = k[1] * d.a2 + k[2] * d.a3 * iast;
+    const T p = 2.0 * sq * k[0] * d.a1 + ir * pa;
+    const T ibeta = 1.0 / (4.0 * d.a1 * d.a1 + d.a2 * d.a2 + d.a3 * d.a3);
+    const T G = grr * p * ibeta * iE2;
+    Q = G * p;
+    const T p_r = dgrr / sq * k[0] * d.a1 - ir2 * pa;
+    const T p_t = 2.0 * sq * k[0] * d.a1t + ir * (k[1] * d.a1 - k[2] * d.a3 * sgn_st * ct * iast * iast);
+    const T p_p = 2.0 * sq * k[0] * d.a1p + ir * (k[1] * d.a2p + k[2] * d.a3p * iast);
+    const T beta_t = 8.0 * d.a1 * d.a1t + 2.0 * d.a2 * d.a1;
+    const T beta_p = 8.0 * d.a1 * d.a1p + 2.0 * d.a2 * d.a2p + 2.0 * d.a3 * d.a3p;
+    Q_r = dgrr * p * p * ibeta * iE2 + 2.0 * G * p_r;
+    Q_t = 2.0 * G * p_t - Q * beta_t * ibeta;
+    Q_p = 2.0 * G * p_p - Q * beta_p * ibeta;
+    Q_kr = 4.0 * G * sq * d.a1;
+    Q_kt = 2.0 * G * ir * d.a2;
+    Q_kp = 2.0 * G * ir * d.a3 * iast;
+  }
+  const T omQ = 1.0 - Q;
+  const T K = gtt * E2 + grr * k[0] * k[0] + ir2 * k[1] * k[1] + gpp * k[2] * k[2];
+  *H = 0.5 * (K + wp2 * omQ);
+  const T ir3 = ir2 * ir;
+  const T rmask = clamped ? 0.0 : 1.0;  // the clamp makes r a constant (zero partial)
+  dHdx[0] = rmask * 0.5 * (dgtt * E2 + dgrr * k[0] * k[0] - 2.0 * ir3 * (k[1] * k[1] + iast * iast * k[2] * k[2]) +
+                           dwp2_r * omQ - wp2 * Q_r);
+  dHdx[1] = 0.5 * (-2.0 * ct * ir2 * iast * iast / st * k[2] * k[2] + dwp2_t * omQ - wp2 * Q_t);
+  dHdx[2] = 0.5 * (dwp2_p * omQ - wp2 * Q_p);
+  dHdk[0] = grr * k[0] - 0.5 * wp2 * Q_kr;
+  dHdk[1] = ir2 * k[1] - 0.5 * wp2 * Q_kt;
+  dHdk[2] = gpp * k[2] - 0.5 * wp2 * Q_kp;
+  *dHdT = -P.omega * dHdx[2];
+}
+
+// ---------------------------------------------------------------------------
+// Resonance condition of propagate's ContinuousCallback (RayTracer.jl:254-298,
+// thick_surface = true): rescale w onto the axion mass shell with E = u[7], then
+// H_photon/E² with ωp at t = e^τ (zeroIn = true), k∥ and the raw radius.
+// NaN when |u7| has dropped below m_a (the reference would raise DomainError there).
+template <class T>
+__host__ __device__ inline T condition(const KParams& P, const T* u, const T& tau) {
+  const T t0 = mexp(tau);
+  const T r = u[0];
+  T gtt, grr;
+  metric_tr(r, P.rs_eff, gtt, grr);
+  T st, ct, sp, cp;
+  msincos(u[1], st, ct);
+  const T ir = 1.0 / r;
+  const T ir2 = ir * ir;
+  const T iast = 1.0 / mabs(st);
+  const T gpp = ir2 * iast * iast;
+  const T E2 = u[6] * u[6];
+  const T nrm = (-E2 * gtt - P.mass_a2) / (grr * u[3] * u[3] + ir2 * u[4] * u[4] + gpp * u[5] * u[5]);
+  const T s = msqrt(nrm);
+  const T w0 = u[3] * s, w1 = u[4] * s, w2 = u[5] * s;
+  const T ksqr = gtt * E2 + grr * w0 * w0 + ir2 * w1 * w1 + gpp * w2 * w2;
+  T wp2 = 0.0;
+  T kpar2 = 0.0;
+  if (r > P.rNS || !P.isotropic) {
+    msincos(u[2] - P.omega * t0, sp, cp);
+    const DipoleAng<T> d = dipole_ang(P, st, ct, sp, cp);
+    if (r > P.rNS) {  // zeroIn = true
+      wp2 = P.wp2_coef * P.Bn_coef * ir2 * ir * mabs(d.b);
+      if (P.bndry_lyr > 0.0) {
+        const T w = msqrt(wp2) + layer_wp(P, r, P.rmax);
+        wp2 = w * w;
+      }
+    }
+    if (!P.isotropic) {
+      const T p = 2.0 * msqrt(grr) * w0 * d.a1 + ir * (w1 * d.a2 + w2 * d.a3 * iast);
+      kpar2 = p * p / (4.0 * d.a1 * d.a1 + d.a2 * d.a2 + d.a3 * d.a3);
+    }
+  }
+  return 0.5 * (ksqr + wp2 * (1.0 - grr * kpar2 / E2)) / E2;
+}
+
+// ---------------------------------------------------------------------------
+// Cartesian -> (r, θ, φ) and the covariant "celerity" of k (RayTracer.jl:193-212,
+// k_norm_Cart :656-664, k_sphere :995-1007).
+template <class T>
+__host__ __device__ inline void cart_to_sph(const T* x, T& r, T& th, T& ph) {
+  r = msqrt(x[0] * x[0] + x[1] * x[1] + x[2] * x[2]);
+  th = macos(x[2] / r);
+  ph = matan2(x[1], x[0]);
+}
+
+template <class T>
+__host__ __device__ inline void celerity(const T* x, const T* k, const T& r, const T& st, double rs, T* w) {
+  const T AA = 1.0 - rs / r;
+  const T iAA = 1.0 / AA;
+  const T dr_dt = (x[0] * k[0] + x[1] * k[1] + x[2] * k[2]) / r;
+  w[0] = dr_dt / msqrt(AA) * iAA;
+  w[1] = (x[2] * dr_dt - r * k[2]) / st * iAA;   // v_θ r
+  w[2] = (x[0] * k[1] - x[1] * k[0]) * iAA;      // v_φ r sinθ
+}
+
+// k_norm_Cart (RayTracer.jl:643-685) with ax_fix = true / is_photon = false: rescale k
+// onto the axion mass shell at erg, always with the GR mass (:181-185).
+template <class T>
+__host__ __device__ inline void k_norm_axion_shell(const KParams& P, const T* x, const T* k, double erg, T* out) {
+  T r, th, ph;
+  cart_to_sph(x, r, th, ph);
+  const T st = msin(th);
+  T w[3];
+  celerity(x, k, r, st, P.rs_gr, w);
+  T gtt, grr;
+  metric_tr(r, P.rs_gr, gtt, grr);
+  const T ir2 = 1.0 / (r * r);
+  const T nrm = (-erg * erg * gtt - P.mass_a2) / (grr * w[0] * w[0] + ir2 * w[1] * w[1] + ir2 / (st * st) * w[2] * w[2]);
+  const T f = msqrt(nrm);
+  out[0] = f * k[0];
+  out[1] = f * k[1];
+  out[2] = f * k[2];
+}
+
+// propagate's initial state u0 = [r θ φ | w/erg | erg Δω] (RayTracer.jl:179-216).
+template <class T>
+__host__ __device__ inline void initial_state(const KParams& P, const T* x0, const T* k0, double erg, double dw, T* u) {
+  T kn[3];
+  k_norm_axion_shell(P, x0, k0, erg, kn);
+  T r, th, ph;
+  cart_to_sph(x0, r, th, ph);
+  T w[3];
+  celerity(x0, kn, r, msin(th), P.rs_eff, w);
+  const double ie = 1.0 / erg;
+  u[0] = r; u[1] = th; u[2] = ph;
+  u[3] = w[0] * ie; u[4] = w[1] * ie; u[5] = w[2] * ie;
+  u[6] = T(erg * dw);
+}
+
+// Covariant (w erg) -> Cartesian momentum with ω = 1 - r_s/r (affect! :331-342 and the
+// back-transform :393-416, which scales the mass inside the star :398-406).
+template <class T>
+__host__ __device__ inline void sph_to_cart(const T* u, double erg, const T& rs, T* x, T* k) {
+  T st, ct, sp, cp;
+  msincos(u[1], st, ct);
+  msincos(u[2], sp, cp);
+  const T om = 1.0 - rs / u[0];
+  const T s = erg * om;
+  const T v0 = u[3] * msqrt(om) * s, v1 = u[4] / u[0] * s, v2 = u[5] / (u[0] * st) * s;
+  const T vt = st * v0 + ct * v1;
+  x[0] = u[0] * st * cp;
+  x[1] = u[0] * st * sp;
+  x[2] = u[0] * ct;
+  k[0] = cp * vt - sp * v2;
+  k[1] = sp * vt + cp * v2;
+  k[2] = ct * v0 - st * v1;
+}
+
+// Final state -> Cartesian (RayTracer.jl:393-416); the mass is scaled by (r/rNS)^3 inside.
+template <class T>
+__host__ __device__ inline void back_transform(const KParams& P, const T* u, double erg, T* x, T* k) {
+  T rs = P.rs_eff;
+  if (u[0] < P.rNS) rs = rs * (u[0] * u[0] * u[0]) / (P.rNS * P.rNS * P.rNS);
+  sph_to_cart(u, erg, rs, x, k);
+}
+
+// ---------------------------------------------------------------------------
+// get_Prob_nonAD (MainRunner.jl:67-124) -> conversion_prob (RayTracer.jl:1405-1473),
+// one_D = false, melrose = true. Per-crossing ("local") quantities first; the group-level
+// linear-indexed values (ksphere[1..3], Bsphere[1..3], x0_pl[1..2], :1432-1443, :510-511)
+// come in separately so groups of Nc > 1 crossings reproduce the reference exactly.
+template <class T>
+struct ProbLocal {
+  T r, th, ph, st, ct;
+  T grr, gthth, gpp;     // GR metric (global Mass_NS, MainRunner.jl:75)
+  T B[3];                // Bsphere (GJ_Model_Sphereical, flat honoured)
+  T ks[3];               // k_sphere (flat honoured)
+  T Bmag, kmag, cth, sth;
+  T ergax, wp;
+};
+
+template <class T>
+__host__ __device__ inline ProbLocal<T> prob_local(const KParams& P, const T* pos, const T* kpos, const T& erg_eff) {
+  ProbLocal<T> L;
+  cart_to_sph(pos, L.r, L.th, L.ph);
+  msincos(L.th, L.st, L.ct);
+  T gtt;
+  metric_tr(L.r, P.rs_gr, gtt, L.grr);
+  const T ir = 1.0 / L.r;
+  L.gthth = ir * ir;
+  L.gpp = L.gthth / (L.st * L.st);
+  T sp, cp;
+  msincos(L.ph, sp, cp);  // t_start = 0
+  const DipoleAng<T> d = dipole_ang(P, L.st, L.ct, sp, cp);
+  const T Bn = P.Bn_coef * ir * ir * ir;
+  T gtt_f, grr_f;
+  metric_tr(L.r, P.rs_eff, gtt_f, grr_f);
+  L.B[0] = 2.0 * Bn * d.a1 / msqrt(grr_f);
+  L.B[1] = Bn * d.a2 * L.r;
+  L.B[2] = Bn * d.a3 * L.r * mabs(L.st);
+  celerity(pos, kpos, L.r, L.st, P.rs_eff, L.ks);
+  const T BB = L.grr * L.B[0] * L.B[0] + L.gthth * L.B[1] * L.B[1] + L.gpp * L.B[2] * L.B[2];
+  const T kk = L.grr * L.ks[0] * L.ks[0] + L.gthth * L.ks[1] * L.ks[1] + L.gpp * L.ks[2] * L.ks[2];
+  const T Bk = L.grr * L.B[0] * L.ks[0] + L.gthth * L.B[1] * L.ks[1] + L.gpp * L.B[2] * L.ks[2];
+  L.Bmag = msqrt(BB) * 1.95e-2;
+  L.kmag = msqrt(kk);
+  L.cth = Bk * 1.95e-2 / (L.kmag * L.Bmag);
+  L.sth = msqrt(1.0 - L.cth * L.cth);  // sin(acos(c))
+  if (P.isotropic) {
+    L.cth = 0.0;
+    L.sth = 1.0;
+  }
+  L.ergax = erg_eff / msqrt(1.0 - 2.0 * P.GM_c2 / L.r);
+  L.wp = 0.0;
+  if (L.r > P.rNS) {  // zeroIn = true
+    L.wp = msqrt(P.wp2_coef * Bn * mabs(d.b));
+    if (P.bndry_lyr > 0.0) L.wp = L.wp + layer_wp(P, L.r, P.rmax_def);
+  }
+  return L;
+}
+
+// Group-level values: linear index q of a column-major m x 3 matrix -> row q % m, col q / m.
+template <class T>
+struct ProbLin {
+  T k1, k2, k3, B1, B2, B3;  // ksphere[1..3], Bsphere[1..3]
+  T r_c, th_c;               // x0_pl[1], x0_pl[2] (Cristoffel's r, theta)
+};
+
+template <class T>
+__host__ __device__ inline T prob_eval(const KParams& P, double g_agg, const ProbLocal<T>& L, const ProbLin<T>& G) {
+  const T wE = L.ergax;
+  const T wE2 = wE * wE;
+  const T vloc = msqrt(wE2 - P.mass_a2) / wE;
+  T st, ct, sp, cp;
+  msincos(L.th, st, ct);
+  msincos(L.ph, sp, cp);
+  const T ir = 1.0 / L.r, ir2 = ir * ir;
+  const T iast = 1.0 / mabs(st), sgn_st = msign(st);
+  const DipoleAng<T> d = dipole_ang(P, st, ct, sp, cp);
+  const T Bn = P.Bn_coef * ir2 * ir;
+  T dmu_E[3];
+  if (P.isotropic) {
+    // grad_x sqrt(kmag² + ωp²), omega_function defaults zeroIn=false, bndry_lyr=-1 (:1421)
+    const T wp2 = P.wp2_coef * Bn * mabs(d.b);
+    const T cB = 0.5 * P.wp2_coef * Bn * msign(d.b);
+    const T inv = 1.0 / msqrt(L.kmag * L.kmag + wp2);
+    dmu_E[0] = -1.5 * wp2 * ir * inv;
+    dmu_E[1] = cB * d.bt * inv;
+    dmu_E[2] = cB * d.bp * inv;
+  } else {
+    // ∇ωp (zeroIn = true, bndry_lyr, Mass_a = m_a; :1427)
+    T dwp[3] = {0.0, 0.0, 0.0};
+    if (L.r > P.rNS) {
+      const T wgj = msqrt(P.wp2_coef * Bn * mabs(d.b));
+      const T c = P.wp2_coef * Bn * msign(d.b) / (2.0 * wgj);
+      dwp[0] = -1.5 * wgj * ir;
+      dwp[1] = c * d.bt;
+      dwp[2] = c * d.bp;
+      if (P.bndry_lyr > 0.0) {
+        const T Ly = layer_wp(P, L.r, P.rmax);
+        dwp[0] = dwp[0] + Ly * (-1.5 * ir - 1.0 / (0.1 * P.rmax));
+      }
+    }
+    // ∇(|B| 1.95e-2) (return_comp = 0, :1429)
+    const T beta = 4.0 * d.a1 * d.a1 + d.a2 * d.a2 + d.a3 * d.a3;
+    const T sb = msqrt(beta);
+    const T beta_t = 8.0 * d.a1 * d.a1t + 2.0 * d.a2 * d.a1;
+    const T beta_p = 8.0 * d.a1 * d.a1p + 2.0 * d.a2 * d.a2p + 2.0 * d.a3 * d.a3p;
+    const T f = 1.95e-2 * Bn;
+    const T dB[3] = {-3.0 * f * sb * ir, f * beta_t / (2.0 * sb), f * beta_p / (2.0 * sb)};
+    // ∇ of B^r √g^rr, B^θ/r, B^φ/(r|sinθ|) times 1.95e-2 (return_comp 1..3, :1432)
+    T gtt_f, grr_f, dgtt_f, dgrr_f;
+    metric_tr_d(L.r, P.rs_eff, gtt_f, grr_f, dgtt_f, dgrr_f);
+    const T sgf = msqrt(grr_f);
+    const T dc1[3] = {2.0 * f * d.a1 * (-3.0 * ir * sgf + 0.5 * dgrr_f / sgf), 2.0 * f * d.a1t * sgf,
+                      2.0 * f * d.a1p * sgf};
+    const T dc2[3] = {-4.0 * f * d.a2 * ir2, f * d.a1 * ir, f * d.a2p * ir};
+    const T dc3[3] = {-4.0 * f * d.a3 * ir2 * iast, -f * d.a3 * ir * sgn_st * ct * iast * iast, f * d.a3p * ir * iast};
+    // Christoffel symbols at (x0_pl[1], x0_pl[2]) with the GR mass (:503-527)
+    const T GM = P.GM_c2;
+    T stc, ctc;
+    msincos(G.th_c, stc, ctc);
+    const T G_rrr = -GM / (G.r_c * (G.r_c - 2.0 * GM));
+    const T G_rtt = -(G.r_c - 2.0 * GM);
+    const T G_rpp = -(G.r_c - 2.0 * GM) * stc * stc;
+    const T G_trt = 1.0 / G.r_c;
+    const T G_tpp = -stc * ctc;
+    const T G_ptp = ctc / stc;
+    const T s = 1.95e-2;
+    const T t2r = G.k1 * (L.grr * G.B1 * s) * G_rrr + G.k2 * G_trt * (G.B2 * L.gthth * s) +
+                  G.k3 * G_trt * (G.B3 * L.gpp * s);
+    const T t2t = G.k1 * (L.gthth * G.B2 * s) * G_rtt + G.k3 * G_ptp * (G.B3 * L.gpp * s) +
+                  G.k2 * (L.grr * G.B1 * s) * G_trt;
+    const T t2p = G.k1 * (L.gpp * G.B3 * s) * G_rpp + G.k2 * G_tpp * (G.B3 * L.gpp * s) +
+                  G.k3 * G_trt * (G.B1 * L.grr * s) + G.k3 * G_ptp * (G.B2 * L.gthth * s);
+    const T t2[3] = {t2r, t2t, t2p};
+    const T ikB = 1.0 / (L.kmag * L.Bmag);
+    const T wp = L.wp;
+    const T wp2 = wp * wp;
+    const T preF = wp / mabs(wE2 * wE2 * wE + L.cth * L.cth * wE * (wp2 * wp2 - 2.0 * wp2 * wE2));
+    const T A1 = wE2 * wE2 * L.sth * L.sth;
+    const T A2 = wE2 * L.cth * wp * (wE2 - wp2);
+    for (int c = 0; c < 3; ++c) {
+      const T term1 = G.k1 * dc1[c] + G.k2 * dc2[c] + G.k3 * dc3[c];
+      const T dct = (term1 + t2[c]) * ikB - L.cth * dB[c] / L.Bmag;
+      dmu_E[c] = preF * (A1 * dwp[c] - A2 * dct);
+    }
+  }
+  const T ik = 1.0 / L.kmag;
+  const T vhat = L.grr * L.ks[0] * ik * dmu_E[0] + L.gthth * L.ks[1] * ik * dmu_E[1] + L.gpp * L.ks[2] * ik * dmu_E[2];
+  const T wp2 = L.wp * L.wp;
+  const T pref = wE2 * wE2 * L.sth * L.sth / (L.cth * L.cth * wp2 * (wp2 - 2.0 * wE2) + wE2 * wE2);
+  const T gB = g_agg * 1e-9 * L.Bmag;
+  return PI / 2.0 * pref * gB * gB / (mabs(vhat) * vloc * C_KM * HBAR);
+}
+
+// Nc = 1: the group values are the crossing's own (forward trees, MainRunner.jl:265).
+template <class T>
+__host__ __device__ inline T prob_nonad_single(const KParams& P, const T* pos, const T* kpos, const T& erg_eff) {
+  const ProbLocal<T> L = prob_local(P, pos, kpos, erg_eff);
+  ProbLin<T> G;
+  G.k1 = L.ks[0]; G.k2 = L.ks[1]; G.k3 = L.ks[2];
+  G.B1 = L.B[0]; G.B2 = L.B[1]; G.B3 = L.B[2];
+  G.r_c = L.r; G.th_c = L.th;
+  return prob_eval(P, P.g_agg, L, G);
+}
+
+// ---------------------------------------------------------------------------
+// Sampler condition (find_samples_new :1547-1583, thick_surface = true) at the Cartesian
+// line point x with local velocity direction vl. sinθ, cosθ, sinφ, cosφ are taken
+// algebraically from x instead of through acos/atan2 + sin/cos (identical values up to
+// rounding); the metric always uses the GR mass (the sampler gets no `flat`).
+template <class T>
+__host__ __device__ inline T sampler_condition(const KParams& P, const T* x, const T* vl, double E) {
+  const T rho2 = x[0] * x[0] + x[1] * x[1];
+  const T r = msqrt(rho2 + x[2] * x[2]);
+  const T ir = 1.0 / r;
+  const T rho = msqrt(rho2);
+  const T st = rho * ir, ct = x[2] * ir;
+  const T irho = 1.0 / rho;
+  const T cp = x[0] * irho, sp = x[1] * irho;  // ψ = φ at t0 = 0
+  T AA = 1.0 - P.rs_gr * ir;
+  if (r < P.rNS) AA = 1.0;
+  const T iAA = 1.0 / AA;
+  const T dr_dt = (x[0] * vl[0] + x[1] * vl[1] + x[2] * vl[2]) * ir;
+  T w0 = dr_dt / msqrt(AA) * iAA;
+  T w1 = (x[2] * dr_dt - r * vl[2]) / st * iAA;
+  T w2 = (x[0] * vl[1] - x[1] * vl[0]) * iAA;
+  T gtt, grr;
+  metric_tr(r, P.rs_gr, gtt, grr);
+  const T ir2 = ir * ir;
+  const T gpp = ir2 / (st * st);
+  const double E2 = E * E;
+  const T nrm = (-E2 * gtt - P.mass_a2) / (grr * w0 * w0 + ir2 * w1 * w1 + gpp * w2 * w2);
+  const T f = msqrt(nrm);
+  w0 = w0 * f; w1 = w1 * f; w2 = w2 * f;
+  const DipoleAng<T> d = dipole_ang(P, st, ct, sp, cp);
+  T wp2 = P.wp2_coef * P.Bn_coef * ir2 * ir * mabs(d.b);  // GJ_Model_ωp_vec: no zeroIn
+  if (P.bndry_lyr > 0.0 && r >= P.rNS) {
+    const T w = msqrt(wp2) + layer_wp(P, r, P.rmax);
+    wp2 = w * w;
+  }
+  T kpar2 = 0.0;
+  if (!P.isotropic) {
+    const T p = 2.0 * msqrt(grr) * w0 * d.a1 + ir * (w1 * d.a2 + w2 * d.a3 / mabs(st));
+    kpar2 = p * p / (4.0 * d.a1 * d.a1 + d.a2 * d.a2 + d.a3 * d.a3);
+  }
+  const T ksqr = gtt * E2 + grr * w0 * w0 + ir2 * w1 * w1 + gpp * w2 * w2;
+  return 0.5 * (ksqr + wp2 * (1.0 - grr * kpar2 / E2)) / E2;
+}
+
+// ωp from GJ_Model_ωp_vec (no zeroIn) at Cartesian x, t = 0 (sampler affect!, :1587)
+template <class T>
+__host__ __device__ inline T wp_cart(const KParams& P, const T* x) {
+  const T rho2 = x[0] * x[0] + x[1] * x[1];
+  const T r = msqrt(rho2 + x[2] * x[2]);
+  const T ir = 1.0 / r;
+  const T rho = msqrt(rho2);
+  const T irho = 1.0 / rho;
+  const DipoleAng<T> d = dipole_ang(P, rho * ir, x[2] * ir, x[1] * irho, x[0] * irho);
+  T wp = msqrt(P.wp2_coef * P.Bn_coef * ir * ir * ir * mabs(d.b));
+  if (P.bndry_lyr > 0.0 && r >= P.rNS) wp = wp + layer_wp(P, r, P.rmax);
+  return wp;
+}
+
+// ---------------------------------------------------------------------------
+// Verner 6(5) "most efficient" pair as used by OrdinaryDiffEq's Vern6 (FSAL: b = A[8,:]).
+// Order conditions verified in tests/test_tableau.py.
+struct Vern6 {
+  static constexpr double c2 = 0.06, c3 = 0.09593333333333333, c4 = 0.1439, c5 = 0.4973, c6 = 0.9725,
+                          c7 = 0.9995;
+  static constexpr double a21 = 0.06;
+  static constexpr double a31 = 0.019239962962962962, a32 = 0.07669337037037037;
+  static constexpr double a41 = 0.035975, a43 = 0.107925;
+  static constexpr double a51 = 1.3186834152331484, a53 = -5.042058063628562, a54 = 4.220674648395414;
+  static constexpr double a61 = -41.872591664327516, a63 = 159.4325621631375, a64 = -122.11921356501003,
+                          a65 = 5.531743066200053;
+  static constexpr double a71 = -54.430156935316504, a73 = 207.06725136501848, a74 = -158.61081378459,
+                          a75 = 6.991816585950242, a76 = -0.018597231062309313;
+  static constexpr double a81 = -54.66374178728198, a83 = 207.95280625538937, a84 = -159.2889574744995,
+                          a85 = 7.018743740796944, a86 = -0.018338785905045722, a87 = -0.0005119484997882099;
+  static constexpr double a91 = 0.03438957868357036, a94 = 0.2582624555633503, a95 = 0.4209371189673537,
+                          a96 = 4.40539646966931, a97 = -176.48311902429865, a98 = 172.36413340141507;
+  static constexpr double bh1 = 0.04909967648382489, bh4 = 0.2251112229516524, bh5 = 0.4694682253029562,
+                          bh6 = 0.8065792249988868, bh8 = -0.6071194891777959, bh9 = 0.05686113944047569;
+  // btilde = b - bhat (error weights)
+  static constexpr double e1 = a91 - bh1, e4 = a94 - bh4, e5 = a95 - bh5, e6 = a96 - bh6, e7 = a97, e8 = a98 - bh8,
+                          e9 = -bh9;
+};
+
+// ---------------------------------------------------------------------------
+// Philox4x32-10 (Salmon et al. 2011): counter-based stream keyed by (seed, ray id), so
+// every initial condition is independent of batch split and GPU count.
+__host__ __device__ inline void philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint64_t p0 = uint64_t(0xD2511F53u) * c[0];
+    const uint64_t p1 = uint64_t(0xCD9E8D57u) * c[2];
+    const uint32_t n0 = uint32_t(p1 >> 32) ^ c[1] ^ k0;
+    const uint32_t n2 = uint32_t(p0 >> 32) ^ c[3] ^ k1;
+    c[0] = n0;
+    c[1] = uint32_t(p1);
+    c[2] = n2;
+    c[3] = uint32_t(p0);
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+}
+
+__host__ __device__ inline double u01(uint32_t a, uint32_t b) {
+  return (double(a >> 5) * 67108864.0 + double(b >> 6)) * (1.0 / 9007199254740992.0);
+}
+
+// The 10 uniforms of one find_samples_new attempt, in the reference's draw order:
+// θi, ϕi, θi_loc, ϕi_loc, ϕRND, rRND (:1486-1497), vIfty x3 (:1531), randInx (:1623).
+__host__ __device__ inline void attempt_uniforms(uint64_t seed, uint64_t ray, uint32_t attempt, double* U) {
+#pragma unroll
+  for (uint32_t blk = 0; blk < 5; ++blk) {
+    uint32_t c[4] = {uint32_t(ray), uint32_t(ray >> 32), attempt, blk};
+    philox4x32_10(c, uint32_t(seed), uint32_t(seed >> 32));
+    U[2 * blk] = u01(c[0], c[1]);
+    U[2 * blk + 1] = u01(c[2], c[3]);
+  }
+}
+
+}  // namespace art

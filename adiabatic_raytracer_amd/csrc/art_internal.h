@@ -1,0 +1,40 @@
+// art_internal.h -- launch wrappers shared by art_kernels.hip and art_capi.cpp.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "art_core.h"
+
+namespace art {
+// Segment inputs / outputs (device pointers, SoA), see art_segment_out / art_crossing_buf.
+struct SegIn {
+  const double *x0, *k0, *erg, *dw, *lnt0;
+  const int8_t* species;
+};
+
+struct SegOut {
+  double *x_end, *k_end, *u7_end, *tau_end;
+  int32_t *status, *n_acc, *n_rej;
+  int32_t cap;
+  int32_t* xcount;
+  double *xpos, *xk, *xt, *xdw, *xp;
+};
+constexpr int N_STATS = 8;  // propagate statistics: attempts, accepted, root re-steps, scan evals,
+                            // interpolant-root evals, rays, init RHS, (reserved)
+int persistent_blocks(const void* func, int64_t work);
+hipError_t launch_propagate(const KParams& P, int64_t n, const SegIn& in, const SegOut& out, int32_t max_crossings,
+                            unsigned long long* queue, unsigned long long* stats, hipStream_t s, int* grid_out);
+hipError_t launch_sample(const KParams& P, double maxR, uint64_t seed, int64_t ray_offset, int64_t n, double* x,
+                         double* k, double* erg, double* vifty, int32_t* w, int32_t* att, unsigned long long* queue,
+                         hipStream_t s);
+hipError_t launch_prob(const KParams& P, int64_t nc, const double* pos, const double* kpos, const double* erg,
+                       int64_t n_groups, const int64_t* gstart, double* out, hipStream_t s);
+hipError_t launch_flux(const KParams& P, int64_t n, const double* x_end, const double* k_end, const int32_t* status,
+                       const int8_t* species, const double* w, int32_t nbins, double* hist, hipStream_t s);
+hipError_t launch_eval_rhs(const KParams& P, int64_t n, const double* u, const double* tau, const double* erg,
+                           const int8_t* species, double* du, hipStream_t s);
+hipError_t launch_eval_hamiltonian(const KParams& P, int64_t n, const double* x, const double* k, const double* T,
+                                   const double* E, double* H, double* dHdx, double* dHdk, double* dHdT,
+                                   hipStream_t s);
+hipError_t launch_eval_condition(const KParams& P, int64_t n, const double* u, const double* tau, double* out,
+                                 hipStream_t s);
+}  // namespace art

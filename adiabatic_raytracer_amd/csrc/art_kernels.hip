@@ -1,0 +1,987 @@
+// art_kernels.hip -- gfx950 kernels for the ray-tracing hot path.
+//
+// propagate_kernel: RT.propagate (RayTracer.jl:171-452) for a batch of segments.
+//   * one wavefront lane per ray; the 7-D state u = [r θ φ | w | u7] and its FSAL
+//     derivative live in VGPRs; NS parameters are kernel arguments (SGPRs);
+//   * persistent lanes with a wave-aggregated work queue: a lane whose segment ends pulls
+//     the next ray id from a 64-ray chunk the wave claimed with ONE global atomicAdd, so
+//     short and long segments (12 vs 5000 steps) never idle a wave;
+//   * every loop iteration is ONE integrator step attempt for every live lane: ordinary
+//     adaptive steps, and the re-steps that polish a resonance root on the true
+//     trajectory (mode ROOT), run the same unrolled stage code in lockstep;
+//   * HBM is touched only to load a segment's initial conditions and to store its end
+//     state and its crossings (Σ ≈ 220 B per segment).
+#include <hip/hip_runtime.h>
+
+#include "art_core.h"
+#include "art_internal.h"
+
+namespace art {
+
+
+// stats[]: totals over the launch, for the roofline accounting (tools/count_flops.cpp)
+enum { ST_ATTEMPTS = 0, ST_ACCEPTED, ST_ROOT_STEPS, ST_SCAN_EVALS, ST_INTERP_EVALS, ST_RAYS, ST_INIT_RHS, ST_NSTATS = 8 };
+
+constexpr int CHUNK = 64;
+
+// ---------------------------------------------------------------------------
+// One Verner 6(5) attempt from (u, k1 = f(u)) over h: writes u_{n+1}, its FSAL derivative
+// k9 and returns the RMS error norm of OrdinaryDiffEq (abstol + max(|u|,|u_new|) reltol).
+template <class T>
+__host__ __device__ inline T vern6_attempt(const KParams& P, bool photon, double erg, const T* u, const T* k1,
+                                           const T& tau, const T& h, T* un, T* k9) {
+  using V = Vern6;
+  T k2[7], k3[7], k4[7], k5[7], k6[7], k7[7], k8[7], y[7];
+#pragma unroll
+  for (int i = 0; i < 7; ++i) y[i] = u[i] + h * (V::a21 * k1[i]);
+  rhs(P, photon, y, tau + V::c2 * h, erg, k2);
+#pragma unroll
+  for (int i = 0; i < 7; ++i) y[i] = u[i] + h * (V::a31 * k1[i] + V::a32 * k2[i]);
+  rhs(P, photon, y, tau + V::c3 * h, erg, k3);
+#pragma unroll
+  for (int i = 0; i < 7; ++i) y[i] = u[i] + h * (V::a41 * k1[i] + V::a43 * k3[i]);
+  rhs(P, photon, y, tau + V::c4 * h, erg, k4);
+#pragma unroll
+  for (int i = 0; i < 7; ++i) y[i] = u[i] + h * (V::a51 * k1[i] + V::a53 * k3[i] + V::a54 * k4[i]);
+  rhs(P, photon, y, tau + V::c5 * h, erg, k5);
+#pragma unroll
+  for (int i = 0; i < 7; ++i)
+    y[i] = u[i] + h * (V::a61 * k1[i] + V::a63 * k3[i] + V::a64 * k4[i] + V::a65 * k5[i]);
+  rhs(P, photon, y, tau + V::c6 * h, erg, k6);
+#pragma unroll
+  for (int i = 0; i < 7; ++i)
+    y[i] = u[i] + h * (V::a71 * k1[i] + V::a73 * k3[i] + V::a74 * k4[i] + V::a75 * k5[i] + V::a76 * k6[i]);
+  rhs(P, photon, y, tau + V::c7 * h, erg, k7);
+#pragma unroll
+  for (int i = 0; i < 7; ++i)
+    y[i] = u[i] + h * (V::a81 * k1[i] + V::a83 * k3[i] + V::a84 * k4[i] + V::a85 * k5[i] + V::a86 * k6[i] +
+                       V::a87 * k7[i]);
+  rhs(P, photon, y, tau + h, erg, k8);
+#pragma unroll
+  for (int i = 0; i < 7; ++i)
+    un[i] = u[i] + h * (V::a91 * k1[i] + V::a94 * k4[i] + V::a95 * k5[i] + V::a96 * k6[i] + V::a97 * k7[i] +
+                        V::a98 * k8[i]);
+  rhs(P, photon, un, tau + h, erg, k9);
+  if (photon && un[0] < P.rNS) un[0] = P.rNS;  // hamiltonian's in-place clamp on the FSAL stage (:531)
+  T acc = 0.0;
+#pragma unroll
+  for (int i = 0; i < 7; ++i) {
+    const T e = h * (V::e1 * k1[i] + V::e4 * k4[i] + V::e5 * k5[i] + V::e6 * k6[i] + V::e7 * k7[i] + V::e8 * k8[i] +
+                     V::e9 * k9[i]);
+    const T au = mabs(u[i]), an = mabs(un[i]);
+    const T sc = P.abstol + (au > an ? au : an) * P.reltol;
+    const T q = e / sc;
+    acc = acc + q * q;
+  }
+  return msqrt(acc * (1.0 / 7.0));
+}
+
+// Classical RK4 over h; k_next = f(u_{n+1}) doubles as the next step's k1.
+template <class T>
+__host__ __device__ inline void rk4_attempt(const KParams& P, bool photon, double erg, const T* u, const T* k1,
+                                            const T& tau, const T& h, T* un, T* kn) {
+  T k2[7], k3[7], k4[7], y[7];
+  const T h2 = 0.5 * h;
+#pragma unroll
+  for (int i = 0; i < 7; ++i) y[i] = u[i] + h2 * k1[i];
+  rhs(P, photon, y, tau + h2, erg, k2);
+#pragma unroll
+  for (int i = 0; i < 7; ++i) y[i] = u[i] + h2 * k2[i];
+  rhs(P, photon, y, tau + h2, erg, k3);
+#pragma unroll
+  for (int i = 0; i < 7; ++i) y[i] = u[i] + h * k3[i];
+  rhs(P, photon, y, tau + h, erg, k4);
+#pragma unroll
+  for (int i = 0; i < 7; ++i) un[i] = u[i] + h / 6.0 * (k1[i] + 2.0 * k2[i] + 2.0 * k3[i] + k4[i]);
+  rhs(P, photon, un, tau + h, erg, kn);
+  if (photon && un[0] < P.rNS) un[0] = P.rNS;
+}
+
+// cubic Hermite dense output between (u0, f0) and (u1, f1) over h at fraction th
+template <class T>
+__host__ __device__ inline void hermite7(const T* u0, const T* f0, const T* u1, const T* f1, const T& h,
+                                         const T& th, T* out) {
+  const T a = 1.0 - th;
+  const T b = th * (th - 1.0);
+  const T c1 = 1.0 - 2.0 * th;
+  const T c2 = (th - 1.0) * h;
+  const T c3 = th * h;
+#pragma unroll
+  for (int i = 0; i < 7; ++i) out[i] = a * u0[i] + th * u1[i] + b * (c1 * (u1[i] - u0[i]) + c2 * f0[i] + c3 * f1[i]);
+}
+
+__device__ inline int sgn(double x) { return (x > 0.0) - (x < 0.0); }
+
+// ode_determine_initdt (DiffEqBase) for an order-6 method; one extra RHS evaluation.
+__device__ inline double initdt(const KParams& P, bool photon, double erg, const double* u0, const double* f0,
+                                double tau0, double dtmax) {
+  double d0 = 0.0, d1 = 0.0, sk[7];
+#pragma unroll
+  for (int i = 0; i < 7; ++i) {
+    sk[i] = P.abstol + fabs(u0[i]) * P.reltol;
+    d0 += (u0[i] / sk[i]) * (u0[i] / sk[i]);
+    d1 += (f0[i] / sk[i]) * (f0[i] / sk[i]);
+  }
+  d0 = sqrt(d0 / 7.0);
+  d1 = sqrt(d1 / 7.0);
+  double dt0 = (d0 < 1e-5 || d1 < 1e-5) ? 1e-6 : 0.01 * (d0 / d1);
+  dt0 = fmin(dt0, dtmax);
+  const double at = fabs(tau0);
+  const double eps_t = nextafter(at, INFINITY) - at;
+  if (dt0 < 10.0 * eps_t) return fmax(1e-6, P.dtmin);
+  double u1[7], f1[7];
+#pragma unroll
+  for (int i = 0; i < 7; ++i) u1[i] = u0[i] + dt0 * f0[i];
+  rhs(P, photon, u1, tau0 + dt0, erg, f1);
+  bool same = true;
+  double d2 = 0.0;
+#pragma unroll
+  for (int i = 0; i < 7; ++i) {
+    same = same && (f0[i] == f1[i]);
+    const double q = (f1[i] - f0[i]) / sk[i];
+    d2 += q * q;
+  }
+  if (same) return fmax(P.dtmin, 100.0 * dt0);
+  d2 = sqrt(d2 / 7.0) / dt0;
+  const double mx = fmax(d1, d2);
+  const double dt1 = (mx <= 1e-15) ? fmax(1e-6, dt0 * 1e-3) : pow(10.0, -(2.0 + log10(mx)) / 6.0);
+  return fmax(P.dtmin, fmin(fmin(100.0 * dt0, dt1), dtmax));
+}
+
+// Root of the condition along the Hermite interpolant inside (tha, thb] (Illinois).
+__device__ inline double illinois_interp(const KParams& P, const double* u0, const double* f0, const double* u1,
+                                         const double* f1, double tau, double h, double tha, double thb, double ca,
+                                         double cb, int& nevals) {
+  double tr = tha - ca * (thb - tha) / (cb - ca);
+  int side = 0;
+  for (int it = 0; it < 40; ++it) {
+    double ui[7];
+    hermite7(u0, f0, u1, f1, h, tr, ui);
+    const double cr = condition(P, ui, tau + tr * h);
+    ++nevals;
+    if (cr == 0.0 || isnan(cr) || (thb - tha) < 1e-12) break;
+    if (sgn(cr) == sgn(ca)) {
+      tha = tr; ca = cr;
+      if (side == -1) cb *= 0.5;
+      side = -1;
+    } else {
+      thb = tr; cb = cr;
+      if (side == 1) ca *= 0.5;
+      side = 1;
+    }
+    const double tn = tha - ca * (thb - tha) / (cb - ca);
+    if (tn == tr) break;
+    tr = tn;
+  }
+  return tr;
+}
+
+// ---------------------------------------------------------------------------
+// affect! (RayTracer.jl:301-350). Returns 0 = skipped, 1 = recorded, 2 = recorded + terminate.
+__device__ inline int affect(const KParams& P, const SegIn& in, const SegOut& out, int64_t n, int64_t ray,
+                             const double* u, double tau, double erg, int& ncross, int max_crossings) {
+  double st, ct, sp, cp;
+  sincos(u[1], &st, &ct);
+  sincos(u[2], &sp, &cp);
+  if (ncross == 0) {  // a "crossing" at the start point is not new (:303-314)
+    const double s = 1.0001;
+    const double pos[3] = {st * cp * u[0], st * sp * u[0], ct * u[0]};
+    bool all_lt = true, all_gt = true;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const double x0i = fabs(in.x0[i * n + ray]);
+      all_lt = all_lt && (fabs(pos[i]) < x0i * s);
+      all_gt = all_gt && (fabs(pos[i]) > x0i / s);
+    }
+    if (all_lt && all_gt) return 0;
+  }
+  double x[3], k[3];
+  sph_to_cart(u, erg, P.rs_eff, x, k);
+  if (sqrt(x[0] * x[0] + x[1] * x[1] + x[2] * x[2]) < P.rNS101) return 0;  // :322-324
+  const int j = ncross;
+  if (out.xcount && j < out.cap) {
+    const double dwc = u[6] / erg;
+    const double eeff = erg * fabs(dwc);  // get_tree: erg_inf_ini .* abs.(Δωc) (MainRunner.jl:265)
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      out.xpos[(int64_t(c) * out.cap + j) * n + ray] = x[c];
+      out.xk[(int64_t(c) * out.cap + j) * n + ray] = k[c];
+    }
+    out.xt[int64_t(j) * n + ray] = exp(tau);
+    out.xdw[int64_t(j) * n + ray] = dwc;
+    out.xp[int64_t(j) * n + ray] = prob_nonad_single(P, x, k, eeff);
+  }
+  ncross = j + 1;
+  const int maxc = max_crossings <= 0 ? -1 : max_crossings;
+  return (ncross >= maxc) ? 2 : 1;
+}
+
+// ---------------------------------------------------------------------------
+// Stage glue of the slot loop. Slot s (1..8) of a Vern6 attempt evaluates k_{s+1} at
+// y = u + h Σ_j a_{s+1,j} k_j; k2 and k8 share one register set (kA) because k2 is dead
+// before k8 is born. Slot 8's input is u_{n+1} itself (FSAL: b = A[9,:]).
+template <int INTEG>
+__device__ inline void stage_input(int s, const double* u, const double* f, const double* kA, const double* k3,
+                                   const double* k4, const double* k5, const double* k6, const double* k7, double h,
+                                   double tau, double* y, double& ty) {
+  using V = Vern6;
+  if (INTEG == ART_RK4) {
+    // classical RK4: slots 1..3 give k2..k4, slot 4 gives f(u_{n+1}); kA = k2, k3 = k3, k4 = k4
+    switch (s) {
+      case 1:
+#pragma unroll
+        for (int i = 0; i < 7; ++i) y[i] = u[i] + 0.5 * h * f[i];
+        ty = tau + 0.5 * h;
+        break;
+      case 2:
+#pragma unroll
+        for (int i = 0; i < 7; ++i) y[i] = u[i] + 0.5 * h * kA[i];
+        ty = tau + 0.5 * h;
+        break;
+      case 3:
+#pragma unroll
+        for (int i = 0; i < 7; ++i) y[i] = u[i] + h * k3[i];
+        ty = tau + h;
+        break;
+      default:
+#pragma unroll
+        for (int i = 0; i < 7; ++i) y[i] = u[i] + h / 6.0 * (f[i] + 2.0 * kA[i] + 2.0 * k3[i] + k4[i]);
+        ty = tau + h;
+        break;
+    }
+    return;
+  }
+  switch (s) {
+    case 1:
+#pragma unroll
+      for (int i = 0; i < 7; ++i) y[i] = u[i] + h * (V::a21 * f[i]);
+      ty = tau + V::c2 * h;
+      break;
+    case 2:
+#pragma unroll
+      for (int i = 0; i < 7; ++i) y[i] = u[i] + h * (V::a31 * f[i] + V::a32 * kA[i]);
+      ty = tau + V::c3 * h;
+      break;
+    case 3:
+#pragma unroll
+      for (int i = 0; i < 7; ++i) y[i] = u[i] + h * (V::a41 * f[i] + V::a43 * k3[i]);
+      ty = tau + V::c4 * h;
+      break;
+    case 4:
+#pragma unroll
+      for (int i = 0; i < 7; ++i) y[i] = u[i] + h * (V::a51 * f[i] + V::a53 * k3[i] + V::a54 * k4[i]);
+      ty = tau + V::c5 * h;
+      break;
+    case 5:
+#pragma unroll
+      for (int i = 0; i < 7; ++i) y[i] = u[i] + h * (V::a61 * f[i] + V::a63 * k3[i] + V::a64 * k4[i] + V::a65 * k5[i]);
+      ty = tau + V::c6 * h;
+      break;
+    case 6:
+#pragma unroll
+      for (int i = 0; i < 7; ++i)
+        y[i] = u[i] + h * (V::a71 * f[i] + V::a73 * k3[i] + V::a74 * k4[i] + V::a75 * k5[i] + V::a76 * k6[i]);
+      ty = tau + V::c7 * h;
+      break;
+    case 7:
+#pragma unroll
+      for (int i = 0; i < 7; ++i)
+        y[i] = u[i] + h * (V::a81 * f[i] + V::a83 * k3[i] + V::a84 * k4[i] + V::a85 * k5[i] + V::a86 * k6[i] +
+                           V::a87 * k7[i]);
+      ty = tau + h;
+      break;
+    default:
+#pragma unroll
+      for (int i = 0; i < 7; ++i)
+        y[i] = u[i] + h * (V::a91 * f[i] + V::a94 * k4[i] + V::a95 * k5[i] + V::a96 * k6[i] + V::a97 * k7[i] +
+                           V::a98 * kA[i]);
+      ty = tau + h;
+      break;
+  }
+}
+
+template <int INTEG>
+__device__ inline void stage_output(int s, const double* kk, double* kA, double* k3, double* k4, double* k5,
+                                    double* k6, double* k7) {
+  // Vern6: slot s stores k_{s+1}; k8 (slot 7) reuses kA; slot 8's k9 stays in kk.
+  // RK4:   slot 1 -> kA (k2), slot 2 -> k3, slot 3 -> k4, slot 4's f(u_{n+1}) stays in kk.
+#pragma unroll
+  for (int i = 0; i < 7; ++i) {
+    const double v = kk[i];
+    if (s == 1 || (INTEG == ART_VERN6 && s == 7)) kA[i] = v;
+    else if (s == 2) k3[i] = v;
+    else if (s == 3) k4[i] = v;
+    else if (INTEG == ART_VERN6 && s == 4) k5[i] = v;
+    else if (INTEG == ART_VERN6 && s == 5) k6[i] = v;
+    else if (INTEG == ART_VERN6 && s == 6) k7[i] = v;
+  }
+}
+
+enum LaneMode { M_IDLE = 0, M_INIT = 1, M_STEP = 2, M_ROOT = 3 };
+
+// ---------------------------------------------------------------------------
+// One loop iteration = one step attempt for every live lane: a runtime loop over the
+// stage slots with the RHS inlined ONCE (wave-uniform slot index; the stage glue is a
+// scalar switch). Lanes that just received a ray (M_INIT) use slots 1-2 for f(u0) and
+// Hairer's initial-dt probe; lanes polishing a crossing (M_ROOT) re-step from the step
+// start. After the slots, one condition call site serves the init sign, the root polish
+// and the ContinuousCallback scan of accepted steps.
+template <int INTEG>
+__global__ __launch_bounds__(256) void propagate_kernel(const KParams P, const int64_t n, const SegIn in,
+                                                        const SegOut out, const int32_t max_crossings,
+                                                        unsigned long long* __restrict__ queue,
+                                                        unsigned long long* __restrict__ stats) {
+  constexpr bool RK4 = (INTEG == ART_RK4);
+  constexpr int NSLOT = RK4 ? 4 : 8;
+  const int lane = threadIdx.x & 63;
+  const double tend = P.ln_t_end;
+  const int npts = P.interp_points;
+
+  int mode = M_IDLE;
+  int ray = -1;
+  bool photon = true;
+  double erg = 0.0;
+  double u[7], f[7], tau = 0.0, dt = 0.0, qold = 1e-4;
+  double cprev = 0.0;
+  int sprev = 0;
+  bool just_evented = false;
+  int n_acc = 0, n_rej = 0, ncross = 0, iter = 0;
+  double hroot = 0.0, r_tha = 0.0, r_ca = 0.0, r_thb = 0.0, r_cb = 0.0, r_t = 0.0, r_slope = 1.0, post_c = 0.0;
+  int post_s = 0, r_side = 0, r_it = 0;
+  int wnext = 0, wend = 0;
+  bool exhausted = false;
+  unsigned s_att = 0, s_acc = 0, s_root = 0, s_scan = 0, s_interp = 0, s_rays = 0, s_init = 0;
+#pragma unroll
+  for (int i = 0; i < 7; ++i) { u[i] = 0.0; f[i] = 0.0; }
+
+  while (true) {
+    // ---- refill idle lanes from the wave's chunk (one atomicAdd per 64 rays) ----
+    if (!exhausted) {
+      unsigned long long need = __ballot(mode == M_IDLE);
+      while (need != 0ull) {
+        if (wnext >= wend) {
+          unsigned long long base = 0;
+          const int leader = __ffsll((long long)need) - 1;
+          if (lane == leader) base = atomicAdd(queue, (unsigned long long)CHUNK);
+          base = __shfl(base, leader);
+          if ((int64_t)base >= n) { exhausted = true; break; }
+          wnext = __builtin_amdgcn_readfirstlane((int)base);
+          wend = __builtin_amdgcn_readfirstlane((int)((int64_t)base + CHUNK < n ? (int64_t)base + CHUNK : n));
+        }
+        const int rank = __popcll(need & ((1ull << lane) - 1ull));
+        const int cnt = __popcll(need);
+        const int take = (wend - wnext) < cnt ? (wend - wnext) : cnt;
+        if (mode == M_IDLE && rank < take) {
+          ray = wnext + rank;
+          mode = M_INIT;
+          // initial state (RayTracer.jl:179-216)
+          const double xs[3] = {in.x0[ray], in.x0[n + ray], in.x0[2 * n + ray]};
+          const double ks[3] = {in.k0[ray], in.k0[n + ray], in.k0[2 * n + ray]};
+          erg = in.erg[ray];
+          photon = in.species[ray] != ART_AXION;
+          initial_state(P, xs, ks, erg, in.dw[ray], u);
+          tau = in.lnt0[ray];
+          n_acc = n_rej = ncross = iter = 0;
+          just_evented = false;
+          qold = 1e-4;
+          s_rays += 1;
+        }
+        wnext += take;
+        need = __ballot(mode == M_IDLE);
+      }
+    }
+    if (__ballot(mode != M_IDLE) == 0ull) break;  // every lane idle and the queue drained
+
+    // ---- this iteration's step size ----
+    bool last = false, forced = false;
+    double hs = 0.0;
+    if (mode == M_ROOT) {
+      hs = r_t * hroot;
+    } else if (mode == M_STEP) {
+      hs = dt;  // (min(dt, dtmax) is implied: the span end clips every step)
+      if (tau + hs >= tend) { hs = tend - tau; last = true; }
+      else if (!RK4 && hs < P.dtmin) { hs = P.dtmin; forced = true; }
+    }
+
+    // ---- stage slots: one RHS per slot per lane ----
+    double kA[7], k3[7], k4[7], k5[7], k6[7], k7[7], y[7], kk[7];
+    double dt0 = 0.0;
+    bool init_short = false;  // initdt returned before its probe RHS
+#pragma unroll 1
+    for (int s = 1; s <= NSLOT; ++s) {
+      double ty = tau;
+      stage_input<INTEG>(s, u, f, kA, k3, k4, k5, k6, k7, hs, tau, y, ty);
+      bool active = (mode == M_STEP || mode == M_ROOT);
+      if (mode == M_INIT) {
+        if (s == 1) {  // f(u0)
+#pragma unroll
+          for (int i = 0; i < 7; ++i) y[i] = u[i];
+          ty = tau;
+          active = true;
+        } else if (s == 2 && !RK4 && !init_short) {  // ode_determine_initdt's probe f(u0 + dt0 f0)
+#pragma unroll
+          for (int i = 0; i < 7; ++i) y[i] = u[i] + dt0 * f[i];
+          ty = tau + dt0;
+          active = true;
+        }
+      }
+      if (active) {
+        rhs(P, photon, y, ty, erg, kk);
+        if (mode != M_INIT) {
+          stage_output<INTEG>(s, kk, kA, k3, k4, k5, k6, k7);
+        } else if (s == 1) {
+#pragma unroll
+          for (int i = 0; i < 7; ++i) f[i] = kk[i];
+          if (photon && u[0] < P.rNS) u[0] = P.rNS;  // hamiltonian's in-place clamp (:531)
+          s_init += 1;
+          if (RK4) {
+            dt = (tend - tau) / P.n_fixed;
+          } else {  // ode_determine_initdt, first half
+            double d0 = 0.0, d1 = 0.0;
+#pragma unroll
+            for (int i = 0; i < 7; ++i) {
+              const double sk = P.abstol + fabs(u[i]) * P.reltol;
+              d0 += (u[i] / sk) * (u[i] / sk);
+              d1 += (f[i] / sk) * (f[i] / sk);
+            }
+            d0 = sqrt(d0 / 7.0);
+            d1 = sqrt(d1 / 7.0);
+            dt0 = (d0 < 1e-5 || d1 < 1e-5) ? 1e-6 : 0.01 * (d0 / d1);
+            dt0 = fmin(dt0, tend - tau);
+            const double at = fabs(tau);
+            if (dt0 < 10.0 * (nextafter(at, INFINITY) - at)) {
+              dt = fmax(1e-6, P.dtmin);
+              init_short = true;
+            }
+          }
+        } else {  // ode_determine_initdt, second half
+          s_init += 1;
+          bool same = true;
+          double d1 = 0.0, d2 = 0.0;
+#pragma unroll
+          for (int i = 0; i < 7; ++i) {
+            const double sk = P.abstol + fabs(u[i]) * P.reltol;
+            same = same && (f[i] == kk[i]);
+            d1 += (f[i] / sk) * (f[i] / sk);
+            d2 += ((kk[i] - f[i]) / sk) * ((kk[i] - f[i]) / sk);
+          }
+          d1 = sqrt(d1 / 7.0);
+          d2 = sqrt(d2 / 7.0) / dt0;
+          if (same) {
+            dt = fmax(P.dtmin, 100.0 * dt0);
+          } else {
+            const double mx = fmax(d1, d2);
+            const double dt1 = (mx <= 1e-15) ? fmax(1e-6, dt0 * 1e-3) : pow(10.0, -(2.0 + log10(mx)) / 6.0);
+            dt = fmax(P.dtmin, fmin(fmin(100.0 * dt0, dt1), tend - tau));
+          }
+        }
+      }
+    }
+    // y = u_{n+1}, kk = f(u_{n+1}) for stepping lanes
+    double EEst = 0.0;
+    if (mode == M_STEP || mode == M_ROOT) {
+      if (photon && y[0] < P.rNS) y[0] = P.rNS;  // clamp on the FSAL stage (:531)
+      if (!RK4) {
+        using V = Vern6;
+        double acc = 0.0;
+#pragma unroll
+        for (int i = 0; i < 7; ++i) {
+          const double e = hs * (V::e1 * f[i] + V::e4 * k4[i] + V::e5 * k5[i] + V::e6 * k6[i] + V::e7 * k7[i] +
+                                 V::e8 * kA[i] + V::e9 * kk[i]);
+          const double sc = P.abstol + fmax(fabs(u[i]), fabs(y[i])) * P.reltol;
+          acc += (e / sc) * (e / sc);
+        }
+        EEst = sqrt(acc / 7.0);
+      }
+    }
+
+    // ---- controller (STEP lanes) ----
+    int finish = -1;
+    bool scan = false;       // accepted step to be scanned for sign changes
+    double dtnext = dt;
+    if (mode == M_STEP) {
+      s_att += 1;
+      ++iter;
+      bool finite = !isnan(EEst) && !isinf(EEst);
+#pragma unroll
+      for (int i = 0; i < 7; ++i) finite = finite && !isnan(y[i]) && !isinf(y[i]);
+      if (!finite) {
+        finish = ART_STATUS_NONFINITE;
+      } else {
+        // PI controller (OrdinaryDiffEq: beta1 = 7/60, beta2 = 1/15, gamma = 0.9, qmin = 0.2, qmax = 10)
+        double q = 1.0, q11 = 1.0;
+        bool accept = true;
+        if (!RK4) {
+          if (EEst == 0.0) {
+            q = 0.1;
+          } else {
+            q11 = pow(EEst, 7.0 / 60.0);
+            q = q11 / pow(qold, 1.0 / 15.0);
+            q = fmax(0.1, fmin(5.0, q / 0.9));
+          }
+          accept = (EEst <= 1.0) || forced;
+        }
+        if (!accept) {
+          dt = hs / fmin(5.0, q11 / 0.9);
+          ++n_rej;
+          if (iter >= P.maxiters) finish = ART_STATUS_MAXITERS;
+        } else {
+          ++n_acc;
+          s_acc += 1;
+          if (!RK4) {
+            qold = fmax(EEst, 1e-4);
+            dtnext = hs / q;
+          }
+          scan = true;
+        }
+      }
+    }
+
+    // ---- condition evaluations: init sign (1), root polish (1), scan (npts - 1) ----
+    double last_c = cprev, last_th = 0.0;
+    int last_s = sprev;
+    bool hit = false;
+    const int nc = (mode == M_INIT || mode == M_ROOT) ? 1 : (scan ? npts - 1 : 0);
+#pragma unroll 1
+    for (int ip = 1; ip <= nc; ++ip) {
+      double ui[7];
+      double tc;
+      const double th = double(ip) / double(npts - 1);
+      if (mode == M_INIT) {
+#pragma unroll
+        for (int i = 0; i < 7; ++i) ui[i] = u[i];
+        tc = tau;
+      } else if (mode == M_ROOT) {
+#pragma unroll
+        for (int i = 0; i < 7; ++i) ui[i] = y[i];
+        tc = tau + hs;
+      } else {
+        hermite7(u, f, y, kk, hs, th, ui);
+        tc = tau + th * hs;
+      }
+      const double ci = condition(P, ui, tc);
+      if (mode == M_INIT) {
+        cprev = ci;
+        sprev = isnan(ci) ? 0 : sgn(ci);
+        mode = M_STEP;
+        break;
+      }
+      if (mode == M_ROOT) {
+        // bracketed polish (Newton with the interpolant slope, then Illinois)
+        s_root += 1;
+        ++r_it;
+        bool done = !(fabs(ci) > 1e-12);
+        if (!done) {
+          if (sgn(ci) == sgn(r_ca)) { r_tha = r_t; r_ca = ci; if (r_side == -1) r_cb *= 0.5; r_side = -1; }
+          else { r_thb = r_t; r_cb = ci; if (r_side == 1) r_ca *= 0.5; r_side = 1; }
+          done = (r_thb - r_tha) * hroot < 1e-13 || r_it >= 9;
+          if (!done) {
+            double tn = (r_it == 1) ? r_t - ci / r_slope : r_tha - r_ca * (r_thb - r_tha) / (r_cb - r_ca);
+            if (!(tn > r_tha && tn < r_thb)) tn = 0.5 * (r_tha + r_thb);
+            r_t = tn;
+          }
+        }
+        if (done) {
+          const double tau_r = tau + hs;
+          const int a = affect(P, in, out, n, ray, y, tau_r, erg, ncross, max_crossings);
+#pragma unroll
+          for (int i = 0; i < 7; ++i) { u[i] = y[i]; f[i] = kk[i]; }
+          tau = tau_r;
+          cprev = post_c;  // the post-event side (DiffEq repeat_nudge): the root is not re-found
+          sprev = post_s;
+          just_evented = true;
+          mode = M_STEP;
+          if (a == 2) finish = ART_STATUS_CROSSING;
+          else if (photon && u[0] < P.rNS101) finish = ART_STATUS_HIT_NS;  // cb_r after the event
+          else if (iter >= P.maxiters) finish = ART_STATUS_MAXITERS;
+        }
+        break;
+      }
+      // ContinuousCallback scan of an accepted step (RayTracer.jl:357-358)
+      s_scan += 1;
+      if (isnan(ci)) { last_s = 0; continue; }  // no resonance possible where |u7| < m_a
+      const int si = sgn(ci);
+      if (last_s != 0 && si != 0 && si != last_s) {
+        int ne = 0;
+        const double t_int = illinois_interp(P, u, f, y, kk, tau, hs, last_th, th, last_c, ci, ne);
+        s_interp += ne;
+        if (!(just_evented && t_int < 0.01)) {  // DiffEq repeat_nudge after an event
+          hit = true;
+          mode = M_ROOT;
+          hroot = hs;
+          r_tha = last_th; r_ca = last_c; r_thb = th; r_cb = ci;
+          r_slope = (ci - last_c) / (th - last_th);
+          r_t = (t_int > last_th && t_int < th) ? t_int : 0.5 * (last_th + th);
+          r_side = 0;
+          r_it = 0;
+          post_c = ci;
+          post_s = si;
+          dt = dtnext;
+          break;
+        }
+      }
+      if (si != 0) { last_s = si; last_c = ci; last_th = th; }
+    }
+    if (scan && !hit) {
+#pragma unroll
+      for (int i = 0; i < 7; ++i) { u[i] = y[i]; f[i] = kk[i]; }
+      tau = last ? tend : tau + hs;
+      cprev = last_c;
+      sprev = last_s;
+      just_evented = false;
+      dt = dtnext;
+      if (photon && u[0] < P.rNS101) finish = ART_STATUS_HIT_NS;  // cb_r (:352-368)
+      else if (last) finish = ART_STATUS_SUCCESS;
+      else if (iter >= P.maxiters) finish = ART_STATUS_MAXITERS;
+    }
+
+    if (finish >= 0) {
+      double xe[3], ke[3];
+      back_transform(P, u, erg, xe, ke);
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        out.x_end[c * n + ray] = xe[c];
+        out.k_end[c * n + ray] = ke[c];
+      }
+      out.u7_end[ray] = u[6];
+      out.tau_end[ray] = tau;
+      out.status[ray] = finish;
+      out.n_acc[ray] = n_acc;
+      out.n_rej[ray] = n_rej;
+      if (out.xcount) out.xcount[ray] = ncross;
+      ray = -1;
+      mode = M_IDLE;
+    }
+  }
+
+  // wave-reduce the statistics and add them once per wave
+  const unsigned v[7] = {s_att, s_acc, s_root, s_scan, s_interp, s_rays, s_init};
+#pragma unroll
+  for (int k = 0; k < 7; ++k) {
+    unsigned long long x = v[k];
+    for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off);
+    if (lane == 0 && x) atomicAdd(&stats[k], x);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// find_samples_new (RayTracer.jl:1480-1653) + main_runner's erg and k_init
+// (MainRunner.jl:511-529): persistent lanes, one (ray, attempt) per lane per iteration.
+__global__ __launch_bounds__(256) void sample_kernel(const KParams P, const double maxR, const uint64_t seed,
+                                                     const int64_t ray_offset, const int64_t n, double* __restrict__ xo,
+                                                     double* __restrict__ ko, double* __restrict__ ergo,
+                                                     double* __restrict__ vifo, int32_t* __restrict__ wo,
+                                                     int32_t* __restrict__ ao, unsigned long long* __restrict__ queue) {
+  const int lane = threadIdx.x & 63;
+  int64_t ray = -1;
+  uint32_t attempt = 0;
+  int64_t wnext = 0, wend = 0;
+  bool exhausted = false;
+  const double send = 2.2 * maxR;
+  const int nsteps = (int)ceil(send / 0.5);
+  const int np = 20;  // ContinuousCallback(interp_points=20) (:1603)
+  while (true) {
+    if (!exhausted) {
+      unsigned long long need = __ballot(ray < 0);
+      while (need != 0ull && !exhausted) {
+        if (wnext >= wend) {
+          unsigned long long base = 0;
+          const int leader = __ffsll((long long)need) - 1;
+          if (lane == leader) base = atomicAdd(queue, (unsigned long long)CHUNK);
+          base = __shfl(base, leader);
+          if ((int64_t)base >= n) { exhausted = true; break; }
+          wnext = (int64_t)base;
+          wend = (wnext + CHUNK < n) ? wnext + CHUNK : n;
+        }
+        const int rank = __popcll(need & ((1ull << lane) - 1ull));
+        const int64_t avail = wend - wnext;
+        const int take = (int)(avail < (int64_t)__popcll(need) ? avail : (int64_t)__popcll(need));
+        if (ray < 0 && rank < take) { ray = wnext + rank; attempt = 0; }
+        wnext += take;
+        need = __ballot(ray < 0);
+      }
+    }
+    if (__ballot(ray >= 0) == 0ull) break;
+    if (ray < 0) continue;
+
+    double U[10];
+    attempt_uniforms(seed, uint64_t(ray_offset + ray), attempt, U);
+    double sti, cti, spi, cpi, stl, ctl, spl, cpl, sR, cR;
+    cti = 1.0 - 2.0 * U[0];
+    sti = sin(acos(cti));
+    sincos(U[1] * 2.0 * PI, &spi, &cpi);
+    ctl = 1.0 - 2.0 * U[2];
+    stl = sin(acos(ctl));
+    sincos(U[3] * 2.0 * PI, &spl, &cpl);
+    sincos(U[4] * 2.0 * PI, &sR, &cR);
+    const double rR = sqrt(U[5]) * maxR;
+    const double va[3] = {sti * cpi, sti * spi, cti};
+    const double vl[3] = {stl * cpl, stl * spl, ctl};
+    const double x1 = rR * cR, x2 = rR * sR;
+    // rotate (x1, x2, 0) by Inv[EulerMatrix(ϕi, θi, 0)] (:1523-1524); cos(-a) = cos a, sin(-a) = -sin a
+    double x0[3] = {x1 * cpi * cti - x2 * spi, x2 * cpi + x1 * spi * cti, -x1 * sti};
+    double vI[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) vI[i] = (220.0 + U[6 + i] * 1.0e-5) / sqrt(3.0);
+    const double vmag = sqrt(vI[0] * vI[0] + vI[1] * vI[1] + vI[2] * vI[2]);
+    const double gammaA = 1.0 / sqrt(1.0 - (vmag / C_KM) * (vmag / C_KM));
+    const double E = P.mass_a * sqrt(1.0 + (vmag / C_KM * gammaA) * (vmag / C_KM * gammaA));
+#pragma unroll
+    for (int i = 0; i < 3; ++i) x0[i] += va[i] * (-maxR * 1.1);
+    int randInx = 1 + (int)(U[9] * 6.0);
+    if (randInx > 6) randInx = 6;
+    int count = 0;
+    double xsel[3] = {0.0, 0.0, 0.0};
+    double xl[3];
+    double s_prev = 0.0;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) xl[i] = x0[i];
+    double c_prev = sampler_condition(P, xl, vl, E);
+    for (int st = 0; st < nsteps; ++st) {
+      const double s0 = st * 0.5;
+      const double s1 = fmin(s0 + 0.5, send);
+      for (int ip = 1; ip < np; ++ip) {
+        const double sc = s0 + (s1 - s0) * double(ip) / double(np - 1);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) xl[i] = x0[i] + va[i] * sc;
+        const double cc = sampler_condition(P, xl, vl, E);
+        if (signbit(c_prev) != signbit(cc) && c_prev != 0.0 && cc != 0.0) {
+          double a = s_prev, b = sc, fa = c_prev, fb = cc, root = sc;
+          int side = 0;
+          for (int it = 0; it < 100; ++it) {  // Illinois on the exact line
+            root = a - fa * (b - a) / (fb - fa);
+            double xr[3];
+#pragma unroll
+            for (int i = 0; i < 3; ++i) xr[i] = x0[i] + va[i] * root;
+            const double fr = sampler_condition(P, xr, vl, E);
+            if (fr == 0.0 || (b - a) < 1e-13 * fmax(1.0, fabs(root))) break;
+            if (signbit(fr) == signbit(fa)) { a = root; fa = fr; if (side == -1) fb *= 0.5; side = -1; }
+            else { b = root; fb = fr; if (side == 1) fa *= 0.5; side = 1; }
+          }
+          double xr[3];
+#pragma unroll
+          for (int i = 0; i < 3; ++i) xr[i] = x0[i] + va[i] * root;
+          // affect! (:1585-1597): keep crossings outside the star with E_loc > ωp
+          const double rr = sqrt(xr[0] * xr[0] + xr[1] * xr[1] + xr[2] * xr[2]);
+          double gtt, grr;
+          metric_tr(rr, P.rs_gr, gtt, grr);
+          if (rr > P.rNS && E / sqrt(grr) > wp_cart(P, xr)) {
+            ++count;
+            if (count == randInx) { xsel[0] = xr[0]; xsel[1] = xr[1]; xsel[2] = xr[2]; }
+          }
+        }
+        s_prev = sc;
+        c_prev = cc;
+      }
+    }
+    const bool give_up = attempt + 1 >= 1000000u;  // bounded: no conversion surface reachable
+    if (count >= randInx || give_up) {
+      if (count < randInx) { xsel[0] = xsel[1] = xsel[2] = NAN; count = 0; }
+      const double rmag = sqrt(xsel[0] * xsel[0] + xsel[1] * xsel[1] + xsel[2] * xsel[2]);
+      const double vml = sqrt(vmag * vmag + 2.0 * P.GM_c2 * C_KM * C_KM / rmag) / C_KM;  // :1644
+      double vel[3], vc[3];
+#pragma unroll
+      for (int i = 0; i < 3; ++i) { vel[i] = vl[i] * vml; vc[i] = vI[i] / C_KM; }
+      // MainRunner.jl:514-529: erg_inf_ini from vIfty/c, k_init = k_norm_Cart(ax_fix = true)
+      const double vm = sqrt(vc[0] * vc[0] + vc[1] * vc[1] + vc[2] * vc[2]);
+      const double gA = 1.0 / sqrt(1.0 - vm * vm);
+      const double Ei = P.mass_a * sqrt(1.0 + (vm * gA) * (vm * gA));
+      double kn[3];
+      k_norm_axion_shell(P, xsel, vel, Ei, kn);
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        xo[c * n + ray] = xsel[c];
+        ko[c * n + ray] = kn[c];
+        vifo[c * n + ray] = vc[c];
+      }
+      ergo[ray] = Ei;
+      wo[ray] = count;
+      ao[ray] = (int32_t)(attempt + 1);
+      ray = -1;
+    } else {
+      ++attempt;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// get_Prob_nonAD over groups; one thread per group (groups are one segment's crossings).
+__global__ __launch_bounds__(256) void prob_kernel(const KParams P, const int64_t nc, const double* __restrict__ pos,
+                                                   const double* __restrict__ kpos, const double* __restrict__ erg,
+                                                   const int64_t n_groups, const int64_t* __restrict__ gstart,
+                                                   double* __restrict__ outp) {
+  const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= n_groups) return;
+  const int64_t a = gstart ? gstart[g] : g;
+  const int64_t b = gstart ? gstart[g + 1] : g + 1;
+  const int64_t m = b - a;
+  if (m <= 0) return;
+  // linear-indexed group values (column-major m x 3): index q -> row q % m, col q / m
+  double ks_lin[3], B_lin[3], x0pl_lin[2];
+  for (int q = 0; q < 3; ++q) {
+    const int64_t row = q % m, col = q / m;
+    const double p3[3] = {pos[a + row], pos[nc + a + row], pos[2 * nc + a + row]};
+    const double k3[3] = {kpos[a + row], kpos[nc + a + row], kpos[2 * nc + a + row]};
+    const ProbLocal<double> Lq = prob_local(P, p3, k3, erg[a + row]);
+    ks_lin[q] = Lq.ks[col];
+    B_lin[q] = Lq.B[col];
+    if (q < 2) {
+      const double sph[3] = {Lq.r, Lq.th, Lq.ph};
+      x0pl_lin[q] = sph[col];
+    }
+  }
+  ProbLin<double> G;
+  G.k1 = ks_lin[0]; G.k2 = ks_lin[1]; G.k3 = ks_lin[2];
+  G.B1 = B_lin[0]; G.B2 = B_lin[1]; G.B3 = B_lin[2];
+  G.r_c = x0pl_lin[0]; G.th_c = x0pl_lin[1];
+  for (int64_t i = a; i < b; ++i) {
+    const double p3[3] = {pos[i], pos[nc + i], pos[2 * nc + i]};
+    const double k3[3] = {kpos[i], kpos[nc + i], kpos[2 * nc + i]};
+    const ProbLocal<double> L = prob_local(P, p3, k3, erg[i]);
+    outp[i] = prob_eval(P, P.g_agg, L, G);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Binned flux (plot/flux.py:38-48): φf = atan2(k_y, k_x) of final particles, per species.
+__global__ __launch_bounds__(256) void flux_kernel(const KParams P, const int64_t n, const double* __restrict__ x_end,
+                                                   const double* __restrict__ k_end, const int32_t* __restrict__ status,
+                                                   const int8_t* __restrict__ species, const double* __restrict__ w,
+                                                   const int32_t nbins, double* __restrict__ hist) {
+  extern __shared__ __attribute__((aligned(16))) double sh[];
+  for (int i = threadIdx.x; i < 2 * nbins; i += blockDim.x) sh[i] = 0.0;
+  __syncthreads();
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const double xr = sqrt(x_end[i] * x_end[i] + x_end[n + i] * x_end[n + i] + x_end[2 * n + i] * x_end[2 * n + i]);
+    // is_final: no crossing and escaped beyond 1.1 rNS (MainRunner.jl:203-209)
+    if (status[i] == ART_STATUS_CROSSING || !(xr > 1.1 * P.rNS)) continue;
+    const double phi = atan2(k_end[n + i], k_end[i]);
+    int bin = (int)floor((phi + PI) / (2.0 * PI) * nbins);
+    bin = bin < 0 ? 0 : (bin >= nbins ? nbins - 1 : bin);
+    const int row = (species && species[i] == ART_AXION) ? 0 : 1;
+    atomicAdd(&sh[row * nbins + bin], w ? w[i] : 1.0);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 2 * nbins; i += blockDim.x)
+    if (sh[i] != 0.0) atomicAdd(&hist[i], sh[i]);
+}
+
+// ---------------------------------------------------------------------------
+// Pointwise physics for parity tests.
+__global__ void eval_rhs_kernel(const KParams P, const int64_t n, const double* __restrict__ u,
+                                const double* __restrict__ tau, const double* __restrict__ erg,
+                                const int8_t* __restrict__ species, double* __restrict__ du) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  double ui[7], d[7];
+  for (int c = 0; c < 7; ++c) ui[c] = u[c * n + i];
+  rhs(P, species[i] != ART_AXION, ui, tau[i], erg[i], d);
+  for (int c = 0; c < 7; ++c) du[c * n + i] = d[c];
+}
+
+__global__ void eval_hamiltonian_kernel(const KParams P, const int64_t n, const double* __restrict__ x,
+                                        const double* __restrict__ k, const double* __restrict__ Tm,
+                                        const double* __restrict__ E, double* __restrict__ H,
+                                        double* __restrict__ dHdx, double* __restrict__ dHdk,
+                                        double* __restrict__ dHdT) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const double xi[3] = {x[i], x[n + i], x[2 * n + i]};
+  const double ki[3] = {k[i], k[n + i], k[2 * n + i]};
+  double h, gx[3], gk[3], gT;
+  hamiltonian_full(P, xi, ki, Tm[i], E[i], &h, gx, gk, &gT);
+  H[i] = h;
+  dHdT[i] = gT;
+  for (int c = 0; c < 3; ++c) {
+    dHdx[c * n + i] = gx[c];
+    dHdk[c * n + i] = gk[c];
+  }
+}
+
+__global__ void eval_condition_kernel(const KParams P, const int64_t n, const double* __restrict__ u,
+                                      const double* __restrict__ tau, double* __restrict__ outc) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  double ui[7];
+  for (int c = 0; c < 7; ++c) ui[c] = u[c * n + i];
+  outc[i] = condition(P, ui, tau[i]);
+}
+
+// ---------------------------------------------------------------------------
+// host-side launch wrappers (art_internal.h)
+int persistent_blocks(const void* func, int64_t work) {
+  int dev = 0, ncu = 0, per_cu = 0;
+  (void)hipGetDevice(&dev);
+  (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, func, 256, 0) != hipSuccess || per_cu < 1) per_cu = 1;
+  const int64_t need = (work + 255) / 256;
+  const int64_t full = (int64_t)ncu * per_cu;
+  return (int)(need < full ? need : full);
+}
+
+hipError_t launch_propagate(const KParams& P, int64_t n, const SegIn& in, const SegOut& out, int32_t max_crossings,
+                            unsigned long long* queue, unsigned long long* stats, hipStream_t s, int* grid_out) {
+  const void* fn = (P.integrator == ART_RK4) ? (const void*)propagate_kernel<ART_RK4>
+                                             : (const void*)propagate_kernel<ART_VERN6>;
+  const int grid = persistent_blocks(fn, n);
+  if (grid_out) *grid_out = grid;
+  if (P.integrator == ART_RK4)
+    hipLaunchKernelGGL(propagate_kernel<ART_RK4>, dim3(grid), dim3(256), 0, s, P, n, in, out, max_crossings, queue, stats);
+  else
+    hipLaunchKernelGGL(propagate_kernel<ART_VERN6>, dim3(grid), dim3(256), 0, s, P, n, in, out, max_crossings, queue,
+                       stats);
+  return hipGetLastError();
+}
+
+hipError_t launch_sample(const KParams& P, double maxR, uint64_t seed, int64_t ray_offset, int64_t n, double* x,
+                         double* k, double* erg, double* vifty, int32_t* w, int32_t* att, unsigned long long* queue,
+                         hipStream_t s) {
+  const int grid = persistent_blocks((const void*)sample_kernel, n);
+  hipLaunchKernelGGL(sample_kernel, dim3(grid), dim3(256), 0, s, P, maxR, seed, ray_offset, n, x, k, erg, vifty, w, att,
+                     queue);
+  return hipGetLastError();
+}
+
+hipError_t launch_prob(const KParams& P, int64_t nc, const double* pos, const double* kpos, const double* erg,
+                       int64_t n_groups, const int64_t* gstart, double* out, hipStream_t s) {
+  const int64_t grid = (n_groups + 255) / 256;
+  hipLaunchKernelGGL(prob_kernel, dim3((unsigned)grid), dim3(256), 0, s, P, nc, pos, kpos, erg, n_groups, gstart, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_flux(const KParams& P, int64_t n, const double* x_end, const double* k_end, const int32_t* status,
+                       const int8_t* species, const double* w, int32_t nbins, double* hist, hipStream_t s) {
+  int64_t grid = (n + 255) / 256;
+  if (grid > 2048) grid = 2048;
+  if (grid < 1) grid = 1;
+  hipLaunchKernelGGL(flux_kernel, dim3((unsigned)grid), dim3(256), 2 * nbins * sizeof(double), s, P, n, x_end, k_end,
+                     status, species, w, nbins, hist);
+  return hipGetLastError();
+}
+
+hipError_t launch_eval_rhs(const KParams& P, int64_t n, const double* u, const double* tau, const double* erg,
+                           const int8_t* species, double* du, hipStream_t s) {
+  hipLaunchKernelGGL(eval_rhs_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, P, n, u, tau, erg, species, du);
+  return hipGetLastError();
+}
+
+hipError_t launch_eval_hamiltonian(const KParams& P, int64_t n, const double* x, const double* k, const double* T,
+                                   const double* E, double* H, double* dHdx, double* dHdk, double* dHdT,
+                                   hipStream_t s) {
+  hipLaunchKernelGGL(eval_hamiltonian_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, P, n, x, k, T, E, H,
+                     dHdx, dHdk, dHdT);
+  return hipGetLastError();
+}
+
+hipError_t launch_eval_condition(const KParams& P, int64_t n, const double* u, const double* tau, double* out,
+                                 hipStream_t s) {
+  hipLaunchKernelGGL(eval_condition_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, P, n, u, tau, out);
+  return hipGetLastError();
+}
+
+template __global__ void propagate_kernel<ART_VERN6>(const KParams, const int64_t, const SegIn, const SegOut,
+                                                     const int32_t, unsigned long long*, unsigned long long*);
+template __global__ void propagate_kernel<ART_RK4>(const KParams, const int64_t, const SegIn, const SegOut,
+                                                   const int32_t, unsigned long long*, unsigned long long*);
+
+}  // namespace art

@@ -122,6 +122,10 @@ int art_synchronize(void);
 /* Duration [ms] of the last propagate kernel, from HIP events recorded on the stream
  * the kernel ran on. */
 double art_last_kernel_ms(void);
+/* Counters of the last propagate launch: [step attempts, accepted steps, root re-steps,
+ * scan condition evals, interpolant-root condition evals, rays, init RHS evals, 0] and the
+ * persistent grid size; they feed the roofline accounting of bench.py. */
+int art_last_stats(uint64_t* stats, int32_t* grid);
 /* The Vern6 tableau the kernel uses: c[9], A[81] row-major, b[9], bhat[9]. */
 int art_vern6_tableau(double* c, double* A, double* b, double* bhat);
 

@@ -568,6 +568,28 @@ class Segment {
     return tr;
   }
 
+  // Bracketed root polish on the true trajectory (same algorithm as the kernel's ROOT mode).
+  struct RootBracket {
+    double tha, ca, thb, cb, t, slope;
+    int side = 0, rit = 0;
+    RootBracket(double a, double fa, double b, double fb, double t_int)
+        : tha(a), ca(fa), thb(b), cb(fb), t(t_int), slope((fb - fa) / (b - a)) {
+      if (!(t > tha && t < thb)) t = 0.5 * (tha + thb);
+    }
+    // feed the true condition at t; returns true when t is the accepted root
+    bool update(double c, double h) {
+      ++rit;
+      if (!(std::abs(c) > 1e-12)) return true;  // converged (or NaN: stop here)
+      if (sgn(c) == sgn(ca)) { tha = t; ca = c; if (side == -1) cb *= 0.5; side = -1; }
+      else { thb = t; cb = c; if (side == 1) ca *= 0.5; side = 1; }
+      if ((thb - tha) * h < 1e-13 || rit >= 9) return true;
+      double tn = (rit == 1) ? t - c / slope : tha - ca * (thb - tha) / (cb - ca);
+      if (!(tn > tha && tn < thb)) tn = 0.5 * (tha + thb);
+      t = tn;
+      return false;
+    }
+  };
+
   // affect! (RayTracer.jl:301-350). Returns 0 skip, 1 recorded, 2 recorded + terminate
   int affect(const double u[7], double tau) {
     const double s = 1.0001;
@@ -680,36 +702,27 @@ class Segment {
         }
         // Sign change in (last_th, th]. (1) Illinois on the cubic Hermite interpolant (cheap
         // condition evaluations only); (2) polish on the TRUE trajectory by re-stepping from
-        // (u, fcur): a Newton step with the interpolant's slope, then secant iterations, until
-        // |condition| <= 1e-12 (above the ~1e-13 noise floor of a re-stepped condition).
-        const double slope = (ci - last_c) / (th - last_th);
-        double t0 = illinois_interp(u, fcur, unew, fnew, tau, h, last_th, th, last_c, ci);
-        double ur[7], fr[7], ub[7], fb[7];
-        step(u, fcur, tau, t0 * h, ur, fr);
-        double c0 = cond(ur, tau + t0 * h);
-        ++n_root_steps;
-        double best = std::abs(c0);
-        std::memcpy(ub, ur, sizeof ub); std::memcpy(fb, fr, sizeof fb);
-        double tbest = t0;
-        double t1 = t0 - c0 / slope;
-        for (int it = 0; it < 8 && best > 1e-12; ++it) {
-          step(u, fcur, tau, t1 * h, ur, fr);
-          double c1 = cond(ur, tau + t1 * h);
-          ++n_root_steps;
-          if (trace) std::fprintf(stderr, "  root it=%d th=%.17g c=%.6e\n", it, t1, c1);
-          if (std::isnan(c1)) break;
-          if (std::abs(c1) < best) {
-            best = std::abs(c1); tbest = t1;
-            std::memcpy(ub, ur, sizeof ub); std::memcpy(fb, fr, sizeof fb);
-          }
-          if (c1 == c0 || std::abs(t1 - t0) * h < 1e-14) break;
-          double t2 = t1 - c1 * (t1 - t0) / (c1 - c0);
-          t0 = t1; c0 = c1; t1 = t2;
+        // (u, fcur), always inside the detection bracket so time never runs backwards: a
+        // Newton step with the interpolant's slope, then Illinois, until |condition| <= 1e-12
+        // (above the ~1e-13 noise floor of a re-stepped condition), the bracket is below
+        // 1e-13 in ln t, or 9 re-steps. After an event, DiffEq takes the sign from a point
+        // nudged 1/100 of a step ahead (repeat_nudge); sign changes before it are ignored.
+        const double t_int = illinois_interp(u, fcur, unew, fnew, tau, h, last_th, th, last_c, ci);
+        if (just_evented && t_int < 0.01) {
+          last_s = si; last_c = ci; last_th = th;
+          continue;
         }
-        std::memcpy(ur, ub, sizeof ub); std::memcpy(fr, fb, sizeof fb);
-        const double tr = tbest;
+        RootBracket rb(last_th, last_c, th, ci, t_int);
         last_s = si; last_c = ci; last_th = th;
-        if (just_evented && tr * h <= 1e-10) continue;  // never re-find the root we resumed from
+        double ur[7], fr[7];
+        for (;;) {
+          step(u, fcur, tau, rb.t * h, ur, fr);
+          const double c1 = cond(ur, tau + rb.t * h);
+          ++n_root_steps;
+          if (trace) std::fprintf(stderr, "  root it=%d th=%.17g c=%.6e\n", rb.rit, rb.t, c1);
+          if (rb.update(c1, h)) break;
+        }
+        const double tr = rb.t;
         const double tau_r = tau + tr * h;
         const int a = affect(ur, tau_r);
         std::memcpy(u, ur, sizeof(double) * 7);
@@ -996,7 +1009,7 @@ void oracle_sample(const art_params* P, double maxR, uint64_t seed, int64_t ray_
 #pragma omp parallel for schedule(dynamic, 1) num_threads(nthreads > 0 ? nthreads : 1)
   for (int64_t i = 0; i < n; ++i) {
     uint64_t ray = uint64_t(ray_offset + i);
-    for (uint32_t a = 0;; ++a) {
+    for (uint32_t a = 0; a < 1000000u; ++a) {
       double U[10];
       attempt_uniforms(seed, ray, a, U);
       SampleAttempt s = find_samples_attempt(*P, maxR, U);

@@ -1,0 +1,55 @@
+// TEST TOOL ONLY: host build of the product's physics header (art_core.h) so the CPU test
+// suite can check the hand-derived analytic gradients against the oracle's dual numbers
+// without a GPU. Never loaded by the product (adiabatic_raytracer_amd).
+#include "../adiabatic_raytracer_amd/csrc/art_core.h"
+
+using namespace art;
+
+extern "C" {
+void cc_rhs(const art_params* p, int species, const double* u, double tau, double erg, double* du) {
+  KParams K = make_kparams(*p);
+  rhs(K, species != ART_AXION, u, tau, erg, du);
+}
+double cc_condition(const art_params* p, const double* u, double tau) {
+  KParams K = make_kparams(*p);
+  return condition(K, u, tau);
+}
+void cc_hamiltonian(const art_params* p, const double* x, const double* k, double T, double E, double* H, double* gx,
+                    double* gk, double* gT) {
+  KParams K = make_kparams(*p);
+  hamiltonian_full(K, x, k, T, E, H, gx, gk, gT);
+}
+void cc_initial_state(const art_params* p, const double* x0, const double* k0, double erg, double dw, double* u) {
+  KParams K = make_kparams(*p);
+  initial_state(K, x0, k0, erg, dw, u);
+}
+void cc_back_transform(const art_params* p, const double* u, double erg, double* x, double* k) {
+  KParams K = make_kparams(*p);
+  back_transform(K, u, erg, x, k);
+}
+double cc_prob_single(const art_params* p, const double* pos, const double* kpos, double erg) {
+  KParams K = make_kparams(*p);
+  return prob_nonad_single(K, pos, kpos, erg);
+}
+double cc_sampler_condition(const art_params* p, const double* x, const double* vl, double E) {
+  KParams K = make_kparams(*p);
+  return sampler_condition(K, x, vl, E);
+}
+}
+
+extern "C" {
+void cc_attempt_uniforms(uint64_t seed, uint64_t ray, uint32_t attempt, double* U) { attempt_uniforms(seed, ray, attempt, U); }
+void cc_philox(const uint32_t* ctr, const uint32_t* key, uint32_t* out) {
+  uint32_t c[4] = {ctr[0], ctr[1], ctr[2], ctr[3]};
+  philox4x32_10(c, key[0], key[1]);
+  for (int i = 0; i < 4; ++i) out[i] = c[i];
+}
+void cc_sincos(const double* x, int64_t n, double* s, double* c) {
+  for (int64_t i = 0; i < n; ++i) msincos(x[i], s[i], c[i]);
+}
+void cc_metric_d(double r, double rs, double* out) {
+  double gtt, grr, dgtt, dgrr;
+  metric_tr_d(r, rs, gtt, grr, dgtt, dgrr);
+  out[0] = gtt; out[1] = grr; out[2] = dgtt; out[3] = dgrr;
+}
+}
