@@ -181,8 +181,8 @@ __device__ inline double illinois_interp(const KParams& P, const double* u0, con
 __device__ inline int affect(const KParams& P, const SegIn& in, const SegOut& out, int64_t n, int64_t ray,
                              const double* u, double tau, double erg, int& ncross, int max_crossings) {
   double st, ct, sp, cp;
-  sincos(u[1], &st, &ct);
-  sincos(u[2], &sp, &cp);
+  msincos(u[1], st, ct);
+  msincos(u[2], sp, cp);
   if (ncross == 0) {  // a "crossing" at the start point is not new (:303-314)
     const double s = 1.0001;
     const double pos[3] = {st * cp * u[0], st * sp * u[0], ct * u[0]};
@@ -201,15 +201,13 @@ __device__ inline int affect(const KParams& P, const SegIn& in, const SegOut& ou
   const int j = ncross;
   if (out.xcount && j < out.cap) {
     const double dwc = u[6] / erg;
-    const double eeff = erg * fabs(dwc);  // get_tree: erg_inf_ini .* abs.(Δωc) (MainRunner.jl:265)
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
       out.xpos[(int64_t(c) * out.cap + j) * n + ray] = x[c];
       out.xk[(int64_t(c) * out.cap + j) * n + ray] = k[c];
     }
     out.xt[int64_t(j) * n + ray] = exp(tau);
-    out.xdw[int64_t(j) * n + ray] = dwc;
-    out.xp[int64_t(j) * n + ray] = prob_nonad_single(P, x, k, eeff);
+    out.xdw[int64_t(j) * n + ray] = dwc;  // P_nonAD: crossing_prob_kernel
   }
   ncross = j + 1;
   const int maxc = max_crossings <= 0 ? -1 : max_crossings;
@@ -217,122 +215,71 @@ __device__ inline int affect(const KParams& P, const SegIn& in, const SegOut& ou
 }
 
 // ---------------------------------------------------------------------------
-// Stage glue of the slot loop. Slot s (1..8) of a Vern6 attempt evaluates k_{s+1} at
-// y = u + h Σ_j a_{s+1,j} k_j; k2 and k8 share one register set (kA) because k2 is dead
-// before k8 is born. Slot 8's input is u_{n+1} itself (FSAL: b = A[9,:]).
-template <int INTEG>
-__device__ inline void stage_input(int s, const double* u, const double* f, const double* kA, const double* k3,
-                                   const double* k4, const double* k5, const double* k6, const double* k7, double h,
-                                   double tau, double* y, double& ty) {
-  using V = Vern6;
-  if (INTEG == ART_RK4) {
-    // classical RK4: slots 1..3 give k2..k4, slot 4 gives f(u_{n+1}); kA = k2, k3 = k3, k4 = k4
-    switch (s) {
-      case 1:
-#pragma unroll
-        for (int i = 0; i < 7; ++i) y[i] = u[i] + 0.5 * h * f[i];
-        ty = tau + 0.5 * h;
-        break;
-      case 2:
-#pragma unroll
-        for (int i = 0; i < 7; ++i) y[i] = u[i] + 0.5 * h * kA[i];
-        ty = tau + 0.5 * h;
-        break;
-      case 3:
-#pragma unroll
-        for (int i = 0; i < 7; ++i) y[i] = u[i] + h * k3[i];
-        ty = tau + h;
-        break;
-      default:
-#pragma unroll
-        for (int i = 0; i < 7; ++i) y[i] = u[i] + h / 6.0 * (f[i] + 2.0 * kA[i] + 2.0 * k3[i] + k4[i]);
-        ty = tau + h;
-        break;
-    }
-    return;
-  }
-  switch (s) {
-    case 1:
-#pragma unroll
-      for (int i = 0; i < 7; ++i) y[i] = u[i] + h * (V::a21 * f[i]);
-      ty = tau + V::c2 * h;
-      break;
-    case 2:
-#pragma unroll
-      for (int i = 0; i < 7; ++i) y[i] = u[i] + h * (V::a31 * f[i] + V::a32 * kA[i]);
-      ty = tau + V::c3 * h;
-      break;
-    case 3:
-#pragma unroll
-      for (int i = 0; i < 7; ++i) y[i] = u[i] + h * (V::a41 * f[i] + V::a43 * k3[i]);
-      ty = tau + V::c4 * h;
-      break;
-    case 4:
-#pragma unroll
-      for (int i = 0; i < 7; ++i) y[i] = u[i] + h * (V::a51 * f[i] + V::a53 * k3[i] + V::a54 * k4[i]);
-      ty = tau + V::c5 * h;
-      break;
-    case 5:
-#pragma unroll
-      for (int i = 0; i < 7; ++i) y[i] = u[i] + h * (V::a61 * f[i] + V::a63 * k3[i] + V::a64 * k4[i] + V::a65 * k5[i]);
-      ty = tau + V::c6 * h;
-      break;
-    case 6:
-#pragma unroll
-      for (int i = 0; i < 7; ++i)
-        y[i] = u[i] + h * (V::a71 * f[i] + V::a73 * k3[i] + V::a74 * k4[i] + V::a75 * k5[i] + V::a76 * k6[i]);
-      ty = tau + V::c7 * h;
-      break;
-    case 7:
-#pragma unroll
-      for (int i = 0; i < 7; ++i)
-        y[i] = u[i] + h * (V::a81 * f[i] + V::a83 * k3[i] + V::a84 * k4[i] + V::a85 * k5[i] + V::a86 * k6[i] +
-                           V::a87 * k7[i]);
-      ty = tau + h;
-      break;
-    default:
-#pragma unroll
-      for (int i = 0; i < 7; ++i)
-        y[i] = u[i] + h * (V::a91 * f[i] + V::a94 * k4[i] + V::a95 * k5[i] + V::a96 * k6[i] + V::a97 * k7[i] +
-                           V::a98 * kA[i]);
-      ty = tau + h;
-      break;
-  }
-}
+// Stage glue, table-driven. Slot s (0-based) of an attempt evaluates the next stage at
+//   y = u + h (cf[s] f + cA[s] kA + Σ_q cL[s][q] L_q),   t = τ + ct[s] h,
+// where kA is ONE register-resident stage vector (k2, later k8 -- their lifetimes do not
+// overlap) and L_0..L_4 are stage vectors parked in LDS (k3..k7 for Vern6; k3, k4 for RK4).
+// Coefficients are wave-uniform scalar loads; the RHS is inlined once.
+constexpr int LDS_SLOTS = 5;
+struct StageTable {
+  double cf[8], cA[8], cL[8][LDS_SLOTS], ct[8];
+  int storeA[8], storeL[8];  // after slot s: kk -> kA? kk -> L[storeL]? (-1: neither)
+  double e_f, e_A, e_L[LDS_SLOTS], e_k;  // error weights (Vern6): btilde of f, kA(=k8), L, k9
+};
 
-template <int INTEG>
-__device__ inline void stage_output(int s, const double* kk, double* kA, double* k3, double* k4, double* k5,
-                                    double* k6, double* k7) {
-  // Vern6: slot s stores k_{s+1}; k8 (slot 7) reuses kA; slot 8's k9 stays in kk.
-  // RK4:   slot 1 -> kA (k2), slot 2 -> k3, slot 3 -> k4, slot 4's f(u_{n+1}) stays in kk.
-#pragma unroll
-  for (int i = 0; i < 7; ++i) {
-    const double v = kk[i];
-    if (s == 1 || (INTEG == ART_VERN6 && s == 7)) kA[i] = v;
-    else if (s == 2) k3[i] = v;
-    else if (s == 3) k4[i] = v;
-    else if (INTEG == ART_VERN6 && s == 4) k5[i] = v;
-    else if (INTEG == ART_VERN6 && s == 5) k6[i] = v;
-    else if (INTEG == ART_VERN6 && s == 6) k7[i] = v;
-  }
-}
+__constant__ StageTable c_vern6 = {
+    // cf: a_{s+2,1}
+    {Vern6::a21, Vern6::a31, Vern6::a41, Vern6::a51, Vern6::a61, Vern6::a71, Vern6::a81, Vern6::a91},
+    // cA: coefficient of kA (k2 for slots 0..6, k8 for slot 7)
+    {0.0, Vern6::a32, 0.0, 0.0, 0.0, 0.0, 0.0, Vern6::a98},
+    // cL: coefficients of k3..k7
+    {{0, 0, 0, 0, 0},
+     {0, 0, 0, 0, 0},
+     {Vern6::a43, 0, 0, 0, 0},
+     {Vern6::a53, Vern6::a54, 0, 0, 0},
+     {Vern6::a63, Vern6::a64, Vern6::a65, 0, 0},
+     {Vern6::a73, Vern6::a74, Vern6::a75, Vern6::a76, 0},
+     {Vern6::a83, Vern6::a84, Vern6::a85, Vern6::a86, Vern6::a87},
+     {0, Vern6::a94, Vern6::a95, Vern6::a96, Vern6::a97}},
+    {Vern6::c2, Vern6::c3, Vern6::c4, Vern6::c5, Vern6::c6, Vern6::c7, 1.0, 1.0},
+    {1, 0, 0, 0, 0, 0, 1, 0},
+    {-1, 0, 1, 2, 3, 4, -1, -1},
+    Vern6::e1, Vern6::e8, {0.0, Vern6::e4, Vern6::e5, Vern6::e6, Vern6::e7}, Vern6::e9};
+
+__constant__ StageTable c_rk4 = {
+    {0.5, 0.0, 0.0, 1.0 / 6.0, 0, 0, 0, 0},
+    {0.0, 0.5, 0.0, 2.0 / 6.0, 0, 0, 0, 0},
+    {{0, 0, 0, 0, 0}, {0, 0, 0, 0, 0}, {1.0, 0, 0, 0, 0}, {2.0 / 6.0, 1.0 / 6.0, 0, 0, 0},
+     {0, 0, 0, 0, 0}, {0, 0, 0, 0, 0}, {0, 0, 0, 0, 0}, {0, 0, 0, 0, 0}},
+    {0.5, 0.5, 1.0, 1.0, 0, 0, 0, 0},
+    {1, 0, 0, 0, 0, 0, 0, 0},
+    {-1, 0, 1, -1, -1, -1, -1, -1},
+    0.0, 0.0, {0, 0, 0, 0, 0}, 0.0};
 
 enum LaneMode { M_IDLE = 0, M_INIT = 1, M_STEP = 2, M_ROOT = 3 };
 
+constexpr int BLOCK = 256;
+// Waves per SIMD the integrator is register-budgeted for (1: 512 VGPR+AGPR, 2: 256).
+#ifndef ART_WAVES_PER_SIMD
+#define ART_WAVES_PER_SIMD 2
+#endif
+
 // ---------------------------------------------------------------------------
 // One loop iteration = one step attempt for every live lane: a runtime loop over the
-// stage slots with the RHS inlined ONCE (wave-uniform slot index; the stage glue is a
-// scalar switch). Lanes that just received a ray (M_INIT) use slots 1-2 for f(u0) and
-// Hairer's initial-dt probe; lanes polishing a crossing (M_ROOT) re-step from the step
-// start. After the slots, one condition call site serves the init sign, the root polish
-// and the ContinuousCallback scan of accepted steps.
+// stage slots with the RHS inlined once. Lanes that just received a ray (M_INIT) use
+// slots 0-1 for f(u0) and Hairer's initial-dt probe; lanes polishing a crossing (M_ROOT)
+// re-step from the step start. After the slots, one condition call site serves the init
+// sign, the root polish and the ContinuousCallback scan of accepted steps.
 template <int INTEG>
-__global__ __launch_bounds__(256) void propagate_kernel(const KParams P, const int64_t n, const SegIn in,
-                                                        const SegOut out, const int32_t max_crossings,
-                                                        unsigned long long* __restrict__ queue,
-                                                        unsigned long long* __restrict__ stats) {
+__global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(const KParams P, const int64_t n, const SegIn in,
+                                                           const SegOut out, const int32_t max_crossings,
+                                                           unsigned long long* __restrict__ queue,
+                                                           unsigned long long* __restrict__ stats) {
   constexpr bool RK4 = (INTEG == ART_RK4);
   constexpr int NSLOT = RK4 ? 4 : 8;
+  const StageTable& T = RK4 ? c_rk4 : c_vern6;
+  __shared__ double lds[LDS_SLOTS * 7 * BLOCK];  // [slot][component][lane]: conflict-free ds_read_b64
+  double* const L = lds + threadIdx.x;
   const int lane = threadIdx.x & 63;
   const double tend = P.ln_t_end;
   const int npts = P.interp_points;
@@ -404,21 +351,36 @@ __global__ __launch_bounds__(256) void propagate_kernel(const KParams P, const i
     }
 
     // ---- stage slots: one RHS per slot per lane ----
-    double kA[7], k3[7], k4[7], k5[7], k6[7], k7[7], y[7], kk[7];
+    double kA[7], y[7], kk[7];
+#pragma unroll
+    for (int i = 0; i < 7; ++i) kA[i] = 0.0;  // read (times a zero coefficient) before its first store
     double dt0 = 0.0;
     bool init_short = false;  // initdt returned before its probe RHS
 #pragma unroll 1
-    for (int s = 1; s <= NSLOT; ++s) {
-      double ty = tau;
-      stage_input<INTEG>(s, u, f, kA, k3, k4, k5, k6, k7, hs, tau, y, ty);
+    for (int s = 0; s < NSLOT; ++s) {
+      const double cf = T.cf[s], cA = T.cA[s];
+      double acc[7];
+#pragma unroll
+      for (int i = 0; i < 7; ++i) acc[i] = cf * f[i] + cA * kA[i];
+#pragma unroll 1
+      for (int q = 0; q < LDS_SLOTS; ++q) {
+        const double c = T.cL[s][q];
+        if (c != 0.0) {
+#pragma unroll
+          for (int i = 0; i < 7; ++i) acc[i] += c * L[(q * 7 + i) * BLOCK];
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 7; ++i) y[i] = u[i] + hs * acc[i];
+      double ty = tau + T.ct[s] * hs;
       bool active = (mode == M_STEP || mode == M_ROOT);
       if (mode == M_INIT) {
-        if (s == 1) {  // f(u0)
+        if (s == 0) {  // f(u0)
 #pragma unroll
           for (int i = 0; i < 7; ++i) y[i] = u[i];
           ty = tau;
           active = true;
-        } else if (s == 2 && !RK4 && !init_short) {  // ode_determine_initdt's probe f(u0 + dt0 f0)
+        } else if (s == 1 && !RK4 && !init_short) {  // ode_determine_initdt's probe f(u0 + dt0 f0)
 #pragma unroll
           for (int i = 0; i < 7; ++i) y[i] = u[i] + dt0 * f[i];
           ty = tau + dt0;
@@ -428,8 +390,16 @@ __global__ __launch_bounds__(256) void propagate_kernel(const KParams P, const i
       if (active) {
         rhs(P, photon, y, ty, erg, kk);
         if (mode != M_INIT) {
-          stage_output<INTEG>(s, kk, kA, k3, k4, k5, k6, k7);
-        } else if (s == 1) {
+          if (T.storeA[s]) {
+#pragma unroll
+            for (int i = 0; i < 7; ++i) kA[i] = kk[i];
+          }
+          const int sl = T.storeL[s];
+          if (sl >= 0) {
+#pragma unroll
+            for (int i = 0; i < 7; ++i) L[(sl * 7 + i) * BLOCK] = kk[i];
+          }
+        } else if (s == 0) {
 #pragma unroll
           for (int i = 0; i < 7; ++i) f[i] = kk[i];
           if (photon && u[0] < P.rNS) u[0] = P.rNS;  // hamiltonian's in-place clamp (:531)
@@ -482,12 +452,13 @@ __global__ __launch_bounds__(256) void propagate_kernel(const KParams P, const i
     if (mode == M_STEP || mode == M_ROOT) {
       if (photon && y[0] < P.rNS) y[0] = P.rNS;  // clamp on the FSAL stage (:531)
       if (!RK4) {
-        using V = Vern6;
         double acc = 0.0;
 #pragma unroll
         for (int i = 0; i < 7; ++i) {
-          const double e = hs * (V::e1 * f[i] + V::e4 * k4[i] + V::e5 * k5[i] + V::e6 * k6[i] + V::e7 * k7[i] +
-                                 V::e8 * kA[i] + V::e9 * kk[i]);
+          double e = T.e_f * f[i] + T.e_A * kA[i] + T.e_k * kk[i];
+#pragma unroll
+          for (int q = 1; q < LDS_SLOTS; ++q) e += T.e_L[q] * L[(q * 7 + i) * BLOCK];
+          e *= hs;
           const double sc = P.abstol + fmax(fabs(u[i]), fabs(y[i])) * P.reltol;
           acc += (e / sc) * (e / sc);
         }
@@ -497,7 +468,7 @@ __global__ __launch_bounds__(256) void propagate_kernel(const KParams P, const i
 
     // ---- controller (STEP lanes) ----
     int finish = -1;
-    bool scan = false;       // accepted step to be scanned for sign changes
+    bool scan = false;  // accepted step to be scanned for sign changes
     double dtnext = dt;
     if (mode == M_STEP) {
       s_att += 1;
@@ -537,16 +508,23 @@ __global__ __launch_bounds__(256) void propagate_kernel(const KParams P, const i
       }
     }
 
-    // ---- condition evaluations: init sign (1), root polish (1), scan (npts - 1) ----
+    // ---- condition evaluations, ONE call site: init sign, root polish, the grid scan of an
+    // accepted step (ContinuousCallback, RayTracer.jl:357-358) and the Illinois root search
+    // on its interpolant. ph: 0 done, 1 single point (INIT / ROOT), 2 grid scan, 3 Illinois.
+    int ph = (mode == M_INIT || mode == M_ROOT) ? 1 : (scan ? 2 : 0);
+    int ip = 1;
     double last_c = cprev, last_th = 0.0;
     int last_s = sprev;
-    bool hit = false;
-    const int nc = (mode == M_INIT || mode == M_ROOT) ? 1 : (scan ? npts - 1 : 0);
+    double i_tha = 0.0, i_ca = 0.0, i_thb = 0.0, i_cb = 0.0, i_tr = 0.0, i_cg = 0.0;
+    int i_side = 0, i_it = 0;
+    bool hit = false, root_done = false;
+    const double inv_n = 1.0 / double(npts - 1);
 #pragma unroll 1
-    for (int ip = 1; ip <= nc; ++ip) {
+    while (ph != 0) {
+      const double th = (ph == 3) ? i_tr : double(ip) * inv_n;
       double ui[7];
-      double tc;
-      const double th = double(ip) / double(npts - 1);
+      hermite7(u, f, y, kk, hs, th, ui);
+      double tc = tau + th * hs;
       if (mode == M_INIT) {
 #pragma unroll
         for (int i = 0; i < 7; ++i) ui[i] = u[i];
@@ -555,19 +533,15 @@ __global__ __launch_bounds__(256) void propagate_kernel(const KParams P, const i
 #pragma unroll
         for (int i = 0; i < 7; ++i) ui[i] = y[i];
         tc = tau + hs;
-      } else {
-        hermite7(u, f, y, kk, hs, th, ui);
-        tc = tau + th * hs;
       }
       const double ci = condition(P, ui, tc);
       if (mode == M_INIT) {
         cprev = ci;
         sprev = isnan(ci) ? 0 : sgn(ci);
+        ph = 0;
         mode = M_STEP;
-        break;
-      }
-      if (mode == M_ROOT) {
-        // bracketed polish (Newton with the interpolant slope, then Illinois)
+      } else if (mode == M_ROOT) {
+        // bracketed polish on the true trajectory (Newton with the interpolant slope, then Illinois)
         s_root += 1;
         ++r_it;
         bool done = !(fabs(ci) > 1e-12);
@@ -581,46 +555,73 @@ __global__ __launch_bounds__(256) void propagate_kernel(const KParams P, const i
             r_t = tn;
           }
         }
-        if (done) {
-          const double tau_r = tau + hs;
-          const int a = affect(P, in, out, n, ray, y, tau_r, erg, ncross, max_crossings);
+        root_done = done;
+        ph = 0;
+      } else if (ph == 2) {
+        s_scan += 1;
+        if (isnan(ci)) {
+          last_s = 0;  // no resonance possible where |u7| < m_a
+        } else {
+          const int si = sgn(ci);
+          if (last_s != 0 && si != 0 && si != last_s) {
+            i_tha = last_th; i_ca = last_c; i_thb = th; i_cb = ci; i_cg = ci;
+            i_tr = i_tha - i_ca * (i_thb - i_tha) / (i_cb - i_ca);
+            i_side = 0;
+            i_it = 0;
+            ph = 3;
+          } else if (si != 0) {
+            last_s = si; last_c = ci; last_th = th;
+          }
+        }
+        if (ph == 2 && ++ip > npts - 1) ph = 0;
+      } else {  // ph == 3: Illinois on the interpolant inside (i_tha, i_thb]
+        s_interp += 1;
+        bool stop = ci == 0.0 || isnan(ci) || (i_thb - i_tha) < 1e-12;
+        if (!stop) {
+          if (sgn(ci) == sgn(i_ca)) { i_tha = i_tr; i_ca = ci; if (i_side == -1) i_cb *= 0.5; i_side = -1; }
+          else { i_thb = i_tr; i_cb = ci; if (i_side == 1) i_ca *= 0.5; i_side = 1; }
+          const double tn = i_tha - i_ca * (i_thb - i_tha) / (i_cb - i_ca);
+          if (tn == i_tr) stop = true;
+          else i_tr = tn;
+          if (++i_it >= 40) stop = true;
+        }
+        if (stop) {
+          // the sign change that opened this search was at grid point ip
+          const double thg = double(ip) * inv_n;
+          const double t_int = i_tr;
+          if (!(just_evented && t_int < 0.01)) {  // DiffEq repeat_nudge after an event
+            hit = true;
+            hroot = hs;
+            r_tha = last_th; r_ca = last_c; r_thb = thg; r_cb = i_cg;
+            r_slope = (i_cg - last_c) / (thg - last_th);
+            r_t = (t_int > last_th && t_int < thg) ? t_int : 0.5 * (last_th + thg);
+            r_side = 0;
+            r_it = 0;
+            post_c = i_cg;
+            post_s = sgn(i_cg);
+            dt = dtnext;
+            ph = 0;
+          } else {
+            last_s = sgn(i_cg); last_c = i_cg; last_th = thg;
+            ph = (++ip > npts - 1) ? 0 : 2;
+          }
+        }
+      }
+    }
+    if (hit) mode = M_ROOT;
+    if (root_done) {
+      const double tau_r = tau + hs;
+      const int a = affect(P, in, out, n, ray, y, tau_r, erg, ncross, max_crossings);
 #pragma unroll
-          for (int i = 0; i < 7; ++i) { u[i] = y[i]; f[i] = kk[i]; }
-          tau = tau_r;
-          cprev = post_c;  // the post-event side (DiffEq repeat_nudge): the root is not re-found
-          sprev = post_s;
-          just_evented = true;
-          mode = M_STEP;
-          if (a == 2) finish = ART_STATUS_CROSSING;
-          else if (photon && u[0] < P.rNS101) finish = ART_STATUS_HIT_NS;  // cb_r after the event
-          else if (iter >= P.maxiters) finish = ART_STATUS_MAXITERS;
-        }
-        break;
-      }
-      // ContinuousCallback scan of an accepted step (RayTracer.jl:357-358)
-      s_scan += 1;
-      if (isnan(ci)) { last_s = 0; continue; }  // no resonance possible where |u7| < m_a
-      const int si = sgn(ci);
-      if (last_s != 0 && si != 0 && si != last_s) {
-        int ne = 0;
-        const double t_int = illinois_interp(P, u, f, y, kk, tau, hs, last_th, th, last_c, ci, ne);
-        s_interp += ne;
-        if (!(just_evented && t_int < 0.01)) {  // DiffEq repeat_nudge after an event
-          hit = true;
-          mode = M_ROOT;
-          hroot = hs;
-          r_tha = last_th; r_ca = last_c; r_thb = th; r_cb = ci;
-          r_slope = (ci - last_c) / (th - last_th);
-          r_t = (t_int > last_th && t_int < th) ? t_int : 0.5 * (last_th + th);
-          r_side = 0;
-          r_it = 0;
-          post_c = ci;
-          post_s = si;
-          dt = dtnext;
-          break;
-        }
-      }
-      if (si != 0) { last_s = si; last_c = ci; last_th = th; }
+      for (int i = 0; i < 7; ++i) { u[i] = y[i]; f[i] = kk[i]; }
+      tau = tau_r;
+      cprev = post_c;  // the post-event side (DiffEq repeat_nudge): the root is not re-found
+      sprev = post_s;
+      just_evented = true;
+      mode = M_STEP;
+      if (a == 2) finish = ART_STATUS_CROSSING;
+      else if (photon && u[0] < P.rNS101) finish = ART_STATUS_HIT_NS;  // cb_r after the event
+      else if (iter >= P.maxiters) finish = ART_STATUS_MAXITERS;
     }
     if (scan && !hit) {
 #pragma unroll
@@ -661,6 +662,27 @@ __global__ __launch_bounds__(256) void propagate_kernel(const KParams P, const i
     unsigned long long x = v[k];
     for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off);
     if (lane == 0 && x) atomicAdd(&stats[k], x);
+  }
+}
+
+// Conversion probability of every recorded crossing (get_Prob_nonAD with Nc = 1,
+// MainRunner.jl:265), run right after the integrator on the same stream: keeping this
+// ~400-FLOP, rarely taken path out of the integrator loop saves it ~90 registers.
+__global__ __launch_bounds__(256) void crossing_prob_kernel(const KParams P, const int64_t n, const SegIn in,
+                                                            const SegOut out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int m = out.xcount[i] < out.cap ? out.xcount[i] : out.cap;
+  const double erg = in.erg[i];
+  for (int j = 0; j < m; ++j) {
+    double x[3], k[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      x[c] = out.xpos[(int64_t(c) * out.cap + j) * n + i];
+      k[c] = out.xk[(int64_t(c) * out.cap + j) * n + i];
+    }
+    const double dwc = out.xdw[int64_t(j) * n + i];
+    out.xp[int64_t(j) * n + i] = prob_nonad_single(P, x, k, erg * fabs(dwc));  // erg_inf_ini .* abs.(Δωc)
   }
 }
 
@@ -926,10 +948,14 @@ hipError_t launch_propagate(const KParams& P, int64_t n, const SegIn& in, const 
   const int grid = persistent_blocks(fn, n);
   if (grid_out) *grid_out = grid;
   if (P.integrator == ART_RK4)
-    hipLaunchKernelGGL(propagate_kernel<ART_RK4>, dim3(grid), dim3(256), 0, s, P, n, in, out, max_crossings, queue, stats);
-  else
-    hipLaunchKernelGGL(propagate_kernel<ART_VERN6>, dim3(grid), dim3(256), 0, s, P, n, in, out, max_crossings, queue,
+    hipLaunchKernelGGL(propagate_kernel<ART_RK4>, dim3(grid), dim3(BLOCK), 0, s, P, n, in, out, max_crossings, queue,
                        stats);
+  else
+    hipLaunchKernelGGL(propagate_kernel<ART_VERN6>, dim3(grid), dim3(BLOCK), 0, s, P, n, in, out, max_crossings, queue,
+                       stats);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess || !out.xcount) return e;
+  hipLaunchKernelGGL(crossing_prob_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, P, n, in, out);
   return hipGetLastError();
 }
 

@@ -1,0 +1,197 @@
+#!/usr/bin/env python3
+"""bench.py -- ray-steps/s (FP64) of the MI355X engine on BASELINE.json's workload.
+
+A "step" = one pass of the hot path over one batch: RT.propagate of every segment of the
+batch (RayTracer.jl:171-452: Vern6 + resonance scan + crossing polish + conversion
+probability at the crossing), the binned flux of the escaping photons (plot/flux.py:38-48)
+and, for N > 1, its RCCL all-reduce. Inputs are forward-tree roots sampled ON THE GPU with
+the restated find_samples_new (seed 1769, Philox keyed by global ray id) BEFORE the timed
+region, so they are resident in HBM when timing starts.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--rays R] [--config flat|gr]
+
+N > 1: launched by torch.distributed.run, one rank per GPU; the R rays are sharded in
+contiguous blocks (strong scaling of the fixed 1e7-ray batch named by BASELINE.json).
+Rank 0 prints ONE JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+
+PEAK_FP64_TFLOPS = 78.6  # MI355X FP64 vector (= FP64 matrix) dense peak, MI355X_MICROARCH / BASELINE.md §3
+PEAK_HBM_GBS = 8000.0
+
+CONFIGS = {
+    # BASELINE.json configs[1..2]: GJ dipole, flat space, m_a = 1e-5 eV, θm = 0.2, ωPul = 1, B0 = 1e14 G
+    "flat": dict(theta_m=0.2, mass_a=1e-5, flat=True),
+    # configs[3]: Schwarzschild GR (runner_GR_tasks.sh:10-14)
+    "gr": dict(theta_m=0.0, mass_a=1e-6, flat=False),
+}
+
+
+def flops_per_launch(stats, fl):
+    """Algorithmic FLOPs of one propagate launch from the kernel's own counters and the
+    instrumented per-operation counts (tools/flops.json, tools/count_flops.cpp)."""
+    att, root, scan, interp = stats["attempts"], stats["root_steps"], stats["scan_evals"], stats["interp_evals"]
+    per_scan = fl["hermite_point"] + fl["condition"]
+    return (att * fl["vern6_attempt"] + root * (fl["vern6_attempt"] + fl["condition"]) + scan * per_scan
+            + interp * per_scan + stats["init_rhs"] * fl["rhs_photon"]
+            + stats["rays"] * (fl["initial_state"] + fl["condition"] + fl["back_transform"]))
+
+
+def cpu_baseline(params, x0, k0, erg, seed, threads):
+    """The oracle (oracle/art_oracle.cpp, OpenMP over rays) on a bounded sample of the same
+    workload: the first rays of the same Philox-sampled forward-root batch, timed on this
+    box's host cores."""
+    import oracle as O
+    O.build()
+    po = O.make_params(**params)
+    n = erg.size
+    t0 = time.perf_counter()
+    r = O.propagate(po, x0, k0, erg, -1.0, -30.0, 1, max_crossings=-1, nthreads=threads)
+    dt = time.perf_counter() - t0
+    steps = int(r["n_accept"].sum())
+    return {"value": steps / dt, "unit": "ray-steps/s", "cores": threads, "kind": "port",
+            "sample": f"first {n} forward-root photon segments of the seed-{seed} batch, {steps} accepted Vern6 "
+                      f"steps in {dt:.1f} s; oracle restatement (C++/OpenMP, dual-number gradients like ForwardDiff)"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--rays", type=int, default=10_000_000)
+    ap.add_argument("--config", default="flat", choices=sorted(CONFIGS))
+    ap.add_argument("--integrator", default="vern6", choices=["vern6", "rk4"])
+    ap.add_argument("--seed", type=int, default=1769)
+    ap.add_argument("--nbins", type=int, default=50)
+    ap.add_argument("--cpu-rays", type=int, default=int(os.environ.get("ART_CPU_RAYS", "200000")))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    import adiabatic_raytracer_amd as A
+    from adiabatic_raytracer_amd import Engine
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    params = A.Params(integrator=args.integrator, **CONFIGS[args.config])
+    eng = Engine(params, device=local)
+    # contiguous shard of the global batch; Philox keyed by global ray id -> GPU-count independent
+    lo = args.rays * rank // world
+    hi = args.rays * (rank + 1) // world
+    n = hi - lo
+    t_s = time.perf_counter()
+    inp = eng.forward_roots(n, seed=args.seed, ray_offset=lo)
+    torch.cuda.synchronize()
+    sample_s = time.perf_counter() - t_s
+    out = eng.alloc_out(n, capacity=1)
+    hist = torch.zeros(2 * args.nbins, dtype=torch.float64, device=eng.device)
+
+    def one_step():
+        eng.propagate(inp, out, max_crossings=-1)
+        hist.zero_()
+        eng.flux_histogram(out, inp["species"], None, args.nbins, hist)
+        if world > 1:
+            dist.all_reduce(hist)  # the only collective: the binned flux (RCCL over xGMI)
+
+    for _ in range(args.warmup):
+        one_step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    kernel_ms, accepted, stats_last = [], 0, None
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        one_step()
+        kernel_ms.append(eng.kernel_ms())  # HIP events on the propagate kernel's stream
+        st = A.raytracer.last_stats()
+        accepted += st["accepted"]
+        stats_last = st
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    # whole-job aggregates: Σ ray-steps over ranks / max wall time over ranks
+    agg = torch.tensor([float(accepted), elapsed, float(n)], dtype=torch.float64, device=eng.device)
+    tmax = agg[1].clone()
+    if world > 1:
+        dist.all_reduce(agg[0:1])
+        dist.all_reduce(agg[2:3])
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+    total_steps, total_rays, t_max = float(agg[0]), int(agg[2]), float(tmax)
+
+    if rank == 0:
+        fl = json.load(open(os.path.join(HERE, "tools", "flops.json")))
+        kms = float(np.mean(kernel_ms))
+        fpl = flops_per_launch(stats_last, fl)
+        achieved = fpl / (kms * 1e-3) / 1e12
+        st = out["status"].cpu().numpy()
+        traffic = None
+        pmc_path = os.path.join(HERE, "profiles", "pmc_summary.json")
+        if os.path.exists(pmc_path):
+            pm = json.load(open(pmc_path))
+            if pm.get("workload") == f"{args.config}:{n}":
+                traffic = pm.get("hbm_bytes_per_launch")
+        line = {
+            "metric": "ray-steps/sec (FP64), 10^7-ray GJ-dipole batch",
+            "value": total_steps / t_max,
+            "unit": "ray-steps/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": t_max / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic: forward-tree roots sampled on the GPU by the restated find_samples_new (Philox seed 1769)",
+            "config": {"workload": f"{total_rays} photon segments, GJ dipole, "
+                                   f"{'flat space' if params.flat else 'Schwarzschild GR'}, {args.integrator}",
+                       "baseline_config": "configs[2] (1e7 rays, sharded over the GPUs)" if args.rays == 10_000_000
+                       else f"{args.rays} rays",
+                       "m_a_eV": params.mass_a, "theta_m": params.theta_m, "omega_pul": params.omega_pul,
+                       "B0_G": params.B0, "rNS_km": params.rNS, "abstol": params.abstol, "reltol": params.reltol,
+                       "interp_points": params.interp_points, "parallelism": f"rays sharded x{world}"},
+            "roofline": {"bound": "fp64-valu", "achieved": achieved, "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
+                         "frac": achieved / PEAK_FP64_TFLOPS, "traffic": traffic,
+                         "kernel": "propagate_kernel<Vern6>", "kernel_ms": kms,
+                         "flops_per_launch": fpl, "flops_per_ray_step": fpl / stats_last["accepted"],
+                         "note": "FP64 VALU-bound (state in VGPRs, ~1 B of HBM per ray-step); peak = 78.6 TFLOP/s "
+                                 "FP64 (vector = matrix dense peak). FLOPs from the kernel's counters x "
+                                 "tools/flops.json (instrumented restatement)."},
+            "kernel_stats": stats_last,
+            "status_counts": np.bincount(st, minlength=5).tolist(),
+            "ic_sampling_s": sample_s,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            threads = int(os.environ.get("ART_CPU_THREADS", str(min(16, os.cpu_count() or 1))))
+            m = min(args.cpu_rays, n)
+            xs = inp["x0"].view(3, n)[:, :m].cpu().numpy().reshape(-1)
+            ks = inp["k0"].view(3, n)[:, :m].cpu().numpy().reshape(-1)
+            line["cpu_baseline"] = cpu_baseline(CONFIGS[args.config] | {"integrator": 0}, xs, ks,
+                                                inp["erg"][:m].cpu().numpy(), args.seed, threads)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

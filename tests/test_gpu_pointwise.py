@@ -55,7 +55,8 @@ def test_condition_matches_oracle(cfg, torch_mod, oracle_lib):
     both = ~np.isnan(ref)
     assert np.array_equal(np.isnan(c), np.isnan(ref))
     err = np.abs(c[both] - ref[both]) / (np.abs(ref[both]) + 1e-12)
-    assert err.max() < 1e-9, err.max()
+    j = np.flatnonzero(both)[np.argmax(err)]
+    assert err.max() < 1e-9, (err.max(), int(j), c[j], ref[j], U[:, j].tolist(), tau[j])
 
 
 @pytest.mark.parametrize("cfg", sorted(CONFIGS))

@@ -52,4 +52,4 @@ for name, kw in {"flat_tm0.2": dict(theta_m=0.2, mass_a=1e-5, flat=True),
                            "ray_steps_per_s": r["stats"]["accepted"] / (r["kernel_ms"] * 1e-3)}
     print(name, "timing", json.dumps(res[name]["timing"]), flush=True)
 os.makedirs("gpurun_out", exist_ok=True)
-json.dump(res, open("gpurun_out/quick.json", "w"), indent=1)
+json.dump(res, open(f"gpurun_out/quick{os.environ.get('QUICK_TAG', '')}.json", "w"), indent=1)
