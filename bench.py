@@ -46,6 +46,15 @@ def flops_per_launch(stats, fl):
             + stats["rays"] * (fl["initial_state"] + fl["condition"] + fl["back_transform"]))
 
 
+# Algorithmic HBM bytes of one propagate launch. Per segment: inputs x0, k0
+# (2 x 3 f64), erg, dw, ln_t0 (f64), species (i8) = 73 B; outputs x_end, k_end (2 x 3 f64),
+# u7, tau (f64), status, n_accept, n_reject, n_cross (i32) = 80 B. Per recorded crossing:
+# position, k (2 x 3 f64), t, dw (f64) written = 64 B; the probability kernel re-reads
+# position, k, dw (56 B) and writes P (8 B).
+BYTES_PER_SEGMENT = 73 + 80
+BYTES_PER_CROSSING = 64 + 56 + 8
+
+
 def cpu_baseline(params, x0, k0, erg, seed, threads):
     """The oracle (oracle/art_oracle.cpp, OpenMP over rays) on a bounded sample of the same
     workload: the first rays of the same Philox-sampled forward-root batch, timed on this
@@ -73,7 +82,7 @@ def main():
     ap.add_argument("--integrator", default="vern6", choices=["vern6", "rk4"])
     ap.add_argument("--seed", type=int, default=1769)
     ap.add_argument("--nbins", type=int, default=50)
-    ap.add_argument("--cpu-rays", type=int, default=int(os.environ.get("ART_CPU_RAYS", "200000")))
+    ap.add_argument("--cpu-rays", type=int, default=int(os.environ.get("ART_CPU_RAYS", "500000")))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
@@ -82,6 +91,7 @@ def main():
 
     import adiabatic_raytracer_amd as A
     from adiabatic_raytracer_amd import Engine
+    from adiabatic_raytracer_amd.shard import allreduce_flux, reduce_totals, shard_range
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -93,8 +103,7 @@ def main():
     params = A.Params(integrator=args.integrator, **CONFIGS[args.config])
     eng = Engine(params, device=local)
     # contiguous shard of the global batch; Philox keyed by global ray id -> GPU-count independent
-    lo = args.rays * rank // world
-    hi = args.rays * (rank + 1) // world
+    lo, hi = shard_range(args.rays, rank, world)
     n = hi - lo
     t_s = time.perf_counter()
     inp = eng.forward_roots(n, seed=args.seed, ray_offset=lo)
@@ -107,8 +116,7 @@ def main():
         eng.propagate(inp, out, max_crossings=-1)
         hist.zero_()
         eng.flux_histogram(out, inp["species"], None, args.nbins, hist)
-        if world > 1:
-            dist.all_reduce(hist)  # the only collective: the binned flux (RCCL over xGMI)
+        allreduce_flux(hist, world)  # the only data-path collective: the binned flux (RCCL over xGMI)
 
     for _ in range(args.warmup):
         one_step()
@@ -130,13 +138,7 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     # whole-job aggregates: Σ ray-steps over ranks / max wall time over ranks
-    agg = torch.tensor([float(accepted), elapsed, float(n)], dtype=torch.float64, device=eng.device)
-    tmax = agg[1].clone()
-    if world > 1:
-        dist.all_reduce(agg[0:1])
-        dist.all_reduce(agg[2:3])
-        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-    total_steps, total_rays, t_max = float(agg[0]), int(agg[2]), float(tmax)
+    total_steps, t_max, total_rays = reduce_totals(accepted, elapsed, n, world, device=eng.device)
 
     if rank == 0:
         fl = json.load(open(os.path.join(HERE, "tools", "flops.json")))
@@ -150,6 +152,8 @@ def main():
             pm = json.load(open(pmc_path))
             if pm.get("workload") == f"{args.config}:{n}":
                 traffic = pm.get("hbm_bytes_per_launch")
+        ncross = int((out["n_cross"].clamp(max=out["capacity"])).sum().item())
+        alg_bytes = n * BYTES_PER_SEGMENT + ncross * BYTES_PER_CROSSING
         line = {
             "metric": "ray-steps/sec (FP64), 10^7-ray GJ-dipole batch",
             "value": total_steps / t_max,
@@ -176,7 +180,10 @@ def main():
                          "flops_per_launch": fpl, "flops_per_ray_step": fpl / stats_last["accepted"],
                          "note": "FP64 VALU-bound (state in VGPRs, ~1 B of HBM per ray-step); peak = 78.6 TFLOP/s "
                                  "FP64 (vector = matrix dense peak). FLOPs from the kernel's counters x "
-                                 "tools/flops.json (instrumented restatement)."},
+                                 "tools/flops.json (instrumented restatement).",
+                         "hbm": {"algorithmic_bytes_per_launch": alg_bytes,
+                                 "achieved_GBs": alg_bytes / (kms * 1e-3) / 1e9, "peak_GBs": PEAK_HBM_GBS,
+                                 "frac": alg_bytes / (kms * 1e-3) / 1e9 / PEAK_HBM_GBS}},
             "kernel_stats": stats_last,
             "status_counts": np.bincount(st, minlength=5).tolist(),
             "ic_sampling_s": sample_s,

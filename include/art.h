@@ -184,8 +184,9 @@ int art_sample_conversion_points_device(const art_params* p, double max_r, uint6
 
 /* ---- binned flux (plot/flux.py:38-48): histogram of the final momentum azimuth
  * φf = atan2(ky, kx) over [-π, π) in nbins bins, separately for axions (row 0) and
- * photons (row 1), weight w[i] (NULL = 1), only rays with status SUCCESS whose final
- * radius exceeds 1.1 rNS (is_final, MainRunner.jl:207-209). hist (2*nbins, device,
+ * photons (row 1), weight w[i] (NULL = 1), only rays that ended without a crossing
+ * (status != ART_STATUS_CROSSING) and whose final radius exceeds 1.1 rNS -- the
+ * reference's is_final (MainRunner.jl:200-207), whatever the retcode. hist (2*nbins, device,
  * float64) is ACCUMULATED into (zero it first). */
 int art_flux_histogram_device(const art_params* p, int64_t n, const double* x_end,
                               const double* k_end, const int32_t* status,

@@ -12,5 +12,5 @@ for grp in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU
            "SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_TRANS_F64" \
            "SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_INST_ANY SQ_WAIT_ANY"; do
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --kernel-trace --pmc $grp -d "$OUT/pass$i" -o pass$i --output-format csv -- $BENCH > "$OUT/pass$i.log" 2>&1 || echo "pass $i ($grp) failed: $?"
+  timeout -k 10 300 rocprofv3 --kernel-trace --pmc $grp -d "$OUT/pass$i" -o pass$i --output-format csv -- $BENCH > "$OUT/pass$i.log" 2>&1 || { echo "pass $i ($grp) failed: $?"; exit 1; }
 done
