@@ -88,7 +88,10 @@ int validate(const art_params* p) {
   return ART_OK;
 }
 
-hipStream_t pick(DeviceCtx* c, void* stream) { return stream ? (hipStream_t)stream : c->stream; }
+// *_device entry points run on the caller's stream exactly as given: NULL is the HIP null
+// stream (torch's default stream), so the library orders correctly with the caller's
+// work. Only the *_host entry points use the library's own stream.
+hipStream_t pick(DeviceCtx*, void* stream) { return (hipStream_t)stream; }
 
 int propagate_device_impl(const art_params* p, int64_t n, const double* x0, const double* k0, const double* erg,
                           const double* dw, const double* ln_t0, const int8_t* species, int32_t max_crossings,

@@ -26,7 +26,8 @@
  *   - *_host entry points take host pointers and do H2D/kernel/D2H on the library's
  *     own HIP stream (a Julia ccall passes Vector/Matrix pointers straight through).
  *     *_device entry points take device (HBM) pointers plus a hipStream_t passed as
- *     void* (NULL = the library stream); they are asynchronous on that stream.
+ *     void*, used exactly as given (NULL = the HIP null stream, which is also
+ *     PyTorch's default stream); they are asynchronous on that stream.
  *   - Return 0 on success or a negative ART_E* code; art_last_error() describes it.
  *   - Thread safety: calls are serialized by an internal mutex; one device per call
  *     (art_set_device).

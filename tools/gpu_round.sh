@@ -11,3 +11,6 @@ cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 timeout -k 10 240 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_bench -o bench --output-format csv \
   -- python3 bench.py --no-cpu-baseline > gpurun_out/bench_prof.json 2> gpurun_out/bench_prof.err || exit $?
 timeout -k 10 240 python3 bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err || exit $?
+[ -n "$ART_PMC" ] && { bash tools/pmc_passes.sh gpurun_out/pmc 10000000 > gpurun_out/pmc.log 2>&1 || exit $?; }
+[ -n "$ART_EXTRA" ] && { timeout -k 10 200 python3 $ART_EXTRA > gpurun_out/extra.log 2>&1 || exit $?; }
+exit 0
