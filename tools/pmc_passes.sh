@@ -6,10 +6,13 @@
 OUT=${1:-gpurun_out/pmc}; RAYS=${2:-10000000}
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p "$OUT/calib" "$OUT/kernel"
-timeout -k 10 120 rocprofv3 --kernel-trace --pmc FETCH_SIZE WRITE_SIZE -d "$OUT/calib" -o calib \
-  --output-format csv -- tools/build/calib_hbm > "$OUT/calib_truth.json" 2> "$OUT/calib.log" || exit $?
+# FETCH_SIZE and WRITE_SIZE cannot share a pass on gfx950 ("exceeds the capabilities of the hardware")
+for c in FETCH_SIZE WRITE_SIZE; do
+  timeout -k 10 120 rocprofv3 --kernel-trace --pmc $c -d "$OUT/calib/$c" -o calib \
+    --output-format csv -- tools/build/calib_hbm > "$OUT/calib_truth.json" 2> "$OUT/calib_$c.log" || exit $?
+done
 i=0
-for grp in "FETCH_SIZE WRITE_SIZE" \
+for grp in "FETCH_SIZE" "WRITE_SIZE" \
            "SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE" \
            "SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_TRANS_F64" \
            "SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_INST_ANY SQ_WAIT_ANY"; do
