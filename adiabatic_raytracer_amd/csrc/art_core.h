@@ -122,7 +122,10 @@ inline KParams make_kparams(const art_params& p) {
 // on r <= 10 km, the keyword default that hot-path callers never override (:455).
 template <class T>
 __host__ __device__ inline void metric_tr(const T& r, double rs, T& gtt, T& grr) {
-  if (r <= 10.0) {
+  if (rs == 0.0) {  // flat space: exactly what both branches below give for rs = 0
+    grr = 1.0;
+    gtt = -1.0;
+  } else if (r <= 10.0) {
     const T rsp = rs * (r * r * r) * 1e-3;  // rs (r/10)^3 (:463)
     grr = 1.0 - r * r * rsp * 1e-3;
     const T D = 3.0 * msqrt(1.0 - rsp * 0.1) - msqrt(grr);
@@ -135,7 +138,12 @@ __host__ __device__ inline void metric_tr(const T& r, double rs, T& gtt, T& grr)
 
 template <class T>
 __host__ __device__ inline void metric_tr_d(const T& r, double rs, T& gtt, T& grr, T& dgtt, T& dgrr) {
-  if (r <= 10.0) {
+  if (rs == 0.0) {  // flat space (wave-uniform branch): no divisions
+    grr = 1.0;
+    gtt = -1.0;
+    dgrr = 0.0;
+    dgtt = 0.0;
+  } else if (r <= 10.0) {
     const T r2 = r * r;
     const T rsp = rs * (r2 * r) * 1e-3;
     grr = 1.0 - r2 * rsp * 1e-3;                  // 1 - rs r^5 / 1e6
@@ -386,28 +394,29 @@ __host__ __device__ inline void hamiltonian_full(const KParams& P, const T* x, c
 // ---------------------------------------------------------------------------
 // Resonance condition of propagate's ContinuousCallback (RayTracer.jl:254-298,
 // thick_surface = true): rescale w onto the axion mass shell with E = u[7], then
-// H_photon/E² with ωp at t = e^τ (zeroIn = true), k∥ and the raw radius.
-// NaN when |u7| has dropped below m_a (the reference would raise DomainError there).
+// H_photon/E² with ωp at t (zeroIn = true), k∥ and the raw radius.
+// The reference computes w' = w √nrm, nrm = (-E² g^tt - m_a²)/(g^rr w_r² + g^θθ w_θ² +
+// g^φφ w_φ²) (:281-282), then ½[g^tt E² + Σ g^ii w'_i² + ωp²(1 - g^rr k∥(w')²/E²)]/E².
+// By construction Σ g^ii w'_i² = nrm·den = -E² g^tt - m_a², so the kinetic part is exactly
+// -m_a², and k∥(w')² = nrm·k∥(w)². This evaluates that closed form: no square root, four
+// divisions, the same value up to rounding. It is NaN where √nrm is (nrm < 0: |u7| has
+// dropped below m_a, where the reference would raise DomainError).
 template <class T>
-__host__ __device__ inline T condition(const KParams& P, const T* u, const T& tau) {
-  const T t0 = mexp(tau);
+__host__ __device__ inline T condition_t(const KParams& P, const T* u, const T& t0) {
   const T r = u[0];
   T gtt, grr;
   metric_tr(r, P.rs_eff, gtt, grr);
-  T st, ct, sp, cp;
+  T st, ct;
   msincos(u[1], st, ct);
+  const T E2 = u[6] * u[6];
+  const T num = -E2 * gtt - P.mass_a2;
+  if (num < 0.0) return T(NAN);
   const T ir = 1.0 / r;
   const T ir2 = ir * ir;
-  const T iast = 1.0 / mabs(st);
-  const T gpp = ir2 * iast * iast;
-  const T E2 = u[6] * u[6];
-  const T nrm = (-E2 * gtt - P.mass_a2) / (grr * u[3] * u[3] + ir2 * u[4] * u[4] + gpp * u[5] * u[5]);
-  const T s = msqrt(nrm);
-  const T w0 = u[3] * s, w1 = u[4] * s, w2 = u[5] * s;
-  const T ksqr = gtt * E2 + grr * w0 * w0 + ir2 * w1 * w1 + gpp * w2 * w2;
   T wp2 = 0.0;
-  T kpar2 = 0.0;
+  T X = 0.0;  // g^rr k∥(w')²/E²
   if (r > P.rNS || !P.isotropic) {
+    T sp, cp;
     msincos(u[2] - P.omega * t0, sp, cp);
     const DipoleAng<T> d = dipole_ang(P, st, ct, sp, cp);
     if (r > P.rNS) {  // zeroIn = true
@@ -418,11 +427,20 @@ __host__ __device__ inline T condition(const KParams& P, const T* u, const T& ta
       }
     }
     if (!P.isotropic) {
-      const T p = 2.0 * msqrt(grr) * w0 * d.a1 + ir * (w1 * d.a2 + w2 * d.a3 * iast);
-      kpar2 = p * p / (4.0 * d.a1 * d.a1 + d.a2 * d.a2 + d.a3 * d.a3);
+      const T iast = 1.0 / mabs(st);
+      const T den = grr * u[3] * u[3] + ir2 * (u[4] * u[4] + iast * iast * u[5] * u[5]);
+      const T sq = (P.rs_eff == 0.0) ? T(1.0) : msqrt(grr);
+      const T p = 2.0 * sq * u[3] * d.a1 + ir * (u[4] * d.a2 + u[5] * d.a3 * iast);
+      const T beta = 4.0 * d.a1 * d.a1 + d.a2 * d.a2 + d.a3 * d.a3;
+      X = grr * num * p * p / (den * beta * E2);
     }
   }
-  return 0.5 * (ksqr + wp2 * (1.0 - grr * kpar2 / E2)) / E2;
+  return 0.5 * (wp2 * (1.0 - X) - P.mass_a2) / E2;
+}
+
+template <class T>
+__host__ __device__ inline T condition(const KParams& P, const T* u, const T& tau) {
+  return condition_t(P, u, mexp(tau));
 }
 
 // ---------------------------------------------------------------------------

@@ -36,13 +36,15 @@ CONFIGS = {
 }
 
 
-def flops_per_launch(stats, fl):
+def flops_per_launch(stats, fl, integrator="vern6"):
     """Algorithmic FLOPs of one propagate launch from the kernel's own counters and the
-    instrumented per-operation counts (tools/flops.json, tools/count_flops.cpp)."""
+    instrumented per-operation counts for this configuration (tools/flops.json, made by
+    tools/count_flops.cpp from the same art_core.h templates the kernel runs)."""
     att, root, scan, interp = stats["attempts"], stats["root_steps"], stats["scan_evals"], stats["interp_evals"]
-    per_scan = fl["hermite_point"] + fl["condition"]
-    return (att * fl["vern6_attempt"] + root * (fl["vern6_attempt"] + fl["condition"]) + scan * per_scan
-            + interp * per_scan + stats["init_rhs"] * fl["rhs_photon"]
+    step = fl["rk4_attempt"] if integrator == "rk4" else fl["vern6_attempt"]
+    return (att * step + root * (step + fl["condition"])
+            + scan * (fl["hermite_point"] + fl["condition_scan_point"])
+            + interp * (fl["hermite_point"] + fl["condition"]) + stats["init_rhs"] * fl["rhs_photon"]
             + stats["rays"] * (fl["initial_state"] + fl["condition"] + fl["back_transform"]))
 
 
@@ -141,9 +143,9 @@ def main():
     total_steps, t_max, total_rays = reduce_totals(accepted, elapsed, n, world, device=eng.device)
 
     if rank == 0:
-        fl = json.load(open(os.path.join(HERE, "tools", "flops.json")))
+        fl = json.load(open(os.path.join(HERE, "tools", "flops.json")))[args.config]
         kms = float(np.mean(kernel_ms))
-        fpl = flops_per_launch(stats_last, fl)
+        fpl = flops_per_launch(stats_last, fl, args.integrator)
         achieved = fpl / (kms * 1e-3) / 1e12
         st = out["status"].cpu().numpy()
         traffic = None
@@ -153,6 +155,10 @@ def main():
             if pm.get("workload") == f"{args.config}:{n}":
                 traffic = pm.get("hbm_bytes_per_launch")
         ncross = int((out["n_cross"].clamp(max=out["capacity"])).sum().item())
+        att = (out["n_accept"] + out["n_reject"]).double()
+        q = torch.quantile(att[:min(n, 1 << 24)], torch.tensor([0.5, 0.99, 0.999], dtype=torch.float64,
+                                                               device=att.device)).tolist()
+        attempt_dist = {"mean": float(att.mean()), "p50": q[0], "p99": q[1], "p999": q[2], "max": float(att.max())}
         alg_bytes = n * BYTES_PER_SEGMENT + ncross * BYTES_PER_CROSSING
         line = {
             "metric": "ray-steps/sec (FP64), 10^7-ray GJ-dipole batch",
@@ -176,7 +182,7 @@ def main():
                        "interp_points": params.interp_points, "parallelism": f"rays sharded x{world}"},
             "roofline": {"bound": "fp64-valu", "achieved": achieved, "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
                          "frac": achieved / PEAK_FP64_TFLOPS, "traffic": traffic,
-                         "kernel": "propagate_kernel<Vern6>", "kernel_ms": kms,
+                         "kernel": f"propagate_kernel<{'RK4' if args.integrator == 'rk4' else 'Vern6'}>", "kernel_ms": kms,
                          "flops_per_launch": fpl, "flops_per_ray_step": fpl / stats_last["accepted"],
                          "note": "FP64 VALU-bound (state in VGPRs, ~1 B of HBM per ray-step); peak = 78.6 TFLOP/s "
                                  "FP64 (vector = matrix dense peak). FLOPs from the kernel's counters x "
@@ -186,6 +192,7 @@ def main():
                                  "frac": alg_bytes / (kms * 1e-3) / 1e9 / PEAK_HBM_GBS}},
             "kernel_stats": stats_last,
             "status_counts": np.bincount(st, minlength=5).tolist(),
+            "attempts_per_ray": attempt_dist,
             "ic_sampling_s": sample_s,
         }
         if world == 1 and not args.no_cpu_baseline:

@@ -56,11 +56,11 @@ long long count(F f) {
   return OC::n;
 }
 
-int main() {
+static void emit(bool flat, bool last) {
   art_params p{};
   p.theta_m = 0.2; p.omega_pul = 1.0; p.B0 = 1e14; p.rNS = 10.0; p.mass_ns = 1.0; p.mass_a = 1e-5; p.g_agg = 1e-12;
   p.bndry_lyr = -1.0; p.ln_t_end = 0.0; p.abstol = 1e-6; p.reltol = 1e-7; p.dtmin = 1e-13; p.maxiters = 100000;
-  p.flat = 1; p.isotropic = 0; p.melrose = 1; p.integrator = 0; p.n_fixed = 1000; p.interp_points = 50;
+  p.flat = flat ? 1 : 0; p.isotropic = 0; p.melrose = 1; p.integrator = 0; p.n_fixed = 1000; p.interp_points = 50;
   KParams K = make_kparams(p);
   // a typical exterior photon state (r > 1.01 rNS: all seven components computed)
   OC u[7] = {OC(20.0), OC(1.1), OC(0.3), OC(0.8), OC(5.0), OC(3.0), OC(-1.00000027e-5)};
@@ -68,6 +68,8 @@ int main() {
   const long long f_rhs = count([&] { rhs_photon(K, u, tau, 1.00000027e-5, du); });
   const long long f_rhs_ax = count([&] { rhs_axion(K, u, tau, 1.00000027e-5, du); });
   const long long f_cond = count([&] { (void)condition(K, u, tau); });
+  // a grid point of the scan: condition at t from the geometric recurrence (t *= q: 1 FLOP)
+  const long long f_cond_scan = count([&] { (void)condition_t(K, u, OC(2e-5)); }) + 1;
   // cubic Hermite point (art_kernels.hip hermite7): 4 setup + 7 x 10
   OC u1[7], f0[7], f1[7], out[7], h(0.01), th(0.3);
   for (int i = 0; i < 7; ++i) { u1[i] = u[i]; f0[i] = du[i]; f1[i] = du[i]; }
@@ -91,12 +93,20 @@ int main() {
   OC pos[3] = {OC(15.0), OC(3.0), OC(4.0)}, kp[3] = {OC(1e-6), OC(2e-6), OC(-1e-6)};
   const long long f_prob = count([&] { (void)prob_nonad_single(K, pos, kp, OC(1.00000027e-5)); });
   std::printf(
-      "{\n  \"convention\": \"+,-,*,/,sqrt,exp,pow = 1 FLOP; sincos = 2; FMA = 2; abs/sign/compare/select = 0\",\n"
-      "  \"rhs_photon\": %lld,\n  \"rhs_axion\": %lld,\n  \"condition\": %lld,\n  \"hermite_point\": %lld,\n"
-      "  \"vern6_stage_glue\": %lld,\n  \"vern6_error_norm\": %lld,\n  \"controller\": %lld,\n"
-      "  \"rk4_stage_glue\": %lld,\n  \"initial_state\": %lld,\n  \"back_transform\": %lld,\n"
-      "  \"prob_nonad\": %lld,\n  \"vern6_attempt\": %lld,\n  \"rk4_attempt\": %lld\n}\n",
-      f_rhs, f_rhs_ax, f_cond, f_herm, f_glue_v6, f_err, f_ctrl, f_glue_rk4, f_init, f_back, f_prob,
-      8 * f_rhs + f_glue_v6 + f_err + f_ctrl, 4 * f_rhs + f_glue_rk4);
+      "  \"%s\": {\n    \"rhs_photon\": %lld,\n    \"rhs_axion\": %lld,\n    \"condition\": %lld,\n"
+      "    \"condition_scan_point\": %lld,\n    \"hermite_point\": %lld,\n"
+      "    \"vern6_stage_glue\": %lld,\n    \"vern6_error_norm\": %lld,\n    \"controller\": %lld,\n"
+      "    \"rk4_stage_glue\": %lld,\n    \"initial_state\": %lld,\n    \"back_transform\": %lld,\n"
+      "    \"prob_nonad\": %lld,\n    \"vern6_attempt\": %lld,\n    \"rk4_attempt\": %lld\n  }%s\n",
+      flat ? "flat" : "gr", f_rhs, f_rhs_ax, f_cond, f_cond_scan, f_herm, f_glue_v6, f_err, f_ctrl, f_glue_rk4,
+      f_init, f_back, f_prob, 8 * f_rhs + f_glue_v6 + f_err + f_ctrl, 4 * f_rhs + f_glue_rk4, last ? "" : ",");
+}
+
+int main() {
+  std::printf("{\n  \"convention\": \"+,-,*,/,sqrt,exp,pow = 1 FLOP; sincos = 2; FMA = 2; "
+              "abs/sign/compare/select = 0\",\n");
+  emit(true, false);
+  emit(false, true);
+  std::printf("}\n");
   return 0;
 }
