@@ -53,6 +53,8 @@ SIGNATURES = {
     "art_sample_conversion_points_host": (C.c_int, [_P, _d, _u64, _i64, _i64, _v, _v, _v, _v, _v, _v]),
     "art_sample_conversion_points_device": (C.c_int, [_P, _d, _u64, _i64, _i64, _v, _v, _v, _v, _v, _v, _v]),
     "art_flux_histogram_device": (C.c_int, [_P, _i64, _v, _v, _v, _v, _v, _i32, _v, _v]),
+    "art_event_weight_host": (C.c_int, [_P, _d, _d, _d, _i64, _v, _v, _v, _v]),
+    "art_event_weight_device": (C.c_int, [_P, _d, _d, _d, _i64, _v, _v, _v, _v, _v]),
     "art_eval_rhs_device": (C.c_int, [_P, _i64, _v, _v, _v, _v, _v, _v]),
     "art_eval_hamiltonian_device": (C.c_int, [_P, _i64, _v, _v, _v, _v, _v, _v, _v, _v, _v]),
     "art_eval_condition_device": (C.c_int, [_P, _i64, _v, _v, _v, _v]),

@@ -375,6 +375,47 @@ int art_sample_conversion_points_host(const art_params* p, double max_r, uint64_
   return ART_OK;
 }
 
+int art_event_weight_device(const art_params* p, double max_r, double rho_dm, double mcmc_weight, int64_t n,
+                            const double* x, const double* k_init, const double* vifty, double* out, void* stream) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  int rc = validate(p);
+  if (rc) return rc;
+  if (n == 0) return ART_OK;
+  if (!x || !k_init || !vifty || !out) return fail(ART_E_INVALID, "NULL buffer");
+  DeviceCtx* c;
+  if ((rc = current_ctx(&c))) return rc;
+  HIP_OK(art::launch_event_weight(art::make_kparams(*p), n, x, k_init, vifty, max_r, rho_dm, mcmc_weight, out,
+                                  pick(c, stream)));
+  return ART_OK;
+}
+
+int art_event_weight_host(const art_params* p, double max_r, double rho_dm, double mcmc_weight, int64_t n,
+                          const double* x, const double* k_init, const double* vifty, double* out) {
+  int rc;
+  DeviceCtx* c;
+  void* d;
+  const size_t nd = (size_t)n;
+  if (n == 0) return ART_OK;
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if ((rc = current_ctx(&c))) return rc;
+    if ((rc = pool_get(c, 5, nd * 14 * sizeof(double), &d))) return rc;
+    double* dd = (double*)d;
+    hipStream_t s = c->stream;
+    HIP_OK(hipMemcpyAsync(dd, x, nd * 3 * sizeof(double), hipMemcpyHostToDevice, s));
+    HIP_OK(hipMemcpyAsync(dd + 3 * nd, k_init, nd * 3 * sizeof(double), hipMemcpyHostToDevice, s));
+    HIP_OK(hipMemcpyAsync(dd + 6 * nd, vifty, nd * 3 * sizeof(double), hipMemcpyHostToDevice, s));
+  }
+  double* dd = (double*)d;
+  if ((rc = art_event_weight_device(p, max_r, rho_dm, mcmc_weight, n, dd, dd + 3 * nd, dd + 6 * nd, dd + 9 * nd,
+                                    c->stream)))
+    return rc;
+  std::lock_guard<std::mutex> lk(g_mu);
+  HIP_OK(hipMemcpyAsync(out, dd + 9 * nd, nd * 5 * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  HIP_OK(hipStreamSynchronize(c->stream));
+  return ART_OK;
+}
+
 int art_flux_histogram_device(const art_params* p, int64_t n, const double* x_end, const double* k_end,
                               const int32_t* status, const int8_t* species, const double* w, int32_t nbins,
                               double* hist, void* stream) {

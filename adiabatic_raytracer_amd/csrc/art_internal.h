@@ -35,6 +35,8 @@ hipError_t launch_eval_rhs(const KParams& P, int64_t n, const double* u, const d
 hipError_t launch_eval_hamiltonian(const KParams& P, int64_t n, const double* x, const double* k, const double* T,
                                    const double* E, double* H, double* dHdx, double* dHdk, double* dHdT,
                                    hipStream_t s);
+hipError_t launch_event_weight(const KParams& P, int64_t n, const double* x, const double* k, const double* v,
+                               double maxR, double rho, double mcmc, double* out, hipStream_t s);
 hipError_t launch_eval_condition(const KParams& P, int64_t n, const double* u, const double* tau, double* out,
                                  hipStream_t s);
 }  // namespace art

@@ -14,6 +14,7 @@
 #include <hip/hip_runtime.h>
 
 #include "art_core.h"
+#include "art_event.h"
 #include "art_internal.h"
 
 namespace art {
@@ -288,7 +289,9 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
   int ray = -1;
   bool photon = true;
   double erg = 0.0;
-  double u[7], f[7], tau = 0.0, dt = 0.0, qold = 1e-4;
+  // qpow = qold^(1/15) of the PI controller, updated only when qold changes (on accept)
+  const double qpow_init = pow(1e-4, 1.0 / 15.0);
+  double u[7], f[7], tau = 0.0, dt = 0.0, qpow = qpow_init;
   double cprev = 0.0;
   int sprev = 0;
   bool just_evented = false;
@@ -330,7 +333,7 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
           tau = in.lnt0[ray];
           n_acc = n_rej = ncross = iter = 0;
           just_evented = false;
-          qold = 1e-4;
+          qpow = qpow_init;  // qoldinit = 1e-4
           s_rays += 1;
         }
         wnext += take;
@@ -487,7 +490,7 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
             q = 0.1;
           } else {
             q11 = pow(EEst, 7.0 / 60.0);
-            q = q11 / pow(qold, 1.0 / 15.0);
+            q = q11 / qpow;
             q = fmax(0.1, fmin(5.0, q / 0.9));
           }
           accept = (EEst <= 1.0) || forced;
@@ -500,7 +503,7 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
           ++n_acc;
           s_acc += 1;
           if (!RK4) {
-            qold = fmax(EEst, 1e-4);
+            qpow = pow(fmax(EEst, 1e-4), 1.0 / 15.0);
             dtnext = hs / q;
           }
           scan = true;
@@ -943,6 +946,24 @@ __global__ void eval_condition_kernel(const KParams P, const int64_t n, const do
   outc[i] = condition(P, ui, tau[i]);
 }
 
+// Event weight of every sampled point (MainRunner.jl:498-557, art_event.h); out: 5n SoA.
+__global__ __launch_bounds__(256) void event_weight_kernel(const KParams P, const int64_t n, const double* __restrict__ x,
+                                                           const double* __restrict__ k, const double* __restrict__ v,
+                                                           const double maxR, const double rho, const double mcmc,
+                                                           double* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const double xi[3] = {x[i], x[n + i], x[2 * n + i]};
+  const double ki[3] = {k[i], k[n + i], k[2 * n + i]};
+  const double vi[3] = {v[i], v[n + i], v[2 * n + i]};
+  const EventW E = event_weight(P, xi, ki, vi, maxR, rho, mcmc);
+  out[i] = E.cos_w;
+  out[n + i] = E.jacobian_GR;
+  out[2 * n + i] = E.sln_prob;
+  out[3 * n + i] = E.erg_inf_ini;
+  out[4 * n + i] = E.vel_eng;
+}
+
 // ---------------------------------------------------------------------------
 // host-side launch wrappers (art_internal.h)
 int persistent_blocks(const void* func, int64_t work) {
@@ -1010,6 +1031,13 @@ hipError_t launch_eval_hamiltonian(const KParams& P, int64_t n, const double* x,
                                    hipStream_t s) {
   hipLaunchKernelGGL(eval_hamiltonian_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, P, n, x, k, T, E, H,
                      dHdx, dHdk, dHdT);
+  return hipGetLastError();
+}
+
+hipError_t launch_event_weight(const KParams& P, int64_t n, const double* x, const double* k, const double* v,
+                               double maxR, double rho, double mcmc, double* out, hipStream_t s) {
+  hipLaunchKernelGGL(event_weight_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, P, n, x, k, v, maxR, rho,
+                     mcmc, out);
   return hipGetLastError();
 }
 

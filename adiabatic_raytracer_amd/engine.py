@@ -99,6 +99,16 @@ class Engine:
                                                  _p(group_start), _p(out), _stream()))
         return out
 
+    # ---- per-sample event weight (MainRunner.jl:498-557): 5 x n SoA
+    def event_weight(self, sample: dict, max_r=None, rho_DM=0.45, n_maxSample=6):
+        n = sample["erg"].numel()
+        max_r = self.params.max_r() if max_r is None else max_r
+        out = self.empty(5 * n)
+        check(self.lib.art_event_weight_device(C.byref(self.cp), float(max_r), float(rho_DM), float(n_maxSample), n,
+                                               _p(sample["x"]), _p(sample["k_init"]), _p(sample["vifty"]), _p(out),
+                                               _stream()))
+        return out.view(5, n)
+
     # ---- pointwise physics (parity tests)
     def eval_rhs(self, u, tau, erg, species):
         n = tau.numel()

@@ -236,6 +236,24 @@ def sample_conversion_points(params: Params, n: int, seed: int = 1769, ray_offse
     return out
 
 
+EVENT_FIELDS = ("cos_w", "jacobian_GR", "sln_prob", "erg_inf_ini", "vel_eng")
+
+
+def event_weight(params: Params, x, k_init, vifty, max_r=None, rho_DM=0.45, n_maxSample=6) -> dict:
+    """Per-sample event weight of main_runner_tree (MainRunner.jl:498-557) on the GPU:
+    cos_w of RT.dwp_ds, jacobian_GR = RT.g_det and sln_prob = |cos_w| redshift phaseS
+    (1e5)^2 c 1e5 mcmc_weights (before the final division by f_inx, :722). x, k_init and
+    vifty are the sampler's SoA outputs (3n)."""
+    max_r = params.max_r() if max_r is None else max_r
+    x, k_init, vifty = (np.ascontiguousarray(a, np.float64).reshape(-1) for a in (x, k_init, vifty))
+    n = x.size // 3
+    out = np.zeros(5 * n)
+    check(_lib.load().art_event_weight_host(C.byref(params.to_c()), float(max_r), float(rho_DM), float(n_maxSample),
+                                            n, _ptr(x), _ptr(k_init), _ptr(vifty), _ptr(out)))
+    o = out.reshape(5, n)
+    return {k: o[i].copy() for i, k in enumerate(EVENT_FIELDS)}
+
+
 def vern6_tableau():
     c, A, b, bh = np.zeros(9), np.zeros(81), np.zeros(9), np.zeros(9)
     check(_lib.load().art_vern6_tableau(_ptr(c), _ptr(A), _ptr(b), _ptr(bh)))

@@ -16,6 +16,8 @@
  *                                  RayTracer.jl:1480-1653, MainRunner.jl:463-529
  *   art_find_conversion_surface    RT.Find_Conversion_Surface RayTracer.jl:1250-1263
  *   art_flux_histogram_device      plot/flux.py:38-48 (binned flux, reduced over ranks)
+ *   art_event_weight_*             sln_prob of a sampled point: dwp_ds cos_w + g_det
+ *                                  (MainRunner.jl:498-557, RayTracer.jl:734-754,1327-1403)
  *   art_eval_*_device              pointwise physics (func!, func_axion!, hamiltonian,
  *                                  GJ_Model_ωp_vecSPH, condition) for parity tests
  *
@@ -182,6 +184,19 @@ int art_sample_conversion_points_device(const art_params* p, double max_r, uint6
                                         int64_t ray_offset, int64_t n, double* x,
                                         double* k_init, double* erg_inf, double* vifty,
                                         int32_t* weights, int32_t* attempts, void* stream);
+
+/* ---- event weight of sampled points (MainRunner.jl:498-557) ----
+ * For n sampled conversion points (x, k_init, vifty: 3n SoA, as returned by the
+ * sampler) computes out (5n SoA): cos_w of dwp_ds (RayTracer.jl:1327-1403),
+ * jacobian_GR = g_det (:734-754, 1 when flat), sln_prob (the incoming axion rate,
+ * npy column 8 before the division by f_inx, :549-552), erg_inf_ini (:517) and
+ * vel_eng (:513). rho_dm [GeV/cm^3] defaults to 0.45 and mcmc_weight = n_maxSample = 6
+ * in the reference (MainRunner.jl:356-362,480). */
+int art_event_weight_host(const art_params* p, double max_r, double rho_dm, double mcmc_weight, int64_t n,
+                          const double* x, const double* k_init, const double* vifty, double* out);
+int art_event_weight_device(const art_params* p, double max_r, double rho_dm, double mcmc_weight, int64_t n,
+                            const double* x, const double* k_init, const double* vifty, double* out,
+                            void* stream);
 
 /* ---- binned flux (plot/flux.py:38-48): histogram of the final momentum azimuth
  * φf = atan2(ky, kx) over [-π, π) in nbins bins, separately for axions (row 0) and

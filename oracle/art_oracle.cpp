@@ -761,6 +761,73 @@ class Segment {
 };
 
 // ---------------------------------------------------------------------------
+// Event weight of one sampled conversion point (MainRunner.jl:498-557): the incoming-axion
+// rate sln_prob (npy column 8 before the final division by f_inx), built from cos_w of
+// dwp_ds (RayTracer.jl:1327-1403) and jacobian_GR = g_det (:734-754).
+
+// omega_function (RayTracer.jl:558-589) as dwp_ds calls it (:1367): time0 = 0, the
+// defaults flat = false, zeroIn = false, bndry_lyr = -1, melrose = true; r < rNS is
+// clamped in place (a constant for the dual numbers). erg is unused by the reference.
+template <class T>
+T omega_function(T r, const T& th, const T& ph, const double k[3], const art_params& P, double Mass_NS, bool iso) {
+  if (val(r) < P.rNS) r = T(P.rNS);
+  T omP = GJ_wp_vecSPH(r, th, ph, T(0.0), P, false, -1.0, P.mass_a);
+  Metric<T> g = g_schwartz(r, th, Mass_NS);
+  T ksqr = g.grr * sq(k[0]) + g.gthth * sq(k[1]) + g.gpp * sq(k[2]);
+  if (iso) return sqrt(ksqr + sq(omP));
+  T kpar = K_par(r, th, ph, T(k[0]), T(k[1]), T(k[2]), T(0.0), P, Mass_NS);
+  T Ham = (ksqr + sq(omP) + sqrt(sq(ksqr) + 2.0 * ksqr * sq(omP) - 4.0 * sq(kpar) * sq(omP) + pow(omP, 4.0))) /
+          std::sqrt(2.0);
+  return sqrt(Ham);
+}
+
+struct EventWeight { double cos_w, jacobian_GR, sln_prob, erg_inf_ini, vel_eng; };
+
+EventWeight event_weight(const art_params& P, const double x[3], const double k_init[3], const double vIfty[3],
+                         double maxR, double rho_DM, double mcmc_weight) {
+  const double Mass_NS = P.mass_ns, Mass_a = P.mass_a;
+  EventWeight E{};
+  // MainRunner.jl:505-517
+  const double rmag = std::sqrt(sq(x[0]) + sq(x[1]) + sq(x[2]));
+  const double vmag2 = sq(vIfty[0]) + sq(vIfty[1]) + sq(vIfty[2]);
+  E.vel_eng = (sq(vIfty[0] / c_km) + sq(vIfty[1] / c_km) + sq(vIfty[2] / c_km)) / 2.0;
+  const double vIfty_mag = std::sqrt(vmag2);
+  const double gammaA = 1.0 / std::sqrt(1.0 - sq(vIfty_mag));
+  E.erg_inf_ini = Mass_a * std::sqrt(1.0 + sq(vIfty_mag * gammaA));
+  // k_sphere (:983-1009, flat honoured) at the sample point
+  Sph s = cart_to_sph(x);
+  const double Mk = P.flat ? 0.0 : Mass_NS;
+  double ks[3];
+  celerity(x, k_init, s, 1.0 - 2.0 * Mk * GNew / (c_km * c_km) / s.r, ks);
+  // dwp_ds cos_w (:1367-1371): gradient of omega_function over (r, θ, φ) at fixed k
+  D3 r = D3::seed(s.r, 0), th = D3::seed(s.th, 1), ph = D3::seed(s.ph, 2);
+  D3 om = omega_function(r, th, ph, ks, P, Mass_NS, P.isotropic != 0);
+  Metric<double> g = g_schwartz(s.r, s.th, Mass_NS);
+  const double gn = std::sqrt(g.grr * sq(om.d[0]) + g.gthth * sq(om.d[1]) + g.gpp * sq(om.d[2]));
+  const double kmag = std::sqrt(g.grr * sq(ks[0]) + g.gthth * sq(ks[1]) + g.gpp * sq(ks[2]));
+  E.cos_w = std::abs(g.grr * ks[0] / kmag * om.d[0] / gn + g.gthth * ks[1] / kmag * om.d[1] / gn +
+                     g.gpp * ks[2] / kmag * om.d[2] / gn);
+  // g_det (:734-754), zeroIn = false, with the run's bndry_lyr and Mass_a
+  if (P.flat) {
+    E.jacobian_GR = 1.0;
+  } else {
+    D3 w = GJ_wp_vecSPH(r, th, ph, D3(0.0), P, false, P.bndry_lyr, Mass_a);
+    const double dr_th = w.d[1] / w.d[0], dr_p = w.d[2] / w.d[0];
+    const double A = g.grr, st2 = sq(std::sin(s.th));
+    const double det = s.r * std::sqrt(st2 * (A * sq(s.r) + sq(dr_th)) + sq(dr_p));
+    const double det0 = s.r * std::sqrt(st2 * (sq(s.r) + sq(dr_th)) + sq(dr_p));
+    E.jacobian_GR = det / det0;
+  }
+  // MainRunner.jl:545-554
+  const double dense_extra = 2.0 / std::sqrt(PI) * (1.0 / (220.0 / c_km)) *
+                             std::sqrt(2.0 * Mass_NS * GNew / (c_km * c_km) / rmag);
+  const double redshift = std::sqrt(1.0 - 2.0 * GNew * Mass_NS / rmag / (c_km * c_km));
+  const double phaseS = dense_extra * (2.0 * PI * sq(maxR)) * (rho_DM * 1e9) / Mass_a * E.jacobian_GR;
+  E.sln_prob = E.cos_w * redshift * phaseS * (1e5 * 1e5) * c_km * 1e5 * mcmc_weight;
+  return E;
+}
+
+// ---------------------------------------------------------------------------
 // Philox4x32-10 (Salmon et al., SC'11) -- the counter-based stream that replaces
 // Julia's global Random stream (SURVEY §7 hard part iv).
 inline void philox4x32_10(const uint32_t ctr_in[4], const uint32_t key_in[2], uint32_t out[4]) {
@@ -1023,6 +1090,18 @@ void oracle_sample(const art_params* P, double maxR, uint64_t seed, int64_t ray_
       erg_inf[i] = E; weights[i] = s.n_found; attempts[i] = int32_t(a + 1);
       break;
     }
+  }
+}
+
+void oracle_event_weight(const art_params* P, int64_t n, const double* x, const double* k_init,
+                         const double* vIfty, double maxR, double rho_DM, double mcmc_weight, double* out5) {
+  // x, k_init, vIfty: 3n SoA; out5: 5n SoA (cos_w, jacobian_GR, sln_prob, erg_inf_ini, vel_eng)
+  for (int64_t i = 0; i < n; ++i) {
+    const double xi[3] = {x[i], x[n + i], x[2 * n + i]}, ki[3] = {k_init[i], k_init[n + i], k_init[2 * n + i]};
+    const double vi[3] = {vIfty[i], vIfty[n + i], vIfty[2 * n + i]};
+    EventWeight E = event_weight(*P, xi, ki, vi, maxR, rho_DM, mcmc_weight);
+    out5[i] = E.cos_w; out5[n + i] = E.jacobian_GR; out5[2 * n + i] = E.sln_prob;
+    out5[3 * n + i] = E.erg_inf_ini; out5[4 * n + i] = E.vel_eng;
   }
 }
 

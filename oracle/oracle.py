@@ -70,6 +70,7 @@ def lib():
             "oracle_back_transform": (None, [pp, pd, d, pd, pd]),
             "oracle_find_conversion_surface": (d, [pp]),
             "oracle_get_prob_nonad": (None, [pp, i64, pd, pd, pd, i64, P(i64), pd]),
+            "oracle_event_weight": (None, [pp, i64, pd, pd, pd, C.c_double, C.c_double, C.c_double, pd]),
             "oracle_propagate": (None, [pp, i64, pd, pd, pd, pd, pd, pi8, i32, pd, pd, pd, pd, pi32, pi32, pi32,
                                         i32, pi32, pd, pd, pd, pd, pd, i32]),
             "oracle_sample": (None, [pp, d, u64, i64, i64, pd, pd, pd, pd, pi32, pi32, i32]),
@@ -153,6 +154,18 @@ def get_prob_nonad(p, pos, kpos, erg_eff, group_start=None):
         lib().oracle_get_prob_nonad(C.byref(p), nc, _pd(pos), _pd(kpos), _pd(erg_eff), gs.size - 1,
                                     gs.ctypes.data_as(C.POINTER(C.c_int64)), _pd(out))
     return out
+
+
+def event_weight(p, x, k_init, vifty, max_r, rho_dm=0.45, mcmc_weight=6.0):
+    """sln_prob of sampled conversion points (MainRunner.jl:498-557); x, k_init, vifty SoA 3n.
+    Returns dict cos_w, jacobian_GR, sln_prob, erg_inf_ini, vel_eng (n each)."""
+    x, k_init, vifty = _arr(x).reshape(-1), _arr(k_init).reshape(-1), _arr(vifty).reshape(-1)
+    n = x.size // 3
+    out = np.zeros(5 * n)
+    lib().oracle_event_weight(C.byref(p), n, _pd(x), _pd(k_init), _pd(vifty), float(max_r), float(rho_dm),
+                              float(mcmc_weight), _pd(out))
+    o = out.reshape(5, n)
+    return {k: o[i].copy() for i, k in enumerate(("cos_w", "jacobian_GR", "sln_prob", "erg_inf_ini", "vel_eng"))}
 
 
 def propagate(p, x0, k0, erg, dw, ln_t0, species, max_crossings=-1, cap=1, nthreads=None):
