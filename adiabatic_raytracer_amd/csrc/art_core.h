@@ -398,11 +398,16 @@ __host__ __device__ inline void hamiltonian_full(const KParams& P, const T* x, c
 // The reference computes w' = w √nrm, nrm = (-E² g^tt - m_a²)/(g^rr w_r² + g^θθ w_θ² +
 // g^φφ w_φ²) (:281-282), then ½[g^tt E² + Σ g^ii w'_i² + ωp²(1 - g^rr k∥(w')²/E²)]/E².
 // By construction Σ g^ii w'_i² = nrm·den = -E² g^tt - m_a², so the kinetic part is exactly
-// -m_a², and k∥(w')² = nrm·k∥(w)². This evaluates that closed form: no square root, four
-// divisions, the same value up to rounding. It is NaN where √nrm is (nrm < 0: |u7| has
+// -m_a², and k∥(w')² = nrm·k∥(w)². This evaluates that closed form: no square root, one
+// division, the same value up to rounding. It is NaN where √nrm is (nrm < 0: |u7| has
 // dropped below m_a, where the reference would raise DomainError).
 template <class T>
 __host__ __device__ inline T condition_t(const KParams& P, const T* u, const T& t0) {
+  // With s = |sinθ|: k∥(w)² = p²/β, p = 2√g^rr w_r a1 + (w_θ a2 + w_φ a3/s)/r, and
+  // den = g^rr w_r² + (w_θ² + w_φ²/s²)/r². Scaling both by r s gives PP = p r s and
+  // DEN = den r² s², so X = g^rr k∥(w')²/E² = g^rr num PP²/(DEN β E²) with no 1/r, 1/s.
+  // ωp² = wpn/wpd (wpd = r³ without a boundary layer). One division in total:
+  //   cond = ½ [wpn (A - B) - m_a² wpd A] / (wpd A E²),  A = DEN β E²,  B = g^rr num PP².
   const T r = u[0];
   T gtt, grr;
   metric_tr(r, P.rs_eff, gtt, grr);
@@ -411,31 +416,32 @@ __host__ __device__ inline T condition_t(const KParams& P, const T* u, const T& 
   const T E2 = u[6] * u[6];
   const T num = -E2 * gtt - P.mass_a2;
   if (num < 0.0) return T(NAN);
-  const T ir = 1.0 / r;
-  const T ir2 = ir * ir;
-  T wp2 = 0.0;
-  T X = 0.0;  // g^rr k∥(w')²/E²
+  T wpn = 0.0, wpd = r * r * r;
+  T A = 1.0, B = 0.0;
   if (r > P.rNS || !P.isotropic) {
     T sp, cp;
     msincos(u[2] - P.omega * t0, sp, cp);
     const DipoleAng<T> d = dipole_ang(P, st, ct, sp, cp);
     if (r > P.rNS) {  // zeroIn = true
-      wp2 = P.wp2_coef * P.Bn_coef * ir2 * ir * mabs(d.b);
+      wpn = P.wp2_coef * P.Bn_coef * mabs(d.b);
       if (P.bndry_lyr > 0.0) {
-        const T w = msqrt(wp2) + layer_wp(P, r, P.rmax);
-        wp2 = w * w;
+        const T w = msqrt(wpn / wpd) + layer_wp(P, r, P.rmax);
+        wpn = w * w;
+        wpd = 1.0;
       }
     }
     if (!P.isotropic) {
-      const T iast = 1.0 / mabs(st);
-      const T den = grr * u[3] * u[3] + ir2 * (u[4] * u[4] + iast * iast * u[5] * u[5]);
+      const T as = mabs(st);
       const T sq = (P.rs_eff == 0.0) ? T(1.0) : msqrt(grr);
-      const T p = 2.0 * sq * u[3] * d.a1 + ir * (u[4] * d.a2 + u[5] * d.a3 * iast);
+      const T ur = u[3] * r * as, ut = u[4] * as;
+      const T DEN = grr * ur * ur + ut * ut + u[5] * u[5];
+      const T PP = 2.0 * sq * ur * d.a1 + ut * d.a2 + u[5] * d.a3;
       const T beta = 4.0 * d.a1 * d.a1 + d.a2 * d.a2 + d.a3 * d.a3;
-      X = grr * num * p * p / (den * beta * E2);
+      A = DEN * beta * E2;
+      B = grr * num * PP * PP;
     }
   }
-  return 0.5 * (wp2 * (1.0 - X) - P.mass_a2) / E2;
+  return 0.5 * (wpn * (A - B) - P.mass_a2 * wpd * A) / (wpd * A * E2);
 }
 
 template <class T>
