@@ -85,6 +85,7 @@ int validate(const art_params* p) {
   if (!(p->rNS > 0) || !(p->mass_a > 0) || !(p->omega_pul != 0)) return fail(ART_E_INVALID, "rNS, mass_a must be > 0 and omega_pul != 0");
   if (!(p->abstol > 0) || !(p->reltol >= 0)) return fail(ART_E_INVALID, "bad tolerances");
   if (p->maxiters < 1) return fail(ART_E_INVALID, "maxiters must be >= 1");
+  if (p->interp_points > 65) return fail(ART_E_INVALID, "interp_points must be <= 65 (the reference uses 50)");
   return ART_OK;
 }
 

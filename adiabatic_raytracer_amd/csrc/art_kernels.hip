@@ -113,6 +113,27 @@ __host__ __device__ inline void hermite7(const T* u0, const T* f0, const T* u1, 
 
 __device__ inline int sgn(double x) { return (x > 0.0) - (x < 0.0); }
 
+// One point of the resonance scan: the condition on the cubic Hermite interpolant of the
+// step (u0, f0) -> (u1, f1) over h, at fraction th and t = e^(τ + th h). Both the
+// wave-cooperative grid pass and the per-lane bracket/Illinois evaluations call this, so a
+// recomputed grid value is bit-identical to the one whose sign the grid pass recorded.
+__device__ inline double scan_point(const KParams& P, const double* u0, const double* f0, const double* u1,
+                                    const double* f1, double h, double tau, double th) {
+  double ui[7];
+  hermite7(u0, f0, u1, f1, h, th, ui);
+  return condition_t(P, ui, exp(tau + th * h));
+}
+
+// Completes this wave's LDS traffic before other lanes of the same wave read it.
+__device__ inline void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// 2-bit sign code of a scan value: 0 zero, 1 positive, 2 negative, 3 NaN
+__device__ inline unsigned sign_code(double c) { return isnan(c) ? 3u : (c > 0.0 ? 1u : (c < 0.0 ? 2u : 0u)); }
+
 // ode_determine_initdt (DiffEqBase) for an order-6 method; one extra RHS evaluation.
 __device__ inline double initdt(const KParams& P, bool photon, double erg, const double* u0, const double* f0,
                                 double tau0, double dtmax) {
@@ -260,6 +281,7 @@ __constant__ StageTable c_rk4 = {
 enum LaneMode { M_IDLE = 0, M_INIT = 1, M_STEP = 2, M_ROOT = 3 };
 
 constexpr int BLOCK = 256;
+constexpr int SCAN_WORDS = 4;  // 2-bit codes for up to 64 grid points (interp_points <= 65)
 // Waves per SIMD the integrator is register-budgeted for (1: 512 VGPR+AGPR, 2: 256).
 #ifndef ART_WAVES_PER_SIMD
 #define ART_WAVES_PER_SIMD 2
@@ -280,7 +302,11 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
   constexpr int NSLOT = RK4 ? 4 : 8;
   const StageTable& T = RK4 ? c_rk4 : c_vern6;
   __shared__ double lds[LDS_SLOTS * 7 * BLOCK];  // [slot][component][lane]: conflict-free ds_read_b64
+  __shared__ unsigned codes[SCAN_WORDS * BLOCK];  // [word][lane]: 2-bit sign codes of the grid scan
+  __shared__ double lastv[BLOCK];                 // value at the last grid point
+  __shared__ int srcl[BLOCK];                     // compact list of the wave's scanning lanes
   double* const L = lds + threadIdx.x;
+  const int wbase = threadIdx.x & ~63;
   const int lane = threadIdx.x & 63;
   const double tend = P.ln_t_end;
   const int npts = P.interp_points;
@@ -511,43 +537,161 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
       }
     }
 
-    // ---- condition evaluations, ONE call site: init sign, root polish, the grid scan of an
-    // accepted step (ContinuousCallback, RayTracer.jl:357-358) and the Illinois root search
-    // on its interpolant. ph: 0 done, 1 single point (INIT / ROOT), 2 grid scan, 3 Illinois.
+    // ---- resonance scan of the accepted steps (ContinuousCallback, RayTracer.jl:357-358) ----
+    // (a) Wave-cooperative grid pass: every lane of the wave evaluates (source lane, grid
+    //     point) items of all the wave's accepted steps, so lanes whose attempt was rejected
+    //     (and the idle lanes of a draining wave) share the 49-point scans instead of waiting.
+    //     Each item leaves a 2-bit sign code in the source lane's LDS words.
+    const int nper = npts - 1;
+    const double inv_n = 1.0 / double(nper);
+    const unsigned long long smask = __ballot(scan);
+    if (smask != 0ull) {
+      const int ns = __popcll(smask);
+      // every lane parks (u, f, y, kk) in its LDS slots and reloads them after the pass, so
+      // their registers are free while the pass holds a source lane's interpolant
+#pragma unroll
+      for (int i = 0; i < 7; ++i) {
+        L[(0 * 7 + i) * BLOCK] = u[i];
+        L[(1 * 7 + i) * BLOCK] = f[i];
+        L[(2 * 7 + i) * BLOCK] = y[i];
+        L[(3 * 7 + i) * BLOCK] = kk[i];
+      }
+      L[(4 * 7 + 0) * BLOCK] = hs;
+      L[(4 * 7 + 1) * BLOCK] = tau;
+      if (scan) {
+        srcl[wbase + __popcll(smask & ((1ull << lane) - 1ull))] = lane;
+#pragma unroll
+        for (int w = 0; w < SCAN_WORDS; ++w) codes[w * BLOCK + threadIdx.x] = 0u;
+      }
+      wave_lds_sync();
+      // item w = (j - 1) ns + c: point-major, advanced by 64 items per pass
+      const int total = ns * nper;
+      const int dj = 64 / ns, dc = 64 % ns;
+      int c = lane % ns, j = lane / ns + 1;
+#pragma unroll 1
+      for (int w0 = 0; w0 < total; w0 += 64) {
+        if (w0 + lane < total) {
+          const int src = srcl[wbase + c];
+          const double* S = lds + wbase + src;
+          double u0[7], f0[7], u1[7], f1[7];
+#pragma unroll
+          for (int i = 0; i < 7; ++i) {
+            u0[i] = S[(0 * 7 + i) * BLOCK];
+            f0[i] = S[(1 * 7 + i) * BLOCK];
+            u1[i] = S[(2 * 7 + i) * BLOCK];
+            f1[i] = S[(3 * 7 + i) * BLOCK];
+          }
+          const double cv = scan_point(P, u0, f0, u1, f1, S[(4 * 7 + 0) * BLOCK], S[(4 * 7 + 1) * BLOCK],
+                                       double(j) * inv_n);
+          atomicOr(&codes[((j - 1) >> 4) * BLOCK + wbase + src], sign_code(cv) << (2 * ((j - 1) & 15)));
+          if (j == nper) lastv[wbase + src] = cv;
+          s_scan += 1;
+        }
+        c += dc;
+        j += dj;
+        if (c >= ns) {
+          c -= ns;
+          j += 1;
+        }
+      }
+      wave_lds_sync();
+#pragma unroll
+      for (int i = 0; i < 7; ++i) {
+        u[i] = L[(0 * 7 + i) * BLOCK];
+        f[i] = L[(1 * 7 + i) * BLOCK];
+        y[i] = L[(2 * 7 + i) * BLOCK];
+        kk[i] = L[(3 * 7 + i) * BLOCK];
+      }
+    }
+
+    // (b) Per lane: walk the sign codes exactly as the sequential scan would (NaN resets the
+    //     sign memory; a sign change opens an Illinois search on the interpolant, ignored
+    //     right after an event -- DiffEq repeat_nudge), plus the single evaluations of fresh
+    //     lanes (initial sign) and of lanes polishing a crossing. Condition evaluations
+    //     here only happen at brackets, Illinois points and root polish steps.
+    //     ph: 0 done, 1 single point (INIT / ROOT), 2 walk codes, 3 Illinois, 5 value at the
+    //     change point, 6 value at the bracket start, 7 value at the step's last nonzero point.
     int ph = (mode == M_INIT || mode == M_ROOT) ? 1 : (scan ? 2 : 0);
-    int ip = 1;
-    double last_c = cprev, last_th = 0.0;
+    int ip = 1, last_j = 0;
     int last_s = sprev;
+    double last_c = cprev;
+    bool lc_ok = true;  // last_c is the value at grid point last_j (0: previous step's)
+    unsigned cw[SCAN_WORDS] = {0u, 0u, 0u, 0u};
+    if (ph == 2) {
+#pragma unroll
+      for (int w = 0; w < SCAN_WORDS; ++w) cw[w] = codes[w * BLOCK + threadIdx.x];
+      // fast path: every grid point has the previous sign (or the previous sign is unknown
+      // and every point has one common nonzero sign)
+      const unsigned s0 = cw[0] & 3u;
+      if (s0 == 1u || s0 == 2u) {
+        bool same = (last_s == 0) || (last_s == (s0 == 1u ? 1 : -1));
+#pragma unroll
+        for (int w = 0; w < SCAN_WORDS; ++w) {
+          const int nw = nper - 16 * w;
+          if (nw <= 0) break;
+          const unsigned m = nw >= 16 ? 0xffffffffu : ((1u << (2 * nw)) - 1u);
+          same = same && ((cw[w] & m) == ((s0 * 0x55555555u) & m));
+        }
+        if (same) {
+          last_s = (s0 == 1u) ? 1 : -1;
+          last_j = nper;
+          last_c = lastv[threadIdx.x];
+          ph = 0;
+        }
+      }
+    }
     double i_tha = 0.0, i_ca = 0.0, i_thb = 0.0, i_cb = 0.0, i_tr = 0.0, i_cg = 0.0;
     int i_side = 0, i_it = 0;
     bool hit = false, root_done = false;
-    const double inv_n = 1.0 / double(npts - 1);
-    // t = e^τ at the grid points by recurrence (two exp per step instead of one per point;
-    // relative rounding <= npts ulp, i.e. < 1e-14 in ψ = φ - ωt)
-    double qg = 1.0, tg = 0.0;
-    if (ph == 2) {
-      qg = exp(hs * inv_n);
-      tg = exp(tau) * qg;
-    }
 #pragma unroll 1
     while (ph != 0) {
-      const double th = (ph == 3) ? i_tr : double(ip) * inv_n;
-      double ui[7];
-      hermite7(u, f, y, kk, hs, th, ui);
-      double tc = tau + th * hs;
-      if (mode == M_INIT) {
-#pragma unroll
-        for (int i = 0; i < 7; ++i) ui[i] = u[i];
-        tc = tau;
-      } else if (mode == M_ROOT) {
-#pragma unroll
-        for (int i = 0; i < 7; ++i) ui[i] = y[i];
-        tc = tau + hs;
+      if (ph == 2) {  // walk the codes from grid point ip
+        bool found = false;
+#pragma unroll 1
+        for (; ip <= nper; ++ip) {
+          const int w = (ip - 1) >> 4;
+          const unsigned word = (w == 0) ? cw[0] : (w == 1) ? cw[1] : (w == 2) ? cw[2] : cw[3];
+          const unsigned code = (word >> (2 * ((ip - 1) & 15))) & 3u;
+          if (code == 3u) {  // no resonance possible where |u7| < m_a
+            last_s = 0;
+            continue;
+          }
+          const int si = (code == 1u) ? 1 : (code == 2u ? -1 : 0);
+          if (last_s != 0 && si != 0 && si != last_s) {
+            found = true;
+            break;
+          }
+          if (si != 0) {
+            last_s = si;
+            last_j = ip;
+            lc_ok = false;
+          }
+        }
+        if (found) {
+          ph = 5;
+        } else if (!lc_ok && last_j == nper) {
+          last_c = lastv[threadIdx.x];
+          ph = 0;
+        } else if (!lc_ok) {
+          ph = 7;
+        } else {
+          ph = 0;
+        }
+        if (ph == 0) break;
       }
-      double t_eval;
-      if (ph == 2) t_eval = tg;
-      else t_eval = exp(tc);
-      const double ci = condition_t(P, ui, t_eval);
+      double th = 0.0;
+      if (ph == 3) th = i_tr;
+      else if (ph == 5) th = double(ip) * inv_n;
+      else if (ph == 6 || ph == 7) th = double(last_j) * inv_n;
+      double ci;
+      if (mode == M_INIT) {
+        ci = condition_t(P, u, exp(tau));
+      } else if (mode == M_ROOT) {
+        ci = condition_t(P, y, exp(tau + hs));
+      } else {
+        ci = scan_point(P, u, f, y, kk, hs, tau, th);
+        s_interp += 1;
+      }
       if (mode == M_INIT) {
         cprev = ci;
         sprev = isnan(ci) ? 0 : sgn(ci);
@@ -570,28 +714,26 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
         }
         root_done = done;
         ph = 0;
-      } else if (ph == 2) {
-        s_scan += 1;
-        if (isnan(ci)) {
-          last_s = 0;  // no resonance possible where |u7| < m_a
-        } else {
-          const int si = sgn(ci);
-          if (last_s != 0 && si != 0 && si != last_s) {
-            i_tha = last_th; i_ca = last_c; i_thb = th; i_cb = ci; i_cg = ci;
-            i_tr = i_tha - i_ca * (i_thb - i_tha) / (i_cb - i_ca);
-            i_side = 0;
-            i_it = 0;
-            ph = 3;
-          } else if (si != 0) {
-            last_s = si; last_c = ci; last_th = th;
-          }
-        }
-        if (ph == 2) {
-          if (++ip > npts - 1) ph = 0;
-          tg *= qg;
+      } else if (ph == 7) {  // value at the step's last nonzero grid point (next step's bracket start)
+        last_c = ci;
+        ph = 0;
+      } else if (ph == 5 || ph == 6) {
+        if (ph == 5) i_cg = ci;
+        else last_c = ci;
+        if (ph == 5 && !lc_ok) {
+          ph = 6;
+        } else {  // open the Illinois search on the interpolant inside (θ_last, θ_ip]
+          lc_ok = true;
+          i_tha = double(last_j) * inv_n;
+          i_ca = last_c;
+          i_thb = double(ip) * inv_n;
+          i_cb = i_cg;
+          i_tr = i_tha - i_ca * (i_thb - i_tha) / (i_cb - i_ca);
+          i_side = 0;
+          i_it = 0;
+          ph = 3;
         }
       } else {  // ph == 3: Illinois on the interpolant inside (i_tha, i_thb]
-        s_interp += 1;
         bool stop = ci == 0.0 || isnan(ci) || (i_thb - i_tha) < 1e-12;
         if (!stop) {
           if (sgn(ci) == sgn(i_ca)) { i_tha = i_tr; i_ca = ci; if (i_side == -1) i_cb *= 0.5; i_side = -1; }
@@ -602,8 +744,8 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
           if (++i_it >= 40) stop = true;
         }
         if (stop) {
-          // the sign change that opened this search was at grid point ip
           const double thg = double(ip) * inv_n;
+          const double last_th = double(last_j) * inv_n;
           const double t_int = i_tr;
           if (!(just_evented && t_int < 0.01)) {  // DiffEq repeat_nudge after an event
             hit = true;
@@ -617,10 +759,13 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
             post_s = sgn(i_cg);
             dt = dtnext;
             ph = 0;
-          } else {
-            last_s = sgn(i_cg); last_c = i_cg; last_th = thg;
-            ph = (++ip > npts - 1) ? 0 : 2;
-            tg *= qg;
+          } else {  // ignored: continue the walk after the change point
+            last_s = sgn(i_cg);
+            last_c = i_cg;
+            last_j = ip;
+            lc_ok = true;
+            ++ip;
+            ph = 2;
           }
         }
       }

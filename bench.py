@@ -152,7 +152,10 @@ def main():
         pmc_path = os.path.join(HERE, "profiles", "pmc_summary.json")
         if os.path.exists(pmc_path):
             pm = json.load(open(pmc_path))
-            if pm.get("workload") == f"{args.config}:{n}":
+            # only a PMC pass of this very library build and workload counts
+            import hashlib
+            sha = hashlib.sha256(open(A._lib.load()._name, "rb").read()).hexdigest()
+            if pm.get("workload") == f"{args.config}:{n}" and pm.get("libart_sha256") == sha:
                 traffic = pm.get("hbm_bytes_per_launch")
         ncross = int((out["n_cross"].clamp(max=out["capacity"])).sum().item())
         att = (out["n_accept"] + out["n_reject"]).double()

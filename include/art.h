@@ -90,7 +90,8 @@ typedef struct art_params {
   int32_t melrose;  /* must be 1 (Gen_Samples.jl:167)                               */
   int32_t integrator;    /* ART_VERN6 or ART_RK4                                    */
   int32_t n_fixed;       /* RK4: steps per segment                                  */
-  int32_t interp_points; /* ContinuousCallback interp_points (RayTracer.jl:358 = 50)*/
+  int32_t interp_points; /* ContinuousCallback interp_points (RayTracer.jl:358 = 50),*/
+                         /* at most 65                                             */
 } art_params;
 
 /* Outputs of one batch of segments (the 14-tuple of RayTracer.jl:448, per ray). */

@@ -1,0 +1,24 @@
+"""Dev A/B timing of the propagate kernel for the library named by ART_LIB: 1e6-ray
+batches of the flat (configs[1]) and GR (configs[3]) workloads. One JSON line per config."""
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import adiabatic_raytracer_amd as A  # noqa: E402
+from adiabatic_raytracer_amd import Engine  # noqa: E402
+
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 1_000_000
+for name, kw in (("flat", dict(theta_m=0.2, mass_a=1e-5, flat=True)), ("gr", dict(theta_m=0.0, mass_a=1e-6, flat=False))):
+    eng = Engine(A.Params(**kw))
+    inp = eng.forward_roots(n, seed=1769)
+    out = eng.alloc_out(n)
+    ms = []
+    for _ in range(3 if name == "flat" else 2):
+        eng.propagate(inp, out)
+        ms.append(eng.kernel_ms())
+    st = A.raytracer.last_stats()
+    att = (out["n_accept"] + out["n_reject"]).max().item()
+    print(json.dumps({"lib": os.environ.get("ART_LIB", "default"), "config": name, "kernel_ms": ms[-1],
+                      "accepted": st["accepted"], "scan_evals": st["scan_evals"], "interp_evals": st["interp_evals"],
+                      "max_attempts": att, "ray_steps_per_s": st["accepted"] / ms[-1] * 1e3}), flush=True)

@@ -50,8 +50,11 @@ def main():
     name, pc = pick(k, "art::propagate_kernel<0>")
     fetch = pc["FETCH_SIZE"][-1] * kb
     write = pc["WRITE_SIZE"][-1] * kb
+    import hashlib
+    lib = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "adiabatic_raytracer_amd", "lib", "libart.so")
     res = {
         "workload": workload,
+        "libart_sha256": hashlib.sha256(open(lib, "rb").read()).hexdigest() if os.path.exists(lib) else None,
         "kernel": name,
         "hbm_bytes_per_launch": fetch * c_read + write * c_write,
         "fetch_bytes_raw": fetch, "write_bytes_raw": write,
