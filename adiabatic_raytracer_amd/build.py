@@ -8,8 +8,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB_DIR = os.path.join(HERE, "lib")
 LIB = os.path.join(LIB_DIR, "libart.so")
-SOURCES = ["art_kernels.hip", "art_capi.cpp"]
-HEADERS = ["art_core.h", "art_internal.h"]
+SOURCES = ["art_kernels.hip", "art_capi.cpp", "art_forest.cpp"]
+HEADERS = ["art_core.h", "art_internal.h", "art_event.h"]
 ARCH = os.environ.get("ART_OFFLOAD_ARCH", "gfx950")
 
 

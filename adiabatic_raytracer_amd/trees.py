@@ -1,0 +1,147 @@
+"""Trees and events on the GPU engine: the host side of main_runner_tree (MainRunner.jl:354-763).
+
+grow_trees()        get_tree (MainRunner.jl:126-352) for many trees at once, through the
+                    native batched driver art_grow_trees (csrc/art_forest.cpp).
+main_runner_tree()  the event loop: sample conversion points, weight them (sln_prob),
+                    backtrace each one (axion, -k, -B0, every crossing), grow its forward
+                    photon tree, and write the reference's npy rows, with the same columns
+                    and the same file name (MainRunner.jl:715-761), so Combine_Files.py and
+                    plot/*.py read them unchanged.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+import os
+from dataclasses import replace
+
+import numpy as np
+
+from . import _lib
+from ._lib import check
+from .raytracer import Params, event_weight, sample_conversion_points
+
+AXION, PHOTON = 0, 1
+
+
+class TreeOpts(C.Structure):
+    _fields_ = [("num_cutoff", C.c_int32), ("mc_nodes", C.c_int32), ("max_nodes", C.c_int32),
+                ("splittings_cutoff", C.c_int32), ("crossing_cap", C.c_int32), ("pad", C.c_int32),
+                ("prob_cutoff", C.c_double), ("seed", C.c_uint64)]
+
+
+# include/art.h art_tree_node, as a numpy record (checked against the C layout in tests)
+NODE_DTYPE = np.dtype([
+    ("tree", np.int32), ("species", np.int32), ("is_final", np.int32), ("n_cross", np.int32),
+    ("status", np.int32), ("pad", np.int32),
+    ("weight", np.float64), ("prob", np.float64), ("parent_weight", np.float64), ("prob_conv", np.float64),
+    ("prob_conv0", np.float64),
+    ("x0", np.float64, 3), ("k0", np.float64, 3), ("t0", np.float64), ("dw0", np.float64),
+    ("x_end", np.float64, 3), ("k_end", np.float64, 3), ("u7_end", np.float64), ("tau_end", np.float64),
+    ("xc", np.float64, 3), ("kc", np.float64, 3), ("tc", np.float64), ("dwc", np.float64), ("pc", np.float64),
+], align=True)
+
+
+def grow_trees(params: Params, x0, k0, erg, species, *, num_cutoff=5, mc_nodes=5, max_nodes=50,
+               splittings_cutoff=-1, crossing_cap=64, prob_cutoff=1e-10, seed=1769):
+    """get_tree for n roots RT.node(x0, k0, 0, -1, species, 1, 1, -1, -1, -1) (MainRunner.jl:578-590,
+    :653-667). x0, k0: (n, 3) or SoA 3n; erg: erg_inf_ini per root. Returns (nodes, counts,
+    infos): nodes is a NODE_DTYPE record array grouped by tree in get_tree's push order."""
+    x0, k0 = np.asarray(x0, np.float64), np.asarray(k0, np.float64)
+    erg = np.ascontiguousarray(erg, np.float64).reshape(-1)
+    n = erg.size
+    if x0.ndim == 2:
+        x0, k0 = x0.T, k0.T
+    x0, k0 = np.ascontiguousarray(x0).reshape(-1), np.ascontiguousarray(k0).reshape(-1)
+    sp = np.ascontiguousarray(np.broadcast_to(np.asarray(species, np.int8), (n,)))
+    opts = TreeOpts(num_cutoff, mc_nodes, max_nodes, splittings_cutoff, crossing_cap, 0, prob_cutoff, seed)
+    per_tree = 1 if (splittings_cutoff > 0 and num_cutoff <= 0) else max_nodes + 2
+    cap = max(1, n * per_tree)
+    lib = _lib.load()
+    ptr = lambda a: a.ctypes.data_as(C.c_void_p)  # noqa: E731
+    while True:
+        nodes = np.zeros(cap, NODE_DTYPE)
+        nn = C.c_int64(0)
+        counts, infos = np.zeros(n, np.int32), np.zeros(n, np.int32)
+        rc = lib.art_grow_trees(C.byref(params.to_c()), n, ptr(x0), ptr(k0), ptr(erg), ptr(sp), C.byref(opts), cap,
+                                ptr(nodes), C.byref(nn), ptr(counts), ptr(infos))
+        if rc == -3 and nn.value > cap:  # ART_E_NOMEM: grow and redo (pathological trees only)
+            cap = nn.value
+            continue
+        check(rc)
+        return nodes[:nn.value], counts, infos
+
+
+def _angles(v):
+    a = np.linalg.norm(v, axis=-1)
+    return np.arccos(v[..., 2] / a), np.arctan2(v[..., 1], v[..., 0]), a
+
+
+def tree_file_name(dir_tag, Mass_a, Ax_g, θm, ωPul, B0, Ntajs, ntimes, num_cutoff, MC_nodes, max_nodes, file_tag):
+    """The npy name of MainRunner.jl:750-760, with Julia's number formatting."""
+    def jl(x):  # Julia string(::Float64): shortest digits, scientific outside [1e-4, 1e6)
+        x = float(x)
+        if x == 0.0:
+            return "-0.0" if math.copysign(1.0, x) < 0 else "0.0"
+        if 1e-4 <= abs(x) < 1e6:
+            r = repr(x)
+            return r if ("." in r or "e" in r) else r + ".0"
+        m, e = np.format_float_scientific(x, unique=True, trim="-").split("e")
+        return f"{m if '.' in m else m + '.0'}e{int(e)}"
+    name = (f"tree_MassAx_{jl(Mass_a)}_AxionG_{jl(Ax_g)}_ThetaM_{jl(θm)}_rotPulsar_{jl(ωPul)}_B0_{jl(B0)}"
+            f"_Ax_trajs_{int(Ntajs)}_N_Times_{int(ntimes)}_num_cutoff_{int(num_cutoff)}_MC_nodes_{int(MC_nodes)}"
+            f"_max_nodes_{int(max_nodes)}_{file_tag}.npy")
+    return os.path.join(dir_tag, "npy", name)
+
+
+def main_runner_tree(params: Params, Ntajs: int, *, seed=1769, ntimes=1000, rho_DM=0.45, n_maxSample=6,
+                     num_cutoff=5, MC_nodes=5, max_nodes=50, prob_cutoff=1e-10, saveMode=0, dir_tag=None,
+                     file_tag="", backtrace_cap=256):
+    """main_runner_tree (MainRunner.jl:354-763) for Ntajs - 1 events (the reference's
+    `while photon_trajs < desired_trajs` loop), all events batched on the GPU. Returns the
+    row matrix (13 columns, 29 with saveMode > 0) after the final division of column 8 by
+    f_inx, and writes it to the reference's npy path when dir_tag is given."""
+    n_ev = max(0, int(Ntajs) - 1)
+    max_r = params.max_r()
+    if max_r < params.rNS:
+        raise ValueError("maxR < rNS: this neutron star has no conversion surface (MainRunner.jl:387-396)")
+    s = sample_conversion_points(params, n_ev, seed=seed, max_r=max_r)
+    w = event_weight(params, s["x"], s["k_init"], s["vifty"], max_r=max_r, rho_DM=rho_DM, n_maxSample=n_maxSample)
+    x = s["x"].reshape(3, n_ev).T
+    k = s["k_init"].reshape(3, n_ev).T
+    erg = s["erg"]
+    # f_inx: find_samples_new calls minus accepted samples (MainRunner.jl:463-481)
+    f_inx = int(np.sum(s["attempts"].astype(np.int64) - 1))
+    # backtrace: axion, -k, -B0, every crossing, only the root is processed (:578-590)
+    nb, c_bck, _ = grow_trees(replace(params, B0=-params.B0), x, -k, erg, AXION, num_cutoff=0,
+                              splittings_cutoff=100000, crossing_cap=backtrace_cap, prob_cutoff=prob_cutoff,
+                              seed=seed)
+    samp_back_weight = nb["prob"] * nb["weight"]  # (:635)
+    prob0 = nb["prob"]
+    # forward photon tree from the sample (:653-667)
+    tree, counts, infos = grow_trees(params, x, k, erg, PHOTON, num_cutoff=num_cutoff, mc_nodes=MC_nodes,
+                                     max_nodes=max_nodes, prob_cutoff=prob_cutoff, seed=seed)
+    fin = tree[tree["is_final"] != 0]
+    ev = fin["tree"]
+    θf, ϕf, _ = _angles(fin["k_end"])
+    θfX, ϕfX, absfX = _angles(fin["x_end"])
+    wgt = fin["weight"] * samp_back_weight[ev]  # tree[ii].weight *= samp_back_weight (:690)
+    ident = np.where(fin["species"] == AXION, 0.0, 1.0)
+    f_inx += int(np.sum(ident == 1.0))
+    dω = fin["u7_end"] / params.mass_a + w["vel_eng"][ev]  # (:713)
+    photon_trajs = ev + 1.0
+    cols = [photon_trajs, ident, θf, ϕf, θfX, ϕfX, absfX, w["sln_prob"][ev], wgt, x[ev, 0], x[ev, 1], x[ev, 2], dω]
+    if saveMode > 0:
+        zero = np.zeros_like(wgt)
+        cols += [wgt, zero, zero + 1.0, k[ev, 0], k[ev, 1], k[ev, 2], w["cos_w"][ev], counts[ev].astype(float),
+                 infos[ev].astype(float), fin["prob"], fin["prob_conv"], fin["prob_conv0"], samp_back_weight[ev],
+                 absfX, c_bck[ev].astype(float), prob0[ev]]
+    rows = np.stack(cols, axis=1) if len(fin) else np.zeros((0, len(cols)))
+    if len(rows):
+        rows[:, 7] /= float(f_inx)  # saveAll[:, 8] ./= f_inx (:747)
+    if dir_tag is not None:
+        path = tree_file_name(dir_tag, params.mass_a, params.g_agg, params.theta_m, params.omega_pul, params.B0, Ntajs,
+                              ntimes, num_cutoff, MC_nodes, max_nodes, file_tag)
+        os.makedirs(os.path.dirname(path), exist_ok=True)
+        np.save(path, rows)
+    return rows

@@ -16,6 +16,7 @@
  *                                  RayTracer.jl:1480-1653, MainRunner.jl:463-529
  *   art_find_conversion_surface    RT.Find_Conversion_Surface RayTracer.jl:1250-1263
  *   art_flux_histogram_device      plot/flux.py:38-48 (binned flux, reduced over ranks)
+ *   art_grow_trees                 get_tree (MainRunner.jl:126-352) for n trees, batched
  *   art_event_weight_*             sln_prob of a sampled point: dwp_ds cos_w + g_det
  *                                  (MainRunner.jl:498-557, RayTracer.jl:734-754,1327-1403)
  *   art_eval_*_device              pointwise physics (func!, func_axion!, hamiltonian,
@@ -185,6 +186,51 @@ int art_sample_conversion_points_device(const art_params* p, double max_r, uint6
                                         int64_t ray_offset, int64_t n, double* x,
                                         double* k_init, double* erg_inf, double* vifty,
                                         int32_t* weights, int32_t* attempts, void* stream);
+
+/* ---- batched tree driver: get_tree (MainRunner.jl:126-352) for n trees at once ----
+ * Roots are RT.node(x0, k0, t = 0, Δω = -1, species, prob = 1, weight = 1, -1, -1, -1) with
+ * root.prob replaced by 1 - exp(-P_nonAD) at the root (:132-137), as main_runner_tree
+ * builds both its backtrace (axion, -k, -B0: pass p with B0 negated) and its forward
+ * (photon) trees (:578-590, :653-667). Every round propagates the next node of every
+ * active tree in one batched launch. Per tree the reference's rules are kept: pop the
+ * highest-weight event (stable sort by weight), stop each segment at its first crossing
+ * when splittings_cutoff <= 0, full splitting while count <= mc_nodes and one
+ * Monte-Carlo branch after (Philox4x32-10 keyed by (seed, tree, count) in place of
+ * rand(Float64)), the |kc| > 1 rule, the 1e-5 km crossing merge, the stop rules and the
+ * info codes 1..4 (negative once Monte-Carlo). */
+typedef struct art_tree_opts {
+  int32_t num_cutoff;        /* 5   (Gen_Samples.jl default)                       */
+  int32_t mc_nodes;          /* 5                                                  */
+  int32_t max_nodes;         /* 50                                                 */
+  int32_t splittings_cutoff; /* -1: forward trees; 100000: backtrace (:588)        */
+  int32_t crossing_cap;      /* crossings stored per segment when splittings > 0   */
+  int32_t pad;
+  double prob_cutoff;        /* 1e-10                                              */
+  uint64_t seed;             /* key of the Monte-Carlo draws                        */
+} art_tree_opts;
+
+/* One RT.node of a finished tree, in the order get_tree pushed it onto `tree`. */
+typedef struct art_tree_node {
+  int32_t tree;      /* index of its root                                          */
+  int32_t species;   /* ART_AXION / ART_PHOTON                                     */
+  int32_t is_final;  /* no crossing and |x_end| > 1.1 rNS (:200-207)               */
+  int32_t n_cross;   /* crossings kept on its segment (after the 1e-5 km merge)    */
+  int32_t status;    /* ART_STATUS_* of its segment                                */
+  int32_t pad;
+  double weight, prob, parent_weight, prob_conv, prob_conv0;
+  double x0[3], k0[3], t0, dw0;               /* node.x .. node.Δω (start)          */
+  double x_end[3], k_end[3], u7_end, tau_end; /* traj[end], mom[end], erg[end], ln t */
+  double xc[3], kc[3], tc, dwc, pc;           /* first crossing, Pc = 1 - e^-P_nonAD */
+} art_tree_node;
+
+/* x0, k0: 3n SoA; erg: n erg_inf_ini; species: n. nodes: caller-owned, node_capacity
+ * records; *n_nodes receives the number of nodes (returns ART_E_NOMEM with the needed
+ * count when node_capacity is too small). counts, infos (n, may be NULL): get_tree's
+ * `count` and `info`. Host pointers; synchronous. */
+int art_grow_trees(const art_params* p, int64_t n, const double* x0, const double* k0,
+                   const double* erg, const int8_t* species, const art_tree_opts* opts,
+                   int64_t node_capacity, art_tree_node* nodes, int64_t* n_nodes,
+                   int32_t* counts, int32_t* infos);
 
 /* ---- event weight of sampled points (MainRunner.jl:498-557) ----
  * For n sampled conversion points (x, k_init, vifty: 3n SoA, as returned by the
