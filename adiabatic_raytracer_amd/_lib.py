@@ -31,6 +31,12 @@ class CrossingBuf(C.Structure):
 
 
 # name -> (restype, argtypes); the test suite checks this table against include/art.h
+class TreeOpts(C.Structure):  # include/art.h art_tree_opts
+    _fields_ = [("num_cutoff", C.c_int32), ("mc_nodes", C.c_int32), ("max_nodes", C.c_int32),
+                ("splittings_cutoff", C.c_int32), ("crossing_cap", C.c_int32), ("pad", C.c_int32),
+                ("prob_cutoff", C.c_double), ("seed", C.c_uint64)]
+
+
 _P = C.POINTER(ArtParams)
 _v = C.c_void_p
 _i64, _i32, _d, _u64 = C.c_int64, C.c_int32, C.c_double, C.c_uint64
@@ -53,6 +59,7 @@ SIGNATURES = {
     "art_sample_conversion_points_host": (C.c_int, [_P, _d, _u64, _i64, _i64, _v, _v, _v, _v, _v, _v]),
     "art_sample_conversion_points_device": (C.c_int, [_P, _d, _u64, _i64, _i64, _v, _v, _v, _v, _v, _v, _v]),
     "art_flux_histogram_device": (C.c_int, [_P, _i64, _v, _v, _v, _v, _v, _i32, _v, _v]),
+    "art_grow_trees": (C.c_int, [_P, _i64, _v, _v, _v, _v, C.POINTER(TreeOpts), _i64, _v, C.POINTER(_i64), _v, _v]),
     "art_event_weight_host": (C.c_int, [_P, _d, _d, _d, _i64, _v, _v, _v, _v]),
     "art_event_weight_device": (C.c_int, [_P, _d, _d, _d, _i64, _v, _v, _v, _v, _v]),
     "art_eval_rhs_device": (C.c_int, [_P, _i64, _v, _v, _v, _v, _v, _v]),

@@ -18,16 +18,10 @@ from dataclasses import replace
 import numpy as np
 
 from . import _lib
-from ._lib import check
+from ._lib import TreeOpts, check
 from .raytracer import Params, event_weight, sample_conversion_points
 
 AXION, PHOTON = 0, 1
-
-
-class TreeOpts(C.Structure):
-    _fields_ = [("num_cutoff", C.c_int32), ("mc_nodes", C.c_int32), ("max_nodes", C.c_int32),
-                ("splittings_cutoff", C.c_int32), ("crossing_cap", C.c_int32), ("pad", C.c_int32),
-                ("prob_cutoff", C.c_double), ("seed", C.c_uint64)]
 
 
 # include/art.h art_tree_node, as a numpy record (checked against the C layout in tests)
