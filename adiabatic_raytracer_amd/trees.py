@@ -71,21 +71,52 @@ def _angles(v):
     return np.arccos(v[..., 2] / a), np.arctan2(v[..., 1], v[..., 0]), a
 
 
+def jl(x) -> str:
+    """Julia's string(::Float64): shortest round-trip digits, scientific notation (1.0e14,
+    2.0e-5) outside [1e-4, 1e6)."""
+    x = float(x)
+    if x == 0.0:
+        return "-0.0" if math.copysign(1.0, x) < 0 else "0.0"
+    if not math.isfinite(x):
+        return "NaN" if math.isnan(x) else ("Inf" if x > 0 else "-Inf")
+    if 1e-4 <= abs(x) < 1e6:
+        r = repr(x)
+        return r if ("." in r or "e" in r) else r + ".0"
+    m, e = np.format_float_scientific(x, unique=True, trim="-").split("e")
+    return f"{m if '.' in m else m + '.0'}e{int(e)}"
+
+
 def tree_file_name(dir_tag, Mass_a, Ax_g, θm, ωPul, B0, Ntajs, ntimes, num_cutoff, MC_nodes, max_nodes, file_tag):
     """The npy name of MainRunner.jl:750-760, with Julia's number formatting."""
-    def jl(x):  # Julia string(::Float64): shortest digits, scientific outside [1e-4, 1e6)
-        x = float(x)
-        if x == 0.0:
-            return "-0.0" if math.copysign(1.0, x) < 0 else "0.0"
-        if 1e-4 <= abs(x) < 1e6:
-            r = repr(x)
-            return r if ("." in r or "e" in r) else r + ".0"
-        m, e = np.format_float_scientific(x, unique=True, trim="-").split("e")
-        return f"{m if '.' in m else m + '.0'}e{int(e)}"
     name = (f"tree_MassAx_{jl(Mass_a)}_AxionG_{jl(Ax_g)}_ThetaM_{jl(θm)}_rotPulsar_{jl(ωPul)}_B0_{jl(B0)}"
             f"_Ax_trajs_{int(Ntajs)}_N_Times_{int(ntimes)}_num_cutoff_{int(num_cutoff)}_MC_nodes_{int(MC_nodes)}"
             f"_max_nodes_{int(max_nodes)}_{file_tag}.npy")
     return os.path.join(dir_tag, "npy", name)
+
+
+def _write_event_text(dir_tag, file_tag, n_ev, s, w, x, k, tree, fin, ev, wgt, ident, counts, elapsed=None):
+    """event_<file_tag> and final_<file_tag> of saveMode > 1 (MainRunner.jl:438-444, 592-609,
+    690-702, 735-741), Julia number formatting. The reference's per-event wall time
+    time() - time0 has no per-event meaning in a batched run; the mean per event is written."""
+    d = os.path.join(dir_tag, "event")
+    os.makedirs(d, exist_ok=True)
+    v = s["vifty"].reshape(3, n_ev).T
+    t_ev = 0.0 if elapsed is None else elapsed / max(1, n_ev)
+    with open(os.path.join(d, "event_" + file_tag), "w") as fe:
+        for i in range(n_ev):
+            vals = [*v[i], w["sln_prob"][i], *x[i], *(-k[i]), *x[i], *k[i]]
+            fe.write(f"{i + 1} " + " ".join(jl(a) for a in vals) + f" {jl(t_ev)} {int(counts[i])}\n")
+    θf, ϕf, absf = _angles(fin["k_end"])
+    θfX, ϕfX, absfX = _angles(fin["x_end"])
+    # node.t: the root's is the integer literal 0 of RT.node(..., 0, ...) (MainRunner.jl:661)
+    first = np.zeros(len(tree), bool)
+    first[np.r_[0, np.flatnonzero(np.diff(tree["tree"])) + 1]] = True
+    is_root = first[tree["is_final"] != 0]
+    with open(os.path.join(d, "final_" + file_tag), "w") as ff:
+        for q in range(len(fin)):
+            t = "0" if is_root[q] else jl(fin["t0"][q])
+            vals = [θf[q], ϕf[q], absf[q], θfX[q], ϕfX[q], absfX[q]]
+            ff.write(f"{int(ev[q]) + 1} {jl(wgt[q])} {int(ident[q])} " + " ".join(jl(a) for a in vals) + f" {t}\n")
 
 
 def main_runner_tree(params: Params, Ntajs: int, *, seed=1769, ntimes=1000, rho_DM=0.45, n_maxSample=6,
@@ -94,7 +125,13 @@ def main_runner_tree(params: Params, Ntajs: int, *, seed=1769, ntimes=1000, rho_
     """main_runner_tree (MainRunner.jl:354-763) for Ntajs - 1 events (the reference's
     `while photon_trajs < desired_trajs` loop), all events batched on the GPU. Returns the
     row matrix (13 columns, 29 with saveMode > 0) after the final division of column 8 by
-    f_inx, and writes it to the reference's npy path when dir_tag is given."""
+    f_inx, and writes it to the reference's npy path when dir_tag is given; saveMode > 1
+    also writes the event_/final_ text files. saveMode > 2 (saveNode dumps of whole
+    trajectories at ntimes save points) is not supported: only segment end states are kept."""
+    if saveMode > 2:
+        raise NotImplementedError("saveMode > 2 (full-trajectory tree dumps) is not supported")
+    import time
+    t_start = time.perf_counter()
     n_ev = max(0, int(Ntajs) - 1)
     max_r = params.max_r()
     if max_r < params.rNS:
@@ -131,6 +168,9 @@ def main_runner_tree(params: Params, Ntajs: int, *, seed=1769, ntimes=1000, rho_
                  infos[ev].astype(float), fin["prob"], fin["prob_conv"], fin["prob_conv0"], samp_back_weight[ev],
                  absfX, c_bck[ev].astype(float), prob0[ev]]
     rows = np.stack(cols, axis=1) if len(fin) else np.zeros((0, len(cols)))
+    if saveMode > 1 and dir_tag is not None:
+        _write_event_text(dir_tag, file_tag, n_ev, s, w, x, k, tree, fin, ev, wgt, ident, counts,
+                          elapsed=time.perf_counter() - t_start)
     if len(rows):
         rows[:, 7] /= float(f_inx)  # saveAll[:, 8] ./= f_inx (:747)
     if dir_tag is not None:

@@ -114,3 +114,23 @@ def test_main_runner_rows_match_oracle(oracle_lib, tmp_path):
             for c in (2, 3, 4, 5, 6, 8, 9, 10, 11, 12, 16, 17, 18, 19, 21, 22, 23, 24, 25):
                 np.testing.assert_allclose(g[:, c], o[:, c], rtol=1e-5, atol=1e-9, err_msg=f"event {e} col {c}")
     assert same >= 0.9 * N_EV, same
+
+
+def test_event_and_final_text_files(tmp_path):
+    """saveMode 2 writes event_/final_ clear text (MainRunner.jl:592-609, 690-702, 735-741)."""
+    import adiabatic_raytracer_amd as A
+    p = A.Params(**CONFIGS["flat"])
+    rows = A.trees.main_runner_tree(p, 17, saveMode=2, dir_tag=str(tmp_path), file_tag="x")
+    ev = (tmp_path / "event" / "event_x").read_text().splitlines()
+    fi = (tmp_path / "event" / "final_x").read_text().splitlines()
+    assert len(ev) == 16 and len(fi) == len(rows)
+    for i, line in enumerate(ev):
+        f = line.split()
+        assert len(f) == 19 and int(f[0]) == i + 1 and int(f[-1]) >= 1
+        [float(v) for v in f[1:]]
+    for line, r in zip(fi, rows):
+        f = line.split()
+        assert len(f) == 10 and int(f[0]) == int(r[0]) and int(f[2]) == int(r[1])
+        np.testing.assert_allclose([float(v) for v in f[3:9]],
+                                   [r[2], r[3], float(f[5]), r[4], r[5], r[6]], rtol=1e-15)
+        assert f[9] == "0" or float(f[9]) > 0
