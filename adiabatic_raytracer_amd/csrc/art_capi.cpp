@@ -108,7 +108,9 @@ int propagate_device_impl(const art_params* p, int64_t n, const double* x0, cons
   if ((rc = current_ctx(&c))) return rc;
   hipStream_t s = pick(c, stream);
   art::KParams K = art::make_kparams(*p);
-  art::SegIn in{x0, k0, erg, dw, ln_t0, species};
+  void* u0 = nullptr;  // 16n doubles of fresh state: u0, f0, dt, c0 (init_kernel -> the integrator)
+  if ((rc = pool_get(c, 6, (size_t)n * 16 * sizeof(double), &u0))) return rc;
+  art::SegIn in{x0, k0, erg, dw, ln_t0, species, (double*)u0};
   art::SegOut so{out->x_end, out->k_end, out->u7_end, out->tau_end, out->status, out->n_accept, out->n_reject,
                  0, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
   if (xc && xc->count) {
@@ -119,9 +121,8 @@ int propagate_device_impl(const art_params* p, int64_t n, const double* x0, cons
     so.xpos = xc->pos; so.xk = xc->k; so.xt = xc->t; so.xdw = xc->dw; so.xp = xc->p_nonad;
   }
   HIP_OK(hipMemsetAsync(c->scratch, 0, sizeof(unsigned long long) * (1 + art::N_STATS), s));
-  HIP_OK(hipEventRecord(c->ev0, s));
-  HIP_OK(art::launch_propagate(K, n, in, so, max_crossings, c->scratch, c->scratch + 1, s, &g_last_grid));
-  HIP_OK(hipEventRecord(c->ev1, s));
+  HIP_OK(art::launch_propagate(K, n, in, so, max_crossings, c->scratch, c->scratch + 1, s, &g_last_grid, c->ev0,
+                                c->ev1));
   return ART_OK;
 }
 

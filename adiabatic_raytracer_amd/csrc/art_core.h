@@ -74,6 +74,7 @@ struct KParams {
   double rNS, rNS101;     // rNS, 1.01 rNS
   double rs_gr, rs_eff;   // 2 GNew M / c^2 (GR); flat ? 0 : rs_gr
   double wp2_coef;        // ωp^2 = wp2_coef |Bz| (RayTracer.jl:1153-1154)
+  double wp2n;            // wp2_coef |Bn_coef|: ωp^2 = wp2n |b| / r^3 for either sign of B0
   double mass_a, mass_a2; // m_a, m_a^2
   double g_agg;
   double bndry_lyr, pole_val, rmax, rmax_def;  // boundary layer (RayTracer.jl:1155-1162)
@@ -95,6 +96,7 @@ inline KParams make_kparams(const art_params& p) {
   k.rs_eff = p.flat ? 0.0 : k.rs_gr;
   const double ne_coef = fabs(2.0 * p.omega_pul / sqrt(4.0 * PI / 137.0) * 1.95e-2 * HBAR);
   k.wp2_coef = 4.0 * PI * ne_coef / 137.0 / 5.0e5;
+  k.wp2n = k.wp2_coef * fabs(k.Bn_coef);  // n_e = |2 ω Bz ...| (RayTracer.jl:1153): the sign of B0 drops out
   k.mass_a = p.mass_a;
   k.mass_a2 = p.mass_a * p.mass_a;
   k.g_agg = p.g_agg;
@@ -222,15 +224,17 @@ __host__ __device__ inline void rhs_photon(const KParams& P, const T* u, const T
   T st, ct, sp, cp;
   msincos(u[1], st, ct);
   msincos(u[2] - P.omega * t, sp, cp);  // ψ = φ - ω (time0 + t), time0 = 0 (MainRunner.jl:177)
-  const T ir = 1.0 / rc;
+  // one division for 1/r and 1/|sinθ|
+  const T ast = mabs(st);
+  const T inv_rs = 1.0 / (rc * ast);
+  const T ir = inv_rs * ast;
   const T ir2 = ir * ir;
-  const T iast = 1.0 / mabs(st);
+  const T iast = inv_rs * rc;
   const T sgn_st = msign(st);
   const T kr = u[3] * erg, kt = u[4] * erg, kp = u[5] * erg;
   const DipoleAng<T> d = dipole_ang(P, st, ct, sp, cp);
-  const T Bn = P.Bn_coef * ir2 * ir;
   const T sgb = msign(d.b);
-  const T cB = P.wp2_coef * Bn;                 // ∂ωp² = cB sgn(b) ∂b, ωp² ∝ r^-3
+  const T cB = P.wp2n * ir2 * ir;               // ∂ωp² = cB sgn(b) ∂b, ωp² ∝ r^-3
   const T wp2 = cB * mabs(d.b);
   const T dwp2_r = -3.0 * wp2 * ir;
   const T dwp2_t = cB * sgb * d.bt;
@@ -239,8 +243,10 @@ __host__ __device__ inline void rhs_photon(const KParams& P, const T* u, const T
   metric_tr_d(rc, P.rs_eff, gtt, grr, dgtt, dgrr);
   const T gpp = ir2 * iast * iast;
   const T E2 = E * E;
-  const T iE2 = 1.0 / E2;
-  const T sq = msqrt(grr);
+  const T iE = 1.0 / E;
+  const T iE2 = iE * iE;
+  const bool flat = P.rs_eff == 0.0;  // wave-uniform: g^rr = 1, ∂g^rr = 0
+  const T sq = flat ? T(1.0) : msqrt(grr);
   // k∥ part (vanishes for isotropic plasma, kpar = 0)
   T Q = 0.0, Q_r = 0.0, Q_t = 0.0, Q_p = 0.0, Q_kr = 0.0, Q_kt = 0.0, Q_kp = 0.0;
   if (!P.isotropic) {
@@ -249,7 +255,7 @@ __host__ __device__ inline void rhs_photon(const KParams& P, const T* u, const T
     const T ibeta = 1.0 / (4.0 * d.a1 * d.a1 + d.a2 * d.a2 + d.a3 * d.a3);
     const T G = grr * p * ibeta * iE2;  // Q = G p
     Q = G * p;
-    const T p_r = dgrr / sq * kr * d.a1 - ir2 * pa;
+    const T p_r = flat ? -ir2 * pa : dgrr / sq * kr * d.a1 - ir2 * pa;
     const T p_t = 2.0 * sq * kr * d.a1t + ir * (kt * d.a1 - kp * d.a3 * sgn_st * ct * iast * iast);
     const T p_p = 2.0 * sq * kr * d.a1p + ir * (kt * d.a2p + kp * d.a3p * iast);
     const T beta_t = 8.0 * d.a1 * d.a1t + 2.0 * d.a2 * d.a1;
@@ -263,16 +269,16 @@ __host__ __device__ inline void rhs_photon(const KParams& P, const T* u, const T
     Q_kp = G2 * ir * d.a3 * iast;
   }
   const T omQ = 1.0 - Q;
-  const T fac = C_KM * t * grr_u / E;
+  const T fac = C_KM * t * grr_u * iE;
   if (r <= P.rNS101) {
     du[0] = 0.0; du[1] = 0.0; du[2] = 0.0; du[3] = 0.0; du[4] = 0.0; du[5] = 0.0;
   } else {
     const T ir3 = ir2 * ir;
     const T H_r = 0.5 * (dgtt * E2 + dgrr * kr * kr - 2.0 * ir3 * (kt * kt + iast * iast * kp * kp) +
                          dwp2_r * omQ - wp2 * Q_r);
-    const T H_t = 0.5 * (-2.0 * ct * ir2 * iast * iast / st * kp * kp + dwp2_t * omQ - wp2 * Q_t);
+    const T H_t = 0.5 * (-2.0 * ct * ir2 * iast * iast * (sgn_st * iast) * kp * kp + dwp2_t * omQ - wp2 * Q_t);
     const T H_p = 0.5 * (dwp2_p * omQ - wp2 * Q_p);
-    const T fx = -fac / erg;
+    const T fx = -fac * (1.0 / erg);  // 1/erg: loop-invariant per ray
     du[0] = (grr * kr - 0.5 * wp2 * Q_kr) * fac;
     du[1] = (ir2 * kt - 0.5 * wp2 * Q_kt) * fac;
     du[2] = (gpp * kp - 0.5 * wp2 * Q_kp) * fac;
@@ -290,7 +296,7 @@ __host__ __device__ inline void rhs_photon(const KParams& P, const T* u, const T
     dwp2_T = dwp2_T * (wtot / wgj);
   }
   const T H_T = 0.5 * (dwp2_T * omQ + wp2_T * P.omega * Q_p);
-  du[6] = H_T * t * grr_u / E;
+  du[6] = H_T * t * grr_u * iE;
 }
 
 // func_axion! (RayTracer.jl:95-123) with hamiltonian_axion (:632-640): H = K/2 at fixed
@@ -337,9 +343,8 @@ __host__ __device__ inline void hamiltonian_full(const KParams& P, const T* x, c
   msincos(x[2] - P.omega * Tm, sp, cp);
   const T ir = 1.0 / rc, ir2 = ir * ir, iast = 1.0 / mabs(st), sgn_st = msign(st);
   const DipoleAng<T> d = dipole_ang(P, st, ct, sp, cp);
-  const T Bn = P.Bn_coef * ir2 * ir;
   const T sgb = msign(d.b);
-  const T cB = P.wp2_coef * Bn;
+  const T cB = P.wp2n * ir2 * ir;
   T wp2 = cB * mabs(d.b);
   T dwp2_r = -3.0 * wp2 * ir, dwp2_t = cB * sgb * d.bt, dwp2_p = cB * sgb * d.bp;
   if (P.bndry_lyr > 0.0) {
@@ -423,7 +428,7 @@ __host__ __device__ inline T condition_t(const KParams& P, const T* u, const T& 
     msincos(u[2] - P.omega * t0, sp, cp);
     const DipoleAng<T> d = dipole_ang(P, st, ct, sp, cp);
     if (r > P.rNS) {  // zeroIn = true
-      wpn = P.wp2_coef * P.Bn_coef * mabs(d.b);
+      wpn = P.wp2n * mabs(d.b);
       if (P.bndry_lyr > 0.0) {
         const T w = msqrt(wpn / wpd) + layer_wp(P, r, P.rmax);
         wpn = w * w;
@@ -579,7 +584,7 @@ __host__ __device__ inline ProbLocal<T> prob_local(const KParams& P, const T* po
   L.ergax = erg_eff / msqrt(1.0 - 2.0 * P.GM_c2 / L.r);
   L.wp = 0.0;
   if (L.r > P.rNS) {  // zeroIn = true
-    L.wp = msqrt(P.wp2_coef * Bn * mabs(d.b));
+    L.wp = msqrt(P.wp2n * ir * ir * ir * mabs(d.b));
     if (P.bndry_lyr > 0.0) L.wp = L.wp + layer_wp(P, L.r, P.rmax_def);
   }
   return L;
@@ -607,8 +612,8 @@ __host__ __device__ inline T prob_eval(const KParams& P, double g_agg, const Pro
   T dmu_E[3];
   if (P.isotropic) {
     // grad_x sqrt(kmag² + ωp²), omega_function defaults zeroIn=false, bndry_lyr=-1 (:1421)
-    const T wp2 = P.wp2_coef * Bn * mabs(d.b);
-    const T cB = 0.5 * P.wp2_coef * Bn * msign(d.b);
+    const T wp2 = P.wp2n * ir2 * ir * mabs(d.b);
+    const T cB = 0.5 * P.wp2n * ir2 * ir * msign(d.b);
     const T inv = 1.0 / msqrt(L.kmag * L.kmag + wp2);
     dmu_E[0] = -1.5 * wp2 * ir * inv;
     dmu_E[1] = cB * d.bt * inv;
@@ -617,8 +622,8 @@ __host__ __device__ inline T prob_eval(const KParams& P, double g_agg, const Pro
     // ∇ωp (zeroIn = true, bndry_lyr, Mass_a = m_a; :1427)
     T dwp[3] = {0.0, 0.0, 0.0};
     if (L.r > P.rNS) {
-      const T wgj = msqrt(P.wp2_coef * Bn * mabs(d.b));
-      const T c = P.wp2_coef * Bn * msign(d.b) / (2.0 * wgj);
+      const T wgj = msqrt(P.wp2n * ir2 * ir * mabs(d.b));
+      const T c = P.wp2n * ir2 * ir * msign(d.b) / (2.0 * wgj);
       dwp[0] = -1.5 * wgj * ir;
       dwp[1] = c * d.bt;
       dwp[2] = c * d.bp;
@@ -632,8 +637,9 @@ __host__ __device__ inline T prob_eval(const KParams& P, double g_agg, const Pro
     const T sb = msqrt(beta);
     const T beta_t = 8.0 * d.a1 * d.a1t + 2.0 * d.a2 * d.a1;
     const T beta_p = 8.0 * d.a1 * d.a1p + 2.0 * d.a2 * d.a2p + 2.0 * d.a3 * d.a3p;
-    const T f = 1.95e-2 * Bn;
-    const T dB[3] = {-3.0 * f * sb * ir, f * beta_t / (2.0 * sb), f * beta_p / (2.0 * sb)};
+    const T f = 1.95e-2 * Bn;        // signed: the components B^i (return_comp 1..3)
+    const T fa = 1.95e-2 * mabs(Bn);  // |B| (return_comp 0) for either sign of B0
+    const T dB[3] = {-3.0 * fa * sb * ir, fa * beta_t / (2.0 * sb), fa * beta_p / (2.0 * sb)};
     // ∇ of B^r √g^rr, B^θ/r, B^φ/(r|sinθ|) times 1.95e-2 (return_comp 1..3, :1432)
     T gtt_f, grr_f, dgtt_f, dgrr_f;
     metric_tr_d(L.r, P.rs_eff, gtt_f, grr_f, dgtt_f, dgrr_f);
@@ -721,7 +727,7 @@ __host__ __device__ inline T sampler_condition(const KParams& P, const T* x, con
   const T f = msqrt(nrm);
   w0 = w0 * f; w1 = w1 * f; w2 = w2 * f;
   const DipoleAng<T> d = dipole_ang(P, st, ct, sp, cp);
-  T wp2 = P.wp2_coef * P.Bn_coef * ir2 * ir * mabs(d.b);  // GJ_Model_ωp_vec: no zeroIn
+  T wp2 = P.wp2n * ir2 * ir * mabs(d.b);  // GJ_Model_ωp_vec: no zeroIn
   if (P.bndry_lyr > 0.0 && r >= P.rNS) {
     const T w = msqrt(wp2) + layer_wp(P, r, P.rmax);
     wp2 = w * w;
@@ -744,7 +750,7 @@ __host__ __device__ inline T wp_cart(const KParams& P, const T* x) {
   const T rho = msqrt(rho2);
   const T irho = 1.0 / rho;
   const DipoleAng<T> d = dipole_ang(P, rho * ir, x[2] * ir, x[1] * irho, x[0] * irho);
-  T wp = msqrt(P.wp2_coef * P.Bn_coef * ir * ir * ir * mabs(d.b));
+  T wp = msqrt(P.wp2n * ir * ir * ir * mabs(d.b));
   if (P.bndry_lyr > 0.0 && r >= P.rNS) wp = wp + layer_wp(P, r, P.rmax);
   return wp;
 }

@@ -88,7 +88,7 @@ __host__ __device__ inline T gj_wp(const KParams& P, const T& r, const T& th, co
   msincos(ph - P.omega * t, sp, cp);
   const DipoleAng<T> d = dipole_ang(P, st, ct, sp, cp);
   if (dout) *dout = d;
-  T wp = msqrt(P.wp2_coef * P.Bn_coef / (r * r * r) * mabs(d.b));
+  T wp = msqrt(P.wp2n / (r * r * r) * mabs(d.b));  // n_e = |2 ω Bz ...|: either sign of B0
   if (with_layer && P.bndry_lyr > 0.0 && r >= P.rNS) wp = wp + layer_wp(P, r, P.rmax);
   return wp;
 }

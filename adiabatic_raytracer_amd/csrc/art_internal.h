@@ -9,6 +9,7 @@ namespace art {
 struct SegIn {
   const double *x0, *k0, *erg, *dw, *lnt0;
   const int8_t* species;
+  double* u0;  // 16n device scratch filled by init_kernel: u0 (7), f(u0) (7), dt, c0
 };
 
 struct SegOut {
@@ -21,8 +22,12 @@ struct SegOut {
 constexpr int N_STATS = 8;  // propagate statistics: attempts, accepted, root re-steps, scan evals,
                             // interpolant-root evals, rays, init RHS, (reserved)
 int persistent_blocks(const void* func, int64_t work);
+// propagate = init (u0 of every ray) -> the persistent integrator -> finalize (Cartesian
+// end state, conversion probability at the crossings); ev0/ev1 (may be null) bracket the
+// integrator kernel alone.
 hipError_t launch_propagate(const KParams& P, int64_t n, const SegIn& in, const SegOut& out, int32_t max_crossings,
-                            unsigned long long* queue, unsigned long long* stats, hipStream_t s, int* grid_out);
+                            unsigned long long* queue, unsigned long long* stats, hipStream_t s, int* grid_out,
+                            hipEvent_t ev0, hipEvent_t ev1);
 hipError_t launch_sample(const KParams& P, double maxR, uint64_t seed, int64_t ray_offset, int64_t n, double* x,
                          double* k, double* erg, double* vifty, int32_t* w, int32_t* att, unsigned long long* queue,
                          hipStream_t s);

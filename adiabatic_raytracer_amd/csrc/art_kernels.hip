@@ -121,7 +121,23 @@ __device__ inline double scan_point(const KParams& P, const double* u0, const do
                                     const double* f1, double h, double tau, double th) {
   double ui[7];
   hermite7(u0, f0, u1, f1, h, th, ui);
-  return condition_t(P, ui, exp(tau + th * h));
+  const double tt = tau + th * h;
+  return condition_t(P, ui, exp(tt));
+}
+
+// scan_point on an interpolant parked in LDS: S = the lane's base in the [slot][component]
+// [lane] layout, slots 0-3 = u0, f0, u1, f1, slot 4 = (h, τ). The cooperative grid pass and
+// the per-lane bracket evaluations both go through here.
+__device__ inline double scan_point_lds(const KParams& P, const double* S, int stride, double th) {
+  double u0[7], f0[7], u1[7], f1[7];
+#pragma unroll
+  for (int i = 0; i < 7; ++i) {
+    u0[i] = S[(0 * 7 + i) * stride];
+    f0[i] = S[(1 * 7 + i) * stride];
+    u1[i] = S[(2 * 7 + i) * stride];
+    f1[i] = S[(3 * 7 + i) * stride];
+  }
+  return scan_point(P, u0, f0, u1, f1, S[(4 * 7 + 0) * stride], S[(4 * 7 + 1) * stride], th);
 }
 
 // Completes this wave's LDS traffic before other lanes of the same wave read it.
@@ -136,7 +152,8 @@ __device__ inline unsigned sign_code(double c) { return isnan(c) ? 3u : (c > 0.0
 
 // ode_determine_initdt (DiffEqBase) for an order-6 method; one extra RHS evaluation.
 __device__ inline double initdt(const KParams& P, bool photon, double erg, const double* u0, const double* f0,
-                                double tau0, double dtmax) {
+                                double tau0, double dtmax, int& probe) {
+  probe = 0;
   double d0 = 0.0, d1 = 0.0, sk[7];
 #pragma unroll
   for (int i = 0; i < 7; ++i) {
@@ -155,6 +172,7 @@ __device__ inline double initdt(const KParams& P, bool photon, double erg, const
 #pragma unroll
   for (int i = 0; i < 7; ++i) u1[i] = u0[i] + dt0 * f0[i];
   rhs(P, photon, u1, tau0 + dt0, erg, f1);
+  probe = 1;
   bool same = true;
   double d2 = 0.0;
 #pragma unroll
@@ -278,7 +296,7 @@ __constant__ StageTable c_rk4 = {
     {-1, 0, 1, -1, -1, -1, -1, -1},
     0.0, 0.0, {0, 0, 0, 0, 0}, 0.0};
 
-enum LaneMode { M_IDLE = 0, M_INIT = 1, M_STEP = 2, M_ROOT = 3 };
+enum LaneMode { M_IDLE = 0, M_STEP = 2, M_ROOT = 3 };
 
 constexpr int BLOCK = 256;
 constexpr int SCAN_WORDS = 4;  // 2-bit codes for up to 64 grid points (interp_points <= 65)
@@ -289,10 +307,10 @@ constexpr int SCAN_WORDS = 4;  // 2-bit codes for up to 64 grid points (interp_p
 
 // ---------------------------------------------------------------------------
 // One loop iteration = one step attempt for every live lane: a runtime loop over the
-// stage slots with the RHS inlined once. Lanes that just received a ray (M_INIT) use
-// slots 0-1 for f(u0) and Hairer's initial-dt probe; lanes polishing a crossing (M_ROOT)
-// re-step from the step start. After the slots, one condition call site serves the init
-// sign, the root polish and the ContinuousCallback scan of accepted steps.
+// stage slots with the RHS inlined once. A lane that takes a new ray loads its fresh state
+// (init_kernel) and steps in the same iteration; lanes polishing a crossing (M_ROOT)
+// re-step from the step start. After the slots, the wave-cooperative scan and one per-lane
+// condition call site (brackets, Illinois, root polish) serve the ContinuousCallback.
 template <int INTEG>
 __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(const KParams P, const int64_t n, const SegIn in,
                                                            const SegOut out, const int32_t max_crossings,
@@ -326,7 +344,7 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
   int post_s = 0, r_side = 0, r_it = 0;
   int wnext = 0, wend = 0;
   bool exhausted = false;
-  unsigned s_att = 0, s_acc = 0, s_root = 0, s_scan = 0, s_interp = 0, s_rays = 0, s_init = 0;
+  unsigned s_att = 0, s_acc = 0, s_root = 0, s_scan = 0, s_interp = 0, s_rays = 0;
 #pragma unroll
   for (int i = 0; i < 7; ++i) { u[i] = 0.0; f[i] = 0.0; }
 
@@ -349,13 +367,19 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
         const int take = (wend - wnext) < cnt ? (wend - wnext) : cnt;
         if (mode == M_IDLE && rank < take) {
           ray = wnext + rank;
-          mode = M_INIT;
-          // initial state (RayTracer.jl:179-216)
-          const double xs[3] = {in.x0[ray], in.x0[n + ray], in.x0[2 * n + ray]};
-          const double ks[3] = {in.k0[ray], in.k0[n + ray], in.k0[2 * n + ray]};
+          mode = M_STEP;
+          // fresh segment: u0, f(u0), the initial dt and the initial condition value, all
+          // precomputed by init_kernel
           erg = in.erg[ray];
           photon = in.species[ray] != ART_AXION;
-          initial_state(P, xs, ks, erg, in.dw[ray], u);
+#pragma unroll
+          for (int i = 0; i < 7; ++i) {
+            u[i] = in.u0[i * n + ray];
+            f[i] = in.u0[(7 + i) * n + ray];
+          }
+          dt = in.u0[14 * n + ray];
+          cprev = in.u0[15 * n + ray];
+          sprev = isnan(cprev) ? 0 : sgn(cprev);
           tau = in.lnt0[ray];
           n_acc = n_rej = ncross = iter = 0;
           just_evented = false;
@@ -383,8 +407,6 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
     double kA[7], y[7], kk[7];
 #pragma unroll
     for (int i = 0; i < 7; ++i) kA[i] = 0.0;  // read (times a zero coefficient) before its first store
-    double dt0 = 0.0;
-    bool init_short = false;  // initdt returned before its probe RHS
 #pragma unroll 1
     for (int s = 0; s < NSLOT; ++s) {
       const double cf = T.cf[s], cA = T.cA[s];
@@ -401,78 +423,17 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
       }
 #pragma unroll
       for (int i = 0; i < 7; ++i) y[i] = u[i] + hs * acc[i];
-      double ty = tau + T.ct[s] * hs;
-      bool active = (mode == M_STEP || mode == M_ROOT);
-      if (mode == M_INIT) {
-        if (s == 0) {  // f(u0)
-#pragma unroll
-          for (int i = 0; i < 7; ++i) y[i] = u[i];
-          ty = tau;
-          active = true;
-        } else if (s == 1 && !RK4 && !init_short) {  // ode_determine_initdt's probe f(u0 + dt0 f0)
-#pragma unroll
-          for (int i = 0; i < 7; ++i) y[i] = u[i] + dt0 * f[i];
-          ty = tau + dt0;
-          active = true;
-        }
-      }
-      if (active) {
+      const double ty = tau + T.ct[s] * hs;
+      if (mode == M_STEP || mode == M_ROOT) {
         rhs(P, photon, y, ty, erg, kk);
-        if (mode != M_INIT) {
-          if (T.storeA[s]) {
+        if (T.storeA[s]) {
 #pragma unroll
-            for (int i = 0; i < 7; ++i) kA[i] = kk[i];
-          }
-          const int sl = T.storeL[s];
-          if (sl >= 0) {
+          for (int i = 0; i < 7; ++i) kA[i] = kk[i];
+        }
+        const int sl = T.storeL[s];
+        if (sl >= 0) {
 #pragma unroll
-            for (int i = 0; i < 7; ++i) L[(sl * 7 + i) * BLOCK] = kk[i];
-          }
-        } else if (s == 0) {
-#pragma unroll
-          for (int i = 0; i < 7; ++i) f[i] = kk[i];
-          if (photon && u[0] < P.rNS) u[0] = P.rNS;  // hamiltonian's in-place clamp (:531)
-          s_init += 1;
-          if (RK4) {
-            dt = (tend - tau) / P.n_fixed;
-          } else {  // ode_determine_initdt, first half
-            double d0 = 0.0, d1 = 0.0;
-#pragma unroll
-            for (int i = 0; i < 7; ++i) {
-              const double sk = P.abstol + fabs(u[i]) * P.reltol;
-              d0 += (u[i] / sk) * (u[i] / sk);
-              d1 += (f[i] / sk) * (f[i] / sk);
-            }
-            d0 = sqrt(d0 / 7.0);
-            d1 = sqrt(d1 / 7.0);
-            dt0 = (d0 < 1e-5 || d1 < 1e-5) ? 1e-6 : 0.01 * (d0 / d1);
-            dt0 = fmin(dt0, tend - tau);
-            const double at = fabs(tau);
-            if (dt0 < 10.0 * (nextafter(at, INFINITY) - at)) {
-              dt = fmax(1e-6, P.dtmin);
-              init_short = true;
-            }
-          }
-        } else {  // ode_determine_initdt, second half
-          s_init += 1;
-          bool same = true;
-          double d1 = 0.0, d2 = 0.0;
-#pragma unroll
-          for (int i = 0; i < 7; ++i) {
-            const double sk = P.abstol + fabs(u[i]) * P.reltol;
-            same = same && (f[i] == kk[i]);
-            d1 += (f[i] / sk) * (f[i] / sk);
-            d2 += ((kk[i] - f[i]) / sk) * ((kk[i] - f[i]) / sk);
-          }
-          d1 = sqrt(d1 / 7.0);
-          d2 = sqrt(d2 / 7.0) / dt0;
-          if (same) {
-            dt = fmax(P.dtmin, 100.0 * dt0);
-          } else {
-            const double mx = fmax(d1, d2);
-            const double dt1 = (mx <= 1e-15) ? fmax(1e-6, dt0 * 1e-3) : pow(10.0, -(2.0 + log10(mx)) / 6.0);
-            dt = fmax(P.dtmin, fmin(fmin(100.0 * dt0, dt1), tend - tau));
-          }
+          for (int i = 0; i < 7; ++i) L[(sl * 7 + i) * BLOCK] = kk[i];
         }
       }
     }
@@ -544,20 +505,21 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
     //     Each item leaves a 2-bit sign code in the source lane's LDS words.
     const int nper = npts - 1;
     const double inv_n = 1.0 / double(nper);
+    // every lane parks (u, f, y, kk, h, τ) in its LDS slots (free after the error estimate):
+    // the scan reads the interpolants from there, and the registers stay free until the
+    // state is reloaded after the scan
+#pragma unroll
+    for (int i = 0; i < 7; ++i) {
+      L[(0 * 7 + i) * BLOCK] = u[i];
+      L[(1 * 7 + i) * BLOCK] = f[i];
+      L[(2 * 7 + i) * BLOCK] = y[i];
+      L[(3 * 7 + i) * BLOCK] = kk[i];
+    }
+    L[(4 * 7 + 0) * BLOCK] = hs;
+    L[(4 * 7 + 1) * BLOCK] = tau;
     const unsigned long long smask = __ballot(scan);
     if (smask != 0ull) {
       const int ns = __popcll(smask);
-      // every lane parks (u, f, y, kk) in its LDS slots and reloads them after the pass, so
-      // their registers are free while the pass holds a source lane's interpolant
-#pragma unroll
-      for (int i = 0; i < 7; ++i) {
-        L[(0 * 7 + i) * BLOCK] = u[i];
-        L[(1 * 7 + i) * BLOCK] = f[i];
-        L[(2 * 7 + i) * BLOCK] = y[i];
-        L[(3 * 7 + i) * BLOCK] = kk[i];
-      }
-      L[(4 * 7 + 0) * BLOCK] = hs;
-      L[(4 * 7 + 1) * BLOCK] = tau;
       if (scan) {
         srcl[wbase + __popcll(smask & ((1ull << lane) - 1ull))] = lane;
 #pragma unroll
@@ -572,17 +534,7 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
       for (int w0 = 0; w0 < total; w0 += 64) {
         if (w0 + lane < total) {
           const int src = srcl[wbase + c];
-          const double* S = lds + wbase + src;
-          double u0[7], f0[7], u1[7], f1[7];
-#pragma unroll
-          for (int i = 0; i < 7; ++i) {
-            u0[i] = S[(0 * 7 + i) * BLOCK];
-            f0[i] = S[(1 * 7 + i) * BLOCK];
-            u1[i] = S[(2 * 7 + i) * BLOCK];
-            f1[i] = S[(3 * 7 + i) * BLOCK];
-          }
-          const double cv = scan_point(P, u0, f0, u1, f1, S[(4 * 7 + 0) * BLOCK], S[(4 * 7 + 1) * BLOCK],
-                                       double(j) * inv_n);
+          const double cv = scan_point_lds(P, lds + wbase + src, BLOCK, double(j) * inv_n);
           atomicOr(&codes[((j - 1) >> 4) * BLOCK + wbase + src], sign_code(cv) << (2 * ((j - 1) & 15)));
           if (j == nper) lastv[wbase + src] = cv;
           s_scan += 1;
@@ -595,13 +547,6 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
         }
       }
       wave_lds_sync();
-#pragma unroll
-      for (int i = 0; i < 7; ++i) {
-        u[i] = L[(0 * 7 + i) * BLOCK];
-        f[i] = L[(1 * 7 + i) * BLOCK];
-        y[i] = L[(2 * 7 + i) * BLOCK];
-        kk[i] = L[(3 * 7 + i) * BLOCK];
-      }
     }
 
     // (b) Per lane: walk the sign codes exactly as the sequential scan would (NaN resets the
@@ -611,7 +556,7 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
     //     here only happen at brackets, Illinois points and root polish steps.
     //     ph: 0 done, 1 single point (INIT / ROOT), 2 walk codes, 3 Illinois, 5 value at the
     //     change point, 6 value at the bracket start, 7 value at the step's last nonzero point.
-    int ph = (mode == M_INIT || mode == M_ROOT) ? 1 : (scan ? 2 : 0);
+    int ph = (mode == M_ROOT) ? 1 : (scan ? 2 : 0);
     int ip = 1, last_j = 0;
     int last_s = sprev;
     double last_c = cprev;
@@ -683,21 +628,19 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
       if (ph == 3) th = i_tr;
       else if (ph == 5) th = double(ip) * inv_n;
       else if (ph == 6 || ph == 7) th = double(last_j) * inv_n;
+      // one condition call site: the fresh state (INIT), the re-stepped end (ROOT) or the
+      // interpolant at th -- the latter exactly as scan_point forms it (bit-identical)
       double ci;
-      if (mode == M_INIT) {
-        ci = condition_t(P, u, exp(tau));
-      } else if (mode == M_ROOT) {
-        ci = condition_t(P, y, exp(tau + hs));
+      if (mode == M_ROOT) {  // the re-stepped end y (slot 2) at τ + h
+        double ui[7];
+#pragma unroll
+        for (int i = 0; i < 7; ++i) ui[i] = L[(2 * 7 + i) * BLOCK];
+        ci = condition_t(P, ui, exp(tau + hs));
       } else {
-        ci = scan_point(P, u, f, y, kk, hs, tau, th);
+        ci = scan_point_lds(P, L, BLOCK, th);
         s_interp += 1;
       }
-      if (mode == M_INIT) {
-        cprev = ci;
-        sprev = isnan(ci) ? 0 : sgn(ci);
-        ph = 0;
-        mode = M_STEP;
-      } else if (mode == M_ROOT) {
+      if (mode == M_ROOT) {
         // bracketed polish on the true trajectory (Newton with the interpolant slope, then Illinois)
         s_root += 1;
         ++r_it;
@@ -770,6 +713,13 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
         }
       }
     }
+#pragma unroll
+    for (int i = 0; i < 7; ++i) {
+      u[i] = L[(0 * 7 + i) * BLOCK];
+      f[i] = L[(1 * 7 + i) * BLOCK];
+      y[i] = L[(2 * 7 + i) * BLOCK];
+      kk[i] = L[(3 * 7 + i) * BLOCK];
+    }
     if (hit) mode = M_ROOT;
     if (root_done) {
       const double tau_r = tau + hs;
@@ -798,13 +748,11 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
       else if (iter >= P.maxiters) finish = ART_STATUS_MAXITERS;
     }
 
-    if (finish >= 0) {
-      double xe[3], ke[3];
-      back_transform(P, u, erg, xe, ke);
+    if (finish >= 0) {  // the raw state; finalize_kernel back-transforms it in place (RayTracer.jl:393-416)
 #pragma unroll
       for (int c = 0; c < 3; ++c) {
-        out.x_end[c * n + ray] = xe[c];
-        out.k_end[c * n + ray] = ke[c];
+        out.x_end[c * n + ray] = u[c];
+        out.k_end[c * n + ray] = u[3 + c];
       }
       out.u7_end[ray] = u[6];
       out.tau_end[ray] = tau;
@@ -818,24 +766,82 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
   }
 
   // wave-reduce the statistics and add them once per wave
-  const unsigned v[7] = {s_att, s_acc, s_root, s_scan, s_interp, s_rays, s_init};
+  const unsigned v[6] = {s_att, s_acc, s_root, s_scan, s_interp, s_rays};
 #pragma unroll
-  for (int k = 0; k < 7; ++k) {
+  for (int k = 0; k < 6; ++k) {
     unsigned long long x = v[k];
     for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off);
     if (lane == 0 && x) atomicAdd(&stats[k], x);
   }
 }
 
-// Conversion probability of every recorded crossing (get_Prob_nonAD with Nc = 1,
-// MainRunner.jl:265), run right after the integrator on the same stream: keeping this
-// ~400-FLOP, rarely taken path out of the integrator loop saves it ~90 registers.
-__global__ __launch_bounds__(256) void crossing_prob_kernel(const KParams P, const int64_t n, const SegIn in,
-                                                            const SegOut out) {
+// Fresh state of every segment, one thread per ray: u0 (RayTracer.jl:179-216: k_norm_Cart
+// onto the axion shell, Cartesian -> (r, θ, φ), covariant celerity), f(u0) with the
+// hamiltonian's in-place clamp (:531), the initial dt (ode_determine_initdt, order 6, with
+// its probe RHS; RK4: the fixed step) and the condition value that seeds the callback's
+// sign memory. Kept out of the persistent integrator, whose registers it would otherwise
+// crowd. Out: in.u0 = 16n doubles [u0 (7) | f0 (7) | dt | c0].
+__global__ __launch_bounds__(256) void init_kernel(const KParams P, const int64_t n, const SegIn in,
+                                                   unsigned long long* __restrict__ stats) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  unsigned nrhs = 0;
+  if (i < n) {
+    const double xs[3] = {in.x0[i], in.x0[n + i], in.x0[2 * n + i]};
+    const double ks[3] = {in.k0[i], in.k0[n + i], in.k0[2 * n + i]};
+    const double erg = in.erg[i], tau = in.lnt0[i];
+    const bool photon = in.species[i] != ART_AXION;
+    double u[7], f[7];
+    initial_state(P, xs, ks, erg, in.dw[i], u);
+    rhs(P, photon, u, tau, erg, f);
+    nrhs = 1;
+    if (photon && u[0] < P.rNS) u[0] = P.rNS;  // hamiltonian's in-place clamp (:531)
+    double dt;
+    if (P.integrator == ART_RK4) {
+      dt = (P.ln_t_end - tau) / P.n_fixed;
+    } else {
+      int probe = 0;
+      dt = initdt(P, photon, erg, u, f, tau, P.ln_t_end - tau, probe);
+      nrhs += probe;
+    }
+    const double c0 = condition_t(P, u, exp(tau));
+#pragma unroll
+    for (int c = 0; c < 7; ++c) {
+      in.u0[c * n + i] = u[c];
+      in.u0[(7 + c) * n + i] = f[c];
+    }
+    in.u0[14 * n + i] = dt;
+    in.u0[15 * n + i] = c0;
+  }
+  unsigned long long x = nrhs;  // init RHS evaluations -> stats[6]
+  for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off);
+  if ((threadIdx.x & 63) == 0 && x) atomicAdd(&stats[6], x);
+}
+
+// End state in Cartesian form (back-transform, RayTracer.jl:393-416) from the raw state the
+// integrator left in x_end / k_end / u7_end, and the conversion probability of every
+// recorded crossing (get_Prob_nonAD with Nc = 1, MainRunner.jl:265). One thread per ray.
+__global__ __launch_bounds__(256) void finalize_kernel(const KParams P, const int64_t n, const SegIn in,
+                                                       const SegOut out) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const int m = out.xcount[i] < out.cap ? out.xcount[i] : out.cap;
   const double erg = in.erg[i];
+  {
+    double u[7], xe[3], ke[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      u[c] = out.x_end[c * n + i];
+      u[3 + c] = out.k_end[c * n + i];
+    }
+    u[6] = out.u7_end[i];
+    back_transform(P, u, erg, xe, ke);
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      out.x_end[c * n + i] = xe[c];
+      out.k_end[c * n + i] = ke[c];
+    }
+  }
+  if (!out.xcount) return;
+  const int m = out.xcount[i] < out.cap ? out.xcount[i] : out.cap;
   for (int j = 0; j < m; ++j) {
     double x[3], k[3];
 #pragma unroll
@@ -1122,20 +1128,26 @@ int persistent_blocks(const void* func, int64_t work) {
 }
 
 hipError_t launch_propagate(const KParams& P, int64_t n, const SegIn& in, const SegOut& out, int32_t max_crossings,
-                            unsigned long long* queue, unsigned long long* stats, hipStream_t s, int* grid_out) {
+                            unsigned long long* queue, unsigned long long* stats, hipStream_t s, int* grid_out,
+                            hipEvent_t ev0, hipEvent_t ev1) {
+  const unsigned g1 = (unsigned)((n + 255) / 256);
+  hipLaunchKernelGGL(init_kernel, dim3(g1), dim3(256), 0, s, P, n, in, stats);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
   const void* fn = (P.integrator == ART_RK4) ? (const void*)propagate_kernel<ART_RK4>
                                              : (const void*)propagate_kernel<ART_VERN6>;
   const int grid = persistent_blocks(fn, n);
   if (grid_out) *grid_out = grid;
+  if (ev0 && (e = hipEventRecord(ev0, s)) != hipSuccess) return e;
   if (P.integrator == ART_RK4)
     hipLaunchKernelGGL(propagate_kernel<ART_RK4>, dim3(grid), dim3(BLOCK), 0, s, P, n, in, out, max_crossings, queue,
                        stats);
   else
     hipLaunchKernelGGL(propagate_kernel<ART_VERN6>, dim3(grid), dim3(BLOCK), 0, s, P, n, in, out, max_crossings, queue,
                        stats);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess || !out.xcount) return e;
-  hipLaunchKernelGGL(crossing_prob_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, P, n, in, out);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  if (ev1 && (e = hipEventRecord(ev1, s)) != hipSuccess) return e;
+  hipLaunchKernelGGL(finalize_kernel, dim3(g1), dim3(256), 0, s, P, n, in, out);
   return hipGetLastError();
 }
 

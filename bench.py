@@ -37,15 +37,16 @@ CONFIGS = {
 
 
 def flops_per_launch(stats, fl, integrator="vern6"):
-    """Algorithmic FLOPs of one propagate launch from the kernel's own counters and the
-    instrumented per-operation counts for this configuration (tools/flops.json, made by
-    tools/count_flops.cpp from the same art_core.h templates the kernel runs)."""
+    """Algorithmic FLOPs of one launch of the integrator kernel (propagate_kernel) from its own
+    counters and the instrumented per-operation counts for this configuration
+    (tools/flops.json, made by tools/count_flops.cpp from the same art_core.h templates the
+    kernel runs). The per-ray set-up (init_kernel) and back-transform (finalize_kernel) are
+    separate kernels and are not counted here."""
     att, root, scan, interp = stats["attempts"], stats["root_steps"], stats["scan_evals"], stats["interp_evals"]
     step = fl["rk4_attempt"] if integrator == "rk4" else fl["vern6_attempt"]
     return (att * step + root * (step + fl["condition"])
             + scan * (fl["hermite_point"] + fl["condition_scan_point"])
-            + interp * (fl["hermite_point"] + fl["condition"]) + stats["init_rhs"] * fl["rhs_photon"]
-            + stats["rays"] * (fl["initial_state"] + fl["condition"] + fl["back_transform"]))
+            + interp * (fl["hermite_point"] + fl["condition"]))
 
 
 # Algorithmic HBM bytes of one propagate launch (DESIGN.md §4). Per segment: inputs x0, k0

@@ -32,8 +32,9 @@ def test_sincos_within_one_ulp():
 
 @pytest.mark.parametrize("cfg", sorted(CONFIGS))
 @pytest.mark.parametrize("species", [1, 0])
-def test_rhs(cfg, species, oracle_lib):
-    p = oracle_lib.make_params(**CONFIGS[cfg])
+@pytest.mark.parametrize("b0sign", [1.0, -1.0])  # main_runner_tree backtraces with -B0 (:585)
+def test_rhs(cfg, species, b0sign, oracle_lib):
+    p = oracle_lib.make_params(B0=1e14 * b0sign, **CONFIGS[cfg])
     U, tau = random_states(400, seed=3 + species, rmin=9.5)
     for i in range(U.shape[1]):
         a = cc.rhs(p, species, U[:, i], tau[i], ERG)
@@ -56,8 +57,9 @@ def test_boundary_layer_rhs(cfg, oracle_lib):
 
 @pytest.mark.parametrize("cfg", sorted(CONFIGS))
 @pytest.mark.parametrize("iso", [False, True])
-def test_condition(cfg, iso, oracle_lib):
-    p = oracle_lib.make_params(isotropic=iso, **CONFIGS[cfg])
+@pytest.mark.parametrize("b0sign", [1.0, -1.0])  # main_runner_tree backtraces with -B0 (:585)
+def test_condition(cfg, iso, b0sign, oracle_lib):
+    p = oracle_lib.make_params(isotropic=iso, B0=1e14 * b0sign, **CONFIGS[cfg])
     U, tau = random_states(400, seed=5, rmin=9.5)
     for i in range(U.shape[1]):
         a, b = cc.condition(p, U[:, i], tau[i]), oracle_lib.condition(p, U[:, i], tau[i])
@@ -67,8 +69,9 @@ def test_condition(cfg, iso, oracle_lib):
 
 
 @pytest.mark.parametrize("cfg", sorted(CONFIGS))
-def test_hamiltonian(cfg, oracle_lib):
-    p = oracle_lib.make_params(**CONFIGS[cfg])
+@pytest.mark.parametrize("b0sign", [1.0, -1.0])  # main_runner_tree backtraces with -B0 (:585)
+def test_hamiltonian(cfg, b0sign, oracle_lib):
+    p = oracle_lib.make_params(B0=1e14 * b0sign, **CONFIGS[cfg])
     U, tau = random_states(300, seed=13, rmin=9.0)  # r < rNS exercises the clamp (RayTracer.jl:531)
     for i in range(U.shape[1]):
         x, k, T, E = U[0:3, i], U[3:6, i] * ERG, np.exp(tau[i]), -U[6, i]
@@ -81,7 +84,8 @@ def test_hamiltonian(cfg, oracle_lib):
 
 
 @pytest.mark.parametrize("cfg", sorted(CONFIGS))
-def test_transforms_and_probability(cfg, oracle_lib):
+@pytest.mark.parametrize("b0sign", [1.0, -1.0])  # main_runner_tree backtraces with -B0 (:585)
+def test_transforms_and_probability(cfg, b0sign, oracle_lib):
     p = oracle_lib.make_params(**CONFIGS[cfg])
     s = oracle_lib.sample(p, oracle_lib.find_conversion_surface(p), 1769, 0, 64, nthreads=1)
     n = 64
@@ -91,8 +95,9 @@ def test_transforms_and_probability(cfg, oracle_lib):
         assert np.allclose(u1, u2, rtol=1e-13, atol=0)
         x1, k1 = cc.back_transform(p, u2, e)
         assert np.allclose(x1, x, rtol=1e-12, atol=1e-12)                 # round trip position
-        p1 = cc.prob_single(p, x, k, e)
-        p2 = oracle_lib.get_prob_nonad(p, x, k, [e])[0]
+        pb = oracle_lib.make_params(B0=1e14 * b0sign, **CONFIGS[cfg])
+        p1 = cc.prob_single(pb, x, k, e)
+        p2 = oracle_lib.get_prob_nonad(pb, x, k, [e])[0]
         assert abs(p1 - p2) <= 1e-9 * abs(p2), (i, p1, p2)
 
 

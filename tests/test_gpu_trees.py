@@ -103,7 +103,7 @@ def test_main_runner_rows_match_oracle(oracle_lib, tmp_path):
     rows = A.trees.main_runner_tree(p, N_EV + 1, saveMode=1, dir_tag=str(tmp_path), file_tag="t")
     ref = T.main_runner_rows(po, N_EV + 1, saveMode=1)
     f = list((tmp_path / "npy").glob("tree_*.npy"))
-    assert len(f) == 1 and np.array_equal(np.load(f[0]), rows)
+    assert len(f) == 1 and np.array_equal(np.load(f[0]), rows, equal_nan=True)
     ev_g, ev_o = rows[:, 0], ref[:, 0]
     same = 0
     for e in range(1, N_EV + 1):
