@@ -49,13 +49,13 @@ def flops_per_launch(stats, fl, integrator="vern6"):
             + interp * (fl["hermite_point"] + fl["condition"]))
 
 
-# Algorithmic HBM bytes of one propagate launch. Per segment: inputs x0, k0
-# (2 x 3 f64), erg, dw, ln_t0 (f64), species (i8) = 73 B; outputs x_end, k_end (2 x 3 f64),
-# u7, tau (f64), status, n_accept, n_reject, n_cross (i32) = 80 B. Per recorded crossing:
-# position, k (2 x 3 f64), t, dw (f64) written = 64 B; the probability kernel re-reads
-# position, k, dw (56 B) and writes P (8 B).
-BYTES_PER_SEGMENT = 73 + 80
-BYTES_PER_CROSSING = 64 + 56 + 8
+# Algorithmic HBM bytes of one launch of the integrator kernel. Per segment:
+# it reads erg, ln_t0 (f64), species (i8) and the 16-double fresh state init_kernel wrote
+# (u0, f0, dt, c0) = 145 B, and writes the end state x_end, k_end (2 x 3 f64), u7, tau (f64)
+# and status, n_accept, n_reject, n_cross (i32) = 80 B. Per recorded crossing it writes
+# position, k (2 x 3 f64), t, dw (f64) = 64 B.
+BYTES_PER_SEGMENT = 145 + 80
+BYTES_PER_CROSSING = 64
 
 
 def cpu_baseline(params, x0, k0, erg, seed, threads):
