@@ -99,9 +99,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal of the N > 1 path on a one-GPU box: every rank on one device, gloo
+    # (ART_BENCH_DEVICE / ART_BENCH_BACKEND); the real runs use one GPU per rank and RCCL
+    if "ART_BENCH_DEVICE" in os.environ:
+        local = int(os.environ["ART_BENCH_DEVICE"])
+    backend = os.environ.get("ART_BENCH_BACKEND", "nccl")
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
 
     params = A.Params(integrator=args.integrator, **CONFIGS[args.config])
     eng = Engine(params, device=local)
