@@ -7,6 +7,7 @@
 
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -108,6 +109,10 @@ int propagate_device_impl(const art_params* p, int64_t n, const double* x0, cons
   if ((rc = current_ctx(&c))) return rc;
   hipStream_t s = pick(c, stream);
   art::KParams K = art::make_kparams(*p);
+  // ART_SCAN_CERT=0 switches the certified-negative scan off (A/B tests: the results are
+  // bit-identical either way, tests/test_gpu_scan_cert.py)
+  if (const char* e = std::getenv("ART_SCAN_CERT"))
+    if (e[0] == '0') K.cert_fac = __builtin_inf();
   void* u0 = nullptr;  // 16n doubles of fresh state: u0, f0, dt, c0 (init_kernel -> the integrator)
   if ((rc = pool_get(c, 6, (size_t)n * 16 * sizeof(double), &u0))) return rc;
   art::SegIn in{x0, k0, erg, dw, ln_t0, species, (double*)u0};

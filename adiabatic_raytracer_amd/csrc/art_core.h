@@ -80,6 +80,10 @@ struct KParams {
   double bndry_lyr, pole_val, rmax, rmax_def;  // boundary layer (RayTracer.jl:1155-1162)
   double GM_c2;           // GNew M / c^2 (Cristoffel, get_Prob_nonAD erg_ax)
   double ln_t_end, abstol, reltol, dtmin;
+  // certified-negative resonance scan (scan_certified_negative): margin
+  // factor on ωp² (+inf disables the certificate), the smallest radius it trusts (10 km in
+  // GR: g_schwartz's interior patch) and m_a² with a margin
+  double cert_fac, cert_rmin, cert_e2;
   int64_t maxiters;
   int32_t flat, isotropic, integrator, n_fixed, interp_points, pad;
 };
@@ -106,6 +110,10 @@ inline KParams make_kparams(const art_params& p) {
   k.rmax = p.rNS * pow(k.pole_val / p.mass_a, 2.0 / 3.0);
   k.rmax_def = p.rNS * pow(k.pole_val / 1e-5, 2.0 / 3.0);  // get_Prob_nonAD passes no Mass_a (:97)
   k.GM_c2 = GNEW * p.mass_ns / (C_KM * C_KM);
+  // certified-negative scan: ωp² = wp2n |b| / r³ needs GJ plasma without a boundary layer
+  k.cert_fac = (p.bndry_lyr > 0.0 || !(p.mass_a > 0.0)) ? __builtin_inf() : 1.0 + 1e-6;
+  k.cert_rmin = k.rs_eff == 0.0 ? 0.0 : 10.0;
+  k.cert_e2 = k.mass_a2 * (1.0 + 1e-9);
   k.ln_t_end = p.ln_t_end;
   k.abstol = p.abstol;
   k.reltol = p.reltol;
@@ -407,7 +415,7 @@ __host__ __device__ inline void hamiltonian_full(const KParams& P, const T* x, c
 // division, the same value up to rounding. It is NaN where √nrm is (nrm < 0: |u7| has
 // dropped below m_a, where the reference would raise DomainError).
 template <class T>
-__host__ __device__ inline T condition_t(const KParams& P, const T* u, const T& t0) {
+__host__ __device__ inline void condition_nd(const KParams& P, const T* u, const T& t0, T& N, T& D) {
   // With s = |sinθ|: k∥(w)² = p²/β, p = 2√g^rr w_r a1 + (w_θ a2 + w_φ a3/s)/r, and
   // den = g^rr w_r² + (w_θ² + w_φ²/s²)/r². Scaling both by r s gives PP = p r s and
   // DEN = den r² s², so X = g^rr k∥(w')²/E² = g^rr num PP²/(DEN β E²) with no 1/r, 1/s.
@@ -420,7 +428,11 @@ __host__ __device__ inline T condition_t(const KParams& P, const T* u, const T& 
   msincos(u[1], st, ct);
   const T E2 = u[6] * u[6];
   const T num = -E2 * gtt - P.mass_a2;
-  if (num < 0.0) return T(NAN);
+  if (num < 0.0) {
+    N = T(NAN);
+    D = T(1.0);
+    return;
+  }
   T wpn = 0.0, wpd = r * r * r;
   T A = 1.0, B = 0.0;
   if (r > P.rNS || !P.isotropic) {
@@ -446,7 +458,61 @@ __host__ __device__ inline T condition_t(const KParams& P, const T* u, const T& 
       B = grr * num * PP * PP;
     }
   }
-  return 0.5 * (wpn * (A - B) - P.mass_a2 * wpd * A) / (wpd * A * E2);
+  N = wpn * (A - B) - P.mass_a2 * wpd * A;
+  D = wpd * A * E2;
+}
+
+// The condition's value: cond = ½ N / D (condition_nd). The grid pass of the scan only needs
+// its sign, which is the sign of N whenever D > 0 (propagate_kernel, sign_code_nd).
+template <class T>
+__host__ __device__ inline T condition_t(const KParams& P, const T* u, const T& t0) {
+  T N, D;
+  condition_nd(P, u, t0, N, D);
+  return 0.5 * N / D;
+}
+
+// ---------------------------------------------------------------------------
+// Certified-negative step of the resonance scan (propagate_kernel).
+// The scanned interpolant -- the cubic Hermite of (u0, f0) -> (u1, f1) over h -- lies in the
+// convex hull of its Bernstein control points u0, u0 + h f0/3, u1 - h f1/3, u1. That bounds
+// r and |u7| from below and θ, φ around the end point over the whole step. With
+// b = Bz/B_n = cosθm (3cos²θ - 1) + 3 sinθm sinθ cosθ cosψ one has |∂b/∂θ| <= 3 and
+// |∂b/∂ψ| <= 1.5 |sinθm|, so |b| <= |b(end)| + 3Δθ + 1.5|sinθm|Δψ (and |b| <= 2). If then
+// ωp² <= wp2n |b|max / r_min³ < m_a² and u7² > m_a² (so num > 0: no NaN), the numerator of
+// condition_nd, wpn (A - B) - m_a² r³ A, is < 0 at every point (B >= 0, A > 0): every grid
+// code of the step is "negative" without evaluating it. The margins (1e-6 on ωp², 1e-9 on
+// u7², a hull slack of 1e-12 of the terms) are far above the rounding of the interpolant
+// and of the condition. The only uncovered case is measure-zero: A = 0, which needs sinθ
+// and w_φ both exactly zero at a grid point.
+struct Hull {
+  double lo, hi;
+};
+
+__host__ __device__ inline Hull bernstein_hull(double a, double fa, double b, double fb, double h) {
+  const double h3 = h * (1.0 / 3.0);
+  const double c1 = a + h3 * fa, c2 = b - h3 * fb;
+  const double s = 1e-12 * (fabs(a) + fabs(b) + fabs(h * fa) + fabs(h * fb));
+  if (!(fabs(c1) + fabs(c2) + s < __builtin_inf())) return {NAN, NAN};  // non-finite: no bound
+  return {fmin(fmin(a, b), fmin(c1, c2)) - s, fmax(fmax(a, b), fmax(c1, c2)) + s};
+}
+
+__host__ __device__ inline bool scan_certified_negative(const KParams& P, const double* u0, const double* f0,
+                                                        const double* u1, const double* f1, double h, double tau) {
+  const Hull r = bernstein_hull(u0[0], f0[0], u1[0], f1[0], h);
+  const Hull e = bernstein_hull(u0[6], f0[6], u1[6], f1[6], h);
+  const double elo = e.lo > 0.0 ? e.lo : (e.hi < 0.0 ? -e.hi : 0.0);
+  if (!(r.lo > P.cert_rmin) || !(elo * elo > P.cert_e2) || !(P.cert_fac < 1e300)) return false;
+  const Hull th = bernstein_hull(u0[1], f0[1], u1[1], f1[1], h);
+  const Hull ph = bernstein_hull(u0[2], f0[2], u1[2], f1[2], h);
+  const double t0 = exp(tau), t1 = exp(tau + h);  // t = e^(τ + θh) is monotone over the step
+  double st, ct, sp, cp;
+  msincos(u1[1], st, ct);
+  msincos(u1[2] - P.omega * t1, sp, cp);
+  const double b1 = P.cm * (3.0 * ct * ct - 1.0) + 3.0 * P.sm * st * ct * cp;
+  const double dth = fmax(th.hi - u1[1], u1[1] - th.lo);
+  const double dps = fmax(ph.hi - u1[2], u1[2] - ph.lo) + fabs(P.omega) * (t1 - t0) * (1.0 + 1e-12);
+  const double bmax = fmin(2.0, fabs(b1) + 3.0 * dth + 1.5 * fabs(P.sm) * dps) + 1e-12;
+  return P.wp2n * bmax * P.cert_fac < P.mass_a2 * (r.lo * r.lo * r.lo);
 }
 
 template <class T>

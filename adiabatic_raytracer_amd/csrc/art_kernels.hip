@@ -21,7 +21,8 @@ namespace art {
 
 
 // stats[]: totals over the launch, for the roofline accounting (tools/count_flops.cpp)
-enum { ST_ATTEMPTS = 0, ST_ACCEPTED, ST_ROOT_STEPS, ST_SCAN_EVALS, ST_INTERP_EVALS, ST_RAYS, ST_INIT_RHS, ST_NSTATS = 8 };
+enum { ST_ATTEMPTS = 0, ST_ACCEPTED, ST_ROOT_STEPS, ST_SCAN_EVALS, ST_INTERP_EVALS, ST_RAYS, ST_INIT_RHS, ST_CERT,
+       ST_NSTATS = 8 };
 
 constexpr int CHUNK = 64;
 
@@ -128,8 +129,8 @@ __device__ inline double scan_point(const KParams& P, const double* u0, const do
 // scan_point on an interpolant parked in LDS: S = the lane's base in the [slot][component]
 // [lane] layout, slots 0-3 = u0, f0, u1, f1, slot 4 = (h, τ). The cooperative grid pass and
 // the per-lane bracket evaluations both go through here.
-__device__ inline double scan_point_lds(const KParams& P, const double* S, int stride, double th) {
-  double u0[7], f0[7], u1[7], f1[7];
+__device__ inline void scan_nd_lds(const KParams& P, const double* S, int stride, double th, double& N, double& D) {
+  double u0[7], f0[7], u1[7], f1[7], ui[7];
 #pragma unroll
   for (int i = 0; i < 7; ++i) {
     u0[i] = S[(0 * 7 + i) * stride];
@@ -137,7 +138,15 @@ __device__ inline double scan_point_lds(const KParams& P, const double* S, int s
     u1[i] = S[(2 * 7 + i) * stride];
     f1[i] = S[(3 * 7 + i) * stride];
   }
-  return scan_point(P, u0, f0, u1, f1, S[(4 * 7 + 0) * stride], S[(4 * 7 + 1) * stride], th);
+  const double h = S[(4 * 7 + 0) * stride], tau = S[(4 * 7 + 1) * stride];
+  hermite7(u0, f0, u1, f1, h, th, ui);
+  condition_nd(P, ui, exp(tau + th * h), N, D);
+}
+
+__device__ inline double scan_point_lds(const KParams& P, const double* S, int stride, double th) {
+  double N, D;
+  scan_nd_lds(P, S, stride, th, N, D);
+  return 0.5 * N / D;  // = condition_t, bit for bit
 }
 
 // Completes this wave's LDS traffic before other lanes of the same wave read it.
@@ -149,6 +158,14 @@ __device__ inline void wave_lds_sync() {
 
 // 2-bit sign code of a scan value: 0 zero, 1 positive, 2 negative, 3 NaN
 __device__ inline unsigned sign_code(double c) { return isnan(c) ? 3u : (c > 0.0 ? 1u : (c < 0.0 ? 2u : 0u)); }
+
+// sign_code(½ N / D) without the division where its sign is certain: D > 0 and finite, N a
+// normal number and the quotient far from underflow. Otherwise the division decides.
+__device__ inline unsigned sign_code_nd(double N, double D) {
+  const double aN = fabs(N);
+  if (D > 0.0 && D < INFINITY && aN >= 1e-290 && !(aN < 1e-290 * D)) return N > 0.0 ? 1u : 2u;
+  return sign_code(0.5 * N / D);
+}
 
 // ode_determine_initdt (DiffEqBase) for an order-6 method; one extra RHS evaluation.
 __device__ inline double initdt(const KParams& P, bool photon, double erg, const double* u0, const double* f0,
@@ -323,11 +340,14 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
   __shared__ unsigned codes[SCAN_WORDS * BLOCK];  // [word][lane]: 2-bit sign codes of the grid scan
   __shared__ double lastv[BLOCK];                 // value at the last grid point
   __shared__ int srcl[BLOCK];                     // compact list of the wave's scanning lanes
+  __shared__ double thgrid[SCAN_WORDS * 16 + 1];  // Θs = j/(npts-1): range(0, 1, length = npts)
   double* const L = lds + threadIdx.x;
   const int wbase = threadIdx.x & ~63;
   const int lane = threadIdx.x & 63;
   const double tend = P.ln_t_end;
   const int npts = P.interp_points;
+  for (int j = threadIdx.x; j < npts; j += BLOCK) thgrid[j] = double(j) / double(npts - 1);
+  __syncthreads();
 
   int mode = M_IDLE;
   int ray = -1;
@@ -337,6 +357,7 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
   const double qpow_init = pow(1e-4, 1.0 / 15.0);
   double u[7], f[7], tau = 0.0, dt = 0.0, qpow = qpow_init;
   double cprev = 0.0;
+  bool cprev_ok = true;  // cprev holds the condition at the step start (false after a certified step)
   int sprev = 0;
   bool just_evented = false;
   int n_acc = 0, n_rej = 0, ncross = 0, iter = 0;
@@ -344,7 +365,7 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
   int post_s = 0, r_side = 0, r_it = 0;
   int wnext = 0, wend = 0;
   bool exhausted = false;
-  unsigned s_att = 0, s_acc = 0, s_root = 0, s_scan = 0, s_interp = 0, s_rays = 0;
+  unsigned s_att = 0, s_acc = 0, s_root = 0, s_scan = 0, s_interp = 0, s_rays = 0, s_cert = 0;
 #pragma unroll
   for (int i = 0; i < 7; ++i) { u[i] = 0.0; f[i] = 0.0; }
 
@@ -379,6 +400,7 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
           }
           dt = in.u0[14 * n + ray];
           cprev = in.u0[15 * n + ray];
+          cprev_ok = true;
           sprev = isnan(cprev) ? 0 : sgn(cprev);
           tau = in.lnt0[ray];
           n_acc = n_rej = ncross = iter = 0;
@@ -504,7 +526,12 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
     //     (and the idle lanes of a draining wave) share the 49-point scans instead of waiting.
     //     Each item leaves a 2-bit sign code in the source lane's LDS words.
     const int nper = npts - 1;
-    const double inv_n = 1.0 / double(nper);
+    // (0) certified-negative steps (scan_certified_negative, art_core.h): every grid point of
+    //     the step provably has a negative condition, so its codes are known without
+    //     evaluating them; its end value is not needed unless the next step opens a bracket
+    //     at its start (then it is recomputed there, bit-identically: cprev_ok = false).
+    const bool cert = scan && scan_certified_negative(P, u, f, y, kk, hs, tau);
+    s_cert += cert ? 1u : 0u;
     // every lane parks (u, f, y, kk, h, τ) in its LDS slots (free after the error estimate):
     // the scan reads the interpolants from there, and the registers stay free until the
     // state is reloaded after the scan
@@ -517,10 +544,11 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
     }
     L[(4 * 7 + 0) * BLOCK] = hs;
     L[(4 * 7 + 1) * BLOCK] = tau;
-    const unsigned long long smask = __ballot(scan);
+    const bool grid = scan && !cert;
+    const unsigned long long smask = __ballot(grid);
     if (smask != 0ull) {
       const int ns = __popcll(smask);
-      if (scan) {
+      if (grid) {
         srcl[wbase + __popcll(smask & ((1ull << lane) - 1ull))] = lane;
 #pragma unroll
         for (int w = 0; w < SCAN_WORDS; ++w) codes[w * BLOCK + threadIdx.x] = 0u;
@@ -534,9 +562,17 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
       for (int w0 = 0; w0 < total; w0 += 64) {
         if (w0 + lane < total) {
           const int src = srcl[wbase + c];
-          const double cv = scan_point_lds(P, lds + wbase + src, BLOCK, double(j) * inv_n);
-          atomicOr(&codes[((j - 1) >> 4) * BLOCK + wbase + src], sign_code(cv) << (2 * ((j - 1) & 15)));
-          if (j == nper) lastv[wbase + src] = cv;
+          double N, D;
+          scan_nd_lds(P, lds + wbase + src, BLOCK, thgrid[j], N, D);
+          unsigned code;
+          if (j == nper) {  // the end value opens the next step's brackets
+            const double cv = 0.5 * N / D;
+            lastv[wbase + src] = cv;
+            code = sign_code(cv);
+          } else {
+            code = sign_code_nd(N, D);
+          }
+          atomicOr(&codes[((j - 1) >> 4) * BLOCK + wbase + src], code << (2 * ((j - 1) & 15)));
           s_scan += 1;
         }
         c += dc;
@@ -560,11 +596,11 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
     int ip = 1, last_j = 0;
     int last_s = sprev;
     double last_c = cprev;
-    bool lc_ok = true;  // last_c is the value at grid point last_j (0: previous step's)
+    bool lc_ok = cprev_ok;  // last_c is the value at grid point last_j (0: the step start)
     unsigned cw[SCAN_WORDS] = {0u, 0u, 0u, 0u};
     if (ph == 2) {
 #pragma unroll
-      for (int w = 0; w < SCAN_WORDS; ++w) cw[w] = codes[w * BLOCK + threadIdx.x];
+      for (int w = 0; w < SCAN_WORDS; ++w) cw[w] = cert ? 0xAAAAAAAAu : codes[w * BLOCK + threadIdx.x];
       // fast path: every grid point has the previous sign (or the previous sign is unknown
       // and every point has one common nonzero sign)
       const unsigned s0 = cw[0] & 3u;
@@ -580,7 +616,8 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
         if (same) {
           last_s = (s0 == 1u) ? 1 : -1;
           last_j = nper;
-          last_c = lastv[threadIdx.x];
+          if (!cert) last_c = lastv[threadIdx.x];
+          lc_ok = !cert;
           ph = 0;
         }
       }
@@ -615,7 +652,10 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
         if (found) {
           ph = 5;
         } else if (!lc_ok && last_j == nper) {
-          last_c = lastv[threadIdx.x];
+          if (!cert) {  // a certified step leaves it to the next step's start (th = 0)
+            last_c = lastv[threadIdx.x];
+            lc_ok = true;
+          }
           ph = 0;
         } else if (!lc_ok) {
           ph = 7;
@@ -626,8 +666,8 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
       }
       double th = 0.0;
       if (ph == 3) th = i_tr;
-      else if (ph == 5) th = double(ip) * inv_n;
-      else if (ph == 6 || ph == 7) th = double(last_j) * inv_n;
+      else if (ph == 5) th = thgrid[ip];
+      else if (ph == 6 || ph == 7) th = thgrid[last_j];
       // one condition call site: the fresh state (INIT), the re-stepped end (ROOT) or the
       // interpolant at th -- the latter exactly as scan_point forms it (bit-identical)
       double ci;
@@ -659,6 +699,7 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
         ph = 0;
       } else if (ph == 7) {  // value at the step's last nonzero grid point (next step's bracket start)
         last_c = ci;
+        lc_ok = true;
         ph = 0;
       } else if (ph == 5 || ph == 6) {
         if (ph == 5) i_cg = ci;
@@ -667,9 +708,9 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
           ph = 6;
         } else {  // open the Illinois search on the interpolant inside (θ_last, θ_ip]
           lc_ok = true;
-          i_tha = double(last_j) * inv_n;
+          i_tha = thgrid[last_j];
           i_ca = last_c;
-          i_thb = double(ip) * inv_n;
+          i_thb = thgrid[ip];
           i_cb = i_cg;
           i_tr = i_tha - i_ca * (i_thb - i_tha) / (i_cb - i_ca);
           i_side = 0;
@@ -687,8 +728,8 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
           if (++i_it >= 40) stop = true;
         }
         if (stop) {
-          const double thg = double(ip) * inv_n;
-          const double last_th = double(last_j) * inv_n;
+          const double thg = thgrid[ip];
+          const double last_th = thgrid[last_j];
           const double t_int = i_tr;
           if (!(just_evented && t_int < 0.01)) {  // DiffEq repeat_nudge after an event
             hit = true;
@@ -728,6 +769,7 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
       for (int i = 0; i < 7; ++i) { u[i] = y[i]; f[i] = kk[i]; }
       tau = tau_r;
       cprev = post_c;  // the post-event side (DiffEq repeat_nudge): the root is not re-found
+      cprev_ok = true;
       sprev = post_s;
       just_evented = true;
       mode = M_STEP;
@@ -740,6 +782,7 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
       for (int i = 0; i < 7; ++i) { u[i] = y[i]; f[i] = kk[i]; }
       tau = last ? tend : tau + hs;
       cprev = last_c;
+      cprev_ok = lc_ok;
       sprev = last_s;
       just_evented = false;
       dt = dtnext;
@@ -766,12 +809,13 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
   }
 
   // wave-reduce the statistics and add them once per wave
-  const unsigned v[6] = {s_att, s_acc, s_root, s_scan, s_interp, s_rays};
+  const unsigned v[7] = {s_att, s_acc, s_root, s_scan, s_interp, s_rays, s_cert};
+  const int slot[7] = {ST_ATTEMPTS, ST_ACCEPTED, ST_ROOT_STEPS, ST_SCAN_EVALS, ST_INTERP_EVALS, ST_RAYS, ST_CERT};
 #pragma unroll
-  for (int k = 0; k < 6; ++k) {
+  for (int k = 0; k < 7; ++k) {
     unsigned long long x = v[k];
     for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off);
-    if (lane == 0 && x) atomicAdd(&stats[k], x);
+    if (lane == 0 && x) atomicAdd(&stats[slot[k]], x);
   }
 }
 

@@ -191,7 +191,7 @@ def last_stats() -> dict:
     s = (C.c_uint64 * 8)()
     g = C.c_int32()
     check(lib.art_last_stats(s, C.byref(g)))
-    keys = ("attempts", "accepted", "root_steps", "scan_evals", "interp_evals", "rays", "init_rhs")
+    keys = ("attempts", "accepted", "root_steps", "scan_evals", "interp_evals", "rays", "init_rhs", "cert_steps")
     d = {k: int(s[i]) for i, k in enumerate(keys)}
     d["grid"] = int(g.value)
     return d

@@ -1,0 +1,72 @@
+"""Soundness of the certified-negative resonance scan (art_core.h scan_certified_negative,
+DESIGN.md §3), on the host build of the product header (tools/corecheck): for random steps
+(u0, f(u0)) -> (u1, f(u1)) over h, whenever the certificate holds, the ORACLE's condition
+(RayTracer.jl:254-298) is negative -- not NaN, not zero -- at every grid point the kernel
+would have scanned (interp_points = 50 on the cubic Hermite interpolant, RayTracer.jl:358).
+The certificate must also fire on a good share of the far-field steps, and never where
+|u7| < m_a (NaN codes) or where the step can reach the conversion surface."""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+from conftest import CONFIGS, random_states
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+import corecheck as cc  # noqa: E402
+
+ERG = 1.0000002692622573e-05
+
+
+def hermite(u0, f0, u1, f1, h, th):
+    a, b = 1.0 - th, th * (th - 1.0)
+    return a * u0 + th * u1 + b * ((1.0 - 2.0 * th) * (u1 - u0) + (th - 1.0) * h * f0 + th * h * f1)
+
+
+@pytest.mark.parametrize("cfg", sorted(CONFIGS))
+def test_certificate_is_sound(cfg, oracle_lib):
+    kw = dict(CONFIGS[cfg])
+    p = oracle_lib.make_params(**kw)
+    mr = oracle_lib.find_conversion_surface(p)
+    erg = kw["mass_a"] * 1.0000002692622573
+    rng = np.random.default_rng(7)
+    U, tau = random_states(600, seed=11, rmin=10.5, rmax=12 * mr, erg=erg)
+    th_grid = np.arange(1, 50) / 49.0
+    fired = nan_side = 0
+    for i in range(U.shape[1]):
+        u0, t0 = U[:, i], tau[i]
+        f0 = oracle_lib.rhs(p, 1, u0, t0, erg)
+        h = 10 ** rng.uniform(-4, 0)
+        um = u0 + 0.5 * h * f0
+        u1 = u0 + h * oracle_lib.rhs(p, 1, um, t0 + 0.5 * h, erg)
+        f1 = oracle_lib.rhs(p, 1, u1, t0 + h, erg)
+        if not (np.all(np.isfinite(u1)) and np.all(np.isfinite(f1))):
+            continue
+        ok = cc.certified_negative(p, u0, f0, u1, f1, h, t0)
+        if abs(u0[6]) < kw["mass_a"] or abs(u1[6]) < kw["mass_a"]:
+            nan_side += 1
+            assert not ok  # NaN codes (|u7| < m_a) are never certified
+        if not ok:
+            continue
+        fired += 1
+        c = np.array([oracle_lib.condition(p, hermite(u0, f0, u1, f1, h, th), t0 + th * h) for th in th_grid])
+        assert np.all(c < 0.0), (i, c.max())
+    assert fired >= 100, fired
+    assert nan_side > 0
+
+
+def test_certificate_rejects_the_conversion_surface(oracle_lib):
+    """A step that starts on the conversion surface (a sampled conversion point) is never
+    certified: its condition is ~0 there."""
+    kw = CONFIGS["flat"]
+    p = oracle_lib.make_params(**kw)
+    s = oracle_lib.sample(p, oracle_lib.find_conversion_surface(p), 1769, 0, 64)
+    n = 64
+    for i in range(n):
+        x, k = s["x"].reshape(3, n)[:, i], s["k_init"].reshape(3, n)[:, i]
+        u0 = oracle_lib.initial_state(p, x, k, s["erg"][i], -1.0)
+        f0 = oracle_lib.rhs(p, 1, u0, -30.0, s["erg"][i])
+        u1 = u0 + 1e-3 * f0
+        f1 = oracle_lib.rhs(p, 1, u1, -30.0 + 1e-3, s["erg"][i])
+        assert not cc.certified_negative(p, u0, f0, u1, f1, 1e-3, -30.0)

@@ -102,3 +102,7 @@ def metric_d(r, rs):
     o = np.zeros(4)
     lib().cc_metric_d(C.c_double(r), C.c_double(rs), P(o))
     return o
+
+
+def certified_negative(p, u0, f0, u1, f1, h, tau):
+    return bool(lib().cc_certified_negative(C.byref(p), P(u0), P(f0), P(u1), P(f1), C.c_double(h), C.c_double(tau)))
