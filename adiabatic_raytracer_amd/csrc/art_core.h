@@ -472,7 +472,7 @@ __host__ __device__ inline T condition_t(const KParams& P, const T* u, const T& 
 }
 
 // ---------------------------------------------------------------------------
-// Certified-negative step of the resonance scan (propagate_kernel).
+// Certified steps of the resonance scan (propagate_kernel).
 // The scanned interpolant -- the cubic Hermite of (u0, f0) -> (u1, f1) over h -- lies in the
 // convex hull of its Bernstein control points u0, u0 + h f0/3, u1 - h f1/3, u1. That bounds
 // r and |u7| from below and θ, φ around the end point over the whole step. With
@@ -483,7 +483,9 @@ __host__ __device__ inline T condition_t(const KParams& P, const T* u, const T& 
 // code of the step is "negative" without evaluating it. The margins (1e-6 on ωp², 1e-9 on
 // u7², a hull slack of 1e-12 of the terms) are far above the rounding of the interpolant
 // and of the condition. The only uncovered case is measure-zero: A = 0, which needs sinθ
-// and w_φ both exactly zero at a grid point.
+// and w_φ both exactly zero at a grid point. Likewise, where u7² (-g^tt) < m_a² over the
+// whole hull (the photon has lost energy below the axion shell), every grid point's NrmSq
+// is negative and every code is "NaN".
 struct Hull {
   double lo, hi;
 };
@@ -496,12 +498,21 @@ __host__ __device__ inline Hull bernstein_hull(double a, double fa, double b, do
   return {fmin(fmin(a, b), fmin(c1, c2)) - s, fmax(fmax(a, b), fmax(c1, c2)) + s};
 }
 
-__host__ __device__ inline bool scan_certified_negative(const KParams& P, const double* u0, const double* f0,
-                                                        const double* u1, const double* f1, double h, double tau) {
+// Returns the certified sign code of every grid point of the step: 2 (negative, above), 3
+// (NaN: u7² (-g^tt) < m_a² all along the step, where the reference's √NrmSq is undefined and
+// condition_nd returns NaN), or 0 when nothing is certain.
+__host__ __device__ inline int scan_certified_code(const KParams& P, const double* u0, const double* f0,
+                                                   const double* u1, const double* f1, double h, double tau) {
+  if (!(P.cert_fac < 1e300)) return 0;
   const Hull r = bernstein_hull(u0[0], f0[0], u1[0], f1[0], h);
+  if (!(r.lo > P.cert_rmin)) return 0;
   const Hull e = bernstein_hull(u0[6], f0[6], u1[6], f1[6], h);
   const double elo = e.lo > 0.0 ? e.lo : (e.hi < 0.0 ? -e.hi : 0.0);
-  if (!(r.lo > P.cert_rmin) || !(elo * elo > P.cert_e2) || !(P.cert_fac < 1e300)) return false;
+  const double ehi = fmax(fabs(e.lo), fabs(e.hi));
+  // -g^tt <= 1 / (1 - rs / r_min) for r > 10 km (flat: exactly 1)
+  const double gmax = P.rs_eff == 0.0 ? 1.0 : 1.0 / (1.0 - P.rs_eff / r.lo);
+  if (ehi * ehi * gmax * (1.0 + 1e-9) < P.mass_a2) return 3;
+  if (!(elo * elo > P.cert_e2)) return 0;
   const Hull th = bernstein_hull(u0[1], f0[1], u1[1], f1[1], h);
   const Hull ph = bernstein_hull(u0[2], f0[2], u1[2], f1[2], h);
   const double t0 = exp(tau), t1 = exp(tau + h);  // t = e^(τ + θh) is monotone over the step
@@ -512,7 +523,7 @@ __host__ __device__ inline bool scan_certified_negative(const KParams& P, const 
   const double dth = fmax(th.hi - u1[1], u1[1] - th.lo);
   const double dps = fmax(ph.hi - u1[2], u1[2] - ph.lo) + fabs(P.omega) * (t1 - t0) * (1.0 + 1e-12);
   const double bmax = fmin(2.0, fabs(b1) + 3.0 * dth + 1.5 * fabs(P.sm) * dps) + 1e-12;
-  return P.wp2n * bmax * P.cert_fac < P.mass_a2 * (r.lo * r.lo * r.lo);
+  return P.wp2n * bmax * P.cert_fac < P.mass_a2 * (r.lo * r.lo * r.lo) ? 2 : 0;
 }
 
 template <class T>

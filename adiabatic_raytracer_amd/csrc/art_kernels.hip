@@ -526,11 +526,13 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
     //     (and the idle lanes of a draining wave) share the 49-point scans instead of waiting.
     //     Each item leaves a 2-bit sign code in the source lane's LDS words.
     const int nper = npts - 1;
-    // (0) certified-negative steps (scan_certified_negative, art_core.h): every grid point of
-    //     the step provably has a negative condition, so its codes are known without
-    //     evaluating them; its end value is not needed unless the next step opens a bracket
-    //     at its start (then it is recomputed there, bit-identically: cprev_ok = false).
-    const bool cert = scan && scan_certified_negative(P, u, f, y, kk, hs, tau);
+    // (0) certified steps (scan_certified_code, art_core.h): every grid point of the step
+    //     provably has a negative (2) or an undefined (3, NaN) condition, so its codes are
+    //     known without evaluating them; its end value is not needed unless the next step
+    //     opens a bracket at its start (then it is recomputed there, bit-identically:
+    //     cprev_ok = false).
+    const int ccode = scan ? scan_certified_code(P, u, f, y, kk, hs, tau) : 0;
+    const bool cert = ccode != 0;
     s_cert += cert ? 1u : 0u;
     // every lane parks (u, f, y, kk, h, τ) in its LDS slots (free after the error estimate):
     // the scan reads the interpolants from there, and the registers stay free until the
@@ -600,7 +602,8 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
     unsigned cw[SCAN_WORDS] = {0u, 0u, 0u, 0u};
     if (ph == 2) {
 #pragma unroll
-      for (int w = 0; w < SCAN_WORDS; ++w) cw[w] = cert ? 0xAAAAAAAAu : codes[w * BLOCK + threadIdx.x];
+      for (int w = 0; w < SCAN_WORDS; ++w)
+        cw[w] = cert ? (ccode == 3 ? 0xFFFFFFFFu : 0xAAAAAAAAu) : codes[w * BLOCK + threadIdx.x];
       // fast path: every grid point has the previous sign (or the previous sign is unknown
       // and every point has one common nonzero sign)
       const unsigned s0 = cw[0] & 3u;
@@ -618,6 +621,20 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
           last_j = nper;
           if (!cert) last_c = lastv[threadIdx.x];
           lc_ok = !cert;
+          ph = 0;
+        }
+      } else if (s0 == 3u) {  // every point NaN: no resonance possible, the sign memory resets
+        bool all = true;
+#pragma unroll
+        for (int w = 0; w < SCAN_WORDS; ++w) {
+          const int nw = nper - 16 * w;
+          if (nw <= 0) break;
+          const unsigned m = nw >= 16 ? 0xffffffffu : ((1u << (2 * nw)) - 1u);
+          all = all && ((cw[w] & m) == m);
+        }
+        if (all) {  // with no sign remembered, the bracket-start value is never read
+          last_s = 0;
+          lc_ok = false;
           ph = 0;
         }
       }
@@ -657,9 +674,9 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
             lc_ok = true;
           }
           ph = 0;
-        } else if (!lc_ok) {
+        } else if (!lc_ok && last_s != 0) {
           ph = 7;
-        } else {
+        } else {  // (with no sign remembered the bracket-start value is never read)
           ph = 0;
         }
         if (ph == 0) break;

@@ -55,10 +55,10 @@ void cc_metric_d(double r, double rs, double* out) {
 }
 
 extern "C" {
-// scan_certified_negative (art_core.h) for one step (u0, f0) -> (u1, f1) over h from τ
-int cc_certified_negative(const art_params* p, const double* u0, const double* f0, const double* u1,
+// scan_certified_code (art_core.h) for one step (u0, f0) -> (u1, f1) over h from τ
+int cc_certified_code(const art_params* p, const double* u0, const double* f0, const double* u1,
                           const double* f1, double h, double tau) {
   KParams K = make_kparams(*p);
-  return scan_certified_negative(K, u0, f0, u1, f1, h, tau) ? 1 : 0;
+  return scan_certified_code(K, u0, f0, u1, f1, h, tau);
 }
 }
