@@ -232,15 +232,22 @@ __host__ __device__ inline void rhs_photon(const KParams& P, const T* u, const T
   T st, ct, sp, cp;
   msincos(u[1], st, ct);
   msincos(u[2] - P.omega * t, sp, cp);  // ψ = φ - ω (time0 + t), time0 = 0 (MainRunner.jl:177)
-  // one division for 1/r and 1/|sinθ|
   const T ast = mabs(st);
-  const T inv_rs = 1.0 / (rc * ast);
-  const T ir = inv_rs * ast;
-  const T ir2 = ir * ir;
-  const T iast = inv_rs * rc;
   const T sgn_st = msign(st);
   const T kr = u[3] * erg, kt = u[4] * erg, kp = u[5] * erg;
   const DipoleAng<T> d = dipole_ang(P, st, ct, sp, cp);
+  // ONE division for 1/r, 1/|sinθ|, 1/E, 1/β and 1/erg: R = 1/(r |sinθ| E β erg)
+  const T beta = 4.0 * d.a1 * d.a1 + d.a2 * d.a2 + d.a3 * d.a3;  // |B|²/B_n² = 1 + 3 a1² >= 1
+  const T X1 = rc * ast, X2 = E * beta;
+  const T R = 1.0 / (X1 * X2 * erg);
+  const T Re = R * erg;
+  const T inv_rs = Re * X2;      // 1/(r |sinθ|)
+  const T iE = Re * X1 * beta;   // 1/E
+  const T ibeta = Re * X1 * E;   // 1/β
+  const T ierg = R * (X1 * X2);  // 1/erg
+  const T ir = inv_rs * ast;
+  const T ir2 = ir * ir;
+  const T iast = inv_rs * rc;
   const T sgb = msign(d.b);
   const T cB = P.wp2n * ir2 * ir;               // ∂ωp² = cB sgn(b) ∂b, ωp² ∝ r^-3
   const T wp2 = cB * mabs(d.b);
@@ -251,7 +258,6 @@ __host__ __device__ inline void rhs_photon(const KParams& P, const T* u, const T
   metric_tr_d(rc, P.rs_eff, gtt, grr, dgtt, dgrr);
   const T gpp = ir2 * iast * iast;
   const T E2 = E * E;
-  const T iE = 1.0 / E;
   const T iE2 = iE * iE;
   const bool flat = P.rs_eff == 0.0;  // wave-uniform: g^rr = 1, ∂g^rr = 0
   const T sq = flat ? T(1.0) : msqrt(grr);
@@ -260,7 +266,6 @@ __host__ __device__ inline void rhs_photon(const KParams& P, const T* u, const T
   if (!P.isotropic) {
     const T pa = kt * d.a2 + kp * d.a3 * iast;
     const T p = 2.0 * sq * kr * d.a1 + ir * pa;
-    const T ibeta = 1.0 / (4.0 * d.a1 * d.a1 + d.a2 * d.a2 + d.a3 * d.a3);
     const T G = grr * p * ibeta * iE2;  // Q = G p
     Q = G * p;
     const T p_r = flat ? -ir2 * pa : dgrr / sq * kr * d.a1 - ir2 * pa;
@@ -278,22 +283,20 @@ __host__ __device__ inline void rhs_photon(const KParams& P, const T* u, const T
   }
   const T omQ = 1.0 - Q;
   const T fac = C_KM * t * grr_u * iE;
-  if (r <= P.rNS101) {
-    du[0] = 0.0; du[1] = 0.0; du[2] = 0.0; du[3] = 0.0; du[4] = 0.0; du[5] = 0.0;
-  } else {
-    const T ir3 = ir2 * ir;
-    const T H_r = 0.5 * (dgtt * E2 + dgrr * kr * kr - 2.0 * ir3 * (kt * kt + iast * iast * kp * kp) +
-                         dwp2_r * omQ - wp2 * Q_r);
-    const T H_t = 0.5 * (-2.0 * ct * ir2 * iast * iast * (sgn_st * iast) * kp * kp + dwp2_t * omQ - wp2 * Q_t);
-    const T H_p = 0.5 * (dwp2_p * omQ - wp2 * Q_p);
-    const T fx = -fac * (1.0 / erg);  // 1/erg: loop-invariant per ray
-    du[0] = (grr * kr - 0.5 * wp2 * Q_kr) * fac;
-    du[1] = (ir2 * kt - 0.5 * wp2 * Q_kt) * fac;
-    du[2] = (gpp * kp - 0.5 * wp2 * Q_kp) * fac;
-    du[3] = H_r * fx;
-    du[4] = H_t * fx;
-    du[5] = H_p * fx;
-  }
+  const T ir3 = ir2 * ir;
+  const T H_r = 0.5 * (dgtt * E2 + dgrr * kr * kr - 2.0 * ir3 * (kt * kt + iast * iast * kp * kp) +
+                       dwp2_r * omQ - wp2 * Q_r);
+  const T H_t = 0.5 * (-2.0 * ct * ir2 * iast * iast * (sgn_st * iast) * kp * kp + dwp2_t * omQ - wp2 * Q_t);
+  const T H_p = 0.5 * (dwp2_p * omQ - wp2 * Q_p);
+  // rows 1..6 vanish for r <= 1.01 rNS (:86): one select on their common factor
+  const T facx = (r <= P.rNS101) ? T(0.0) : fac;
+  const T fx = -facx * ierg;
+  du[0] = (grr * kr - 0.5 * wp2 * Q_kr) * facx;
+  du[1] = (ir2 * kt - 0.5 * wp2 * Q_kt) * facx;
+  du[2] = (gpp * kp - 0.5 * wp2 * Q_kp) * facx;
+  du[3] = H_r * fx;
+  du[4] = H_t * fx;
+  du[5] = H_p * fx;
   // ∂H/∂t = -ω ∂H/∂ψ (K is static); with a boundary layer ωp² -> (sqrt(ωp²) + L)²
   T dwp2_T = -P.omega * dwp2_p;
   T wp2_T = wp2;

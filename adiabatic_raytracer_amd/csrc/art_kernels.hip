@@ -492,13 +492,16 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
         finish = ART_STATUS_NONFINITE;
       } else {
         // PI controller (OrdinaryDiffEq: beta1 = 7/60, beta2 = 1/15, gamma = 0.9, qmin = 0.2, qmax = 10)
-        double q = 1.0, q11 = 1.0;
+        // (EEst^(7/60) and max(EEst, 1e-4)^(1/15) from one logarithm; OrdinaryDiffEq itself
+        // uses FastPower.fastpower, an exp2/log2 approximation)
+        double q = 1.0, q11 = 1.0, lE = -INFINITY;
         bool accept = true;
         if (!RK4) {
           if (EEst == 0.0) {
             q = 0.1;
           } else {
-            q11 = pow(EEst, 7.0 / 60.0);
+            lE = log(EEst);
+            q11 = exp((7.0 / 60.0) * lE);
             q = q11 / qpow;
             q = fmax(0.1, fmin(5.0, q / 0.9));
           }
@@ -512,7 +515,7 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
           ++n_acc;
           s_acc += 1;
           if (!RK4) {
-            qpow = pow(fmax(EEst, 1e-4), 1.0 / 15.0);
+            qpow = exp(fmax(lE, -9.210340371976182) * (1.0 / 15.0));  // log(1e-4)
             dtnext = hs / q;
           }
           scan = true;

@@ -46,7 +46,8 @@ def flops_per_launch(stats, fl, integrator="vern6"):
     step = fl["rk4_attempt"] if integrator == "rk4" else fl["vern6_attempt"]
     return (att * step + root * (step + fl["condition"])
             + scan * (fl["hermite_point"] + fl["condition_scan_point"])
-            + interp * (fl["hermite_point"] + fl["condition"]))
+            + interp * (fl["hermite_point"] + fl["condition"])
+            + stats["accepted"] * fl["scan_certificate"])  # tried on every accepted step
 
 
 # Algorithmic HBM bytes of one launch of the integrator kernel. Per segment:

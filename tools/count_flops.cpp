@@ -92,14 +92,18 @@ static void emit(bool flat, bool last) {
   const long long f_back = count([&] { back_transform(K, u, 1.00000027e-5, xe, ke); });
   OC pos[3] = {OC(15.0), OC(3.0), OC(4.0)}, kp[3] = {OC(1e-6), OC(2e-6), OC(-1e-6)};
   const long long f_prob = count([&] { (void)prob_nonad_single(K, pos, kp, OC(1.00000027e-5)); });
+  // scan_certified_code (double only, hand count): 4 Bernstein hulls x 11, the u7 bounds 4,
+  // t0 and t1 3, two sincos 4 + ψ 2, b(end) 8, Δθ 2, Δψ 6, |b|max 5, the final test 5
+  const long long f_cert = 4 * 11 + 4 + 3 + 6 + 8 + 2 + 6 + 5 + 5;
   std::printf(
       "  \"%s\": {\n    \"rhs_photon\": %lld,\n    \"rhs_axion\": %lld,\n    \"condition\": %lld,\n"
       "    \"condition_scan_point\": %lld,\n    \"hermite_point\": %lld,\n"
       "    \"vern6_stage_glue\": %lld,\n    \"vern6_error_norm\": %lld,\n    \"controller\": %lld,\n"
       "    \"rk4_stage_glue\": %lld,\n    \"initial_state\": %lld,\n    \"back_transform\": %lld,\n"
-      "    \"prob_nonad\": %lld,\n    \"vern6_attempt\": %lld,\n    \"rk4_attempt\": %lld\n  }%s\n",
+      "    \"prob_nonad\": %lld,\n    \"scan_certificate\": %lld,\n    \"vern6_attempt\": %lld,\n"
+      "    \"rk4_attempt\": %lld\n  }%s\n",
       flat ? "flat" : "gr", f_rhs, f_rhs_ax, f_cond, f_cond_scan, f_herm, f_glue_v6, f_err, f_ctrl, f_glue_rk4,
-      f_init, f_back, f_prob, 8 * f_rhs + f_glue_v6 + f_err + f_ctrl, 4 * f_rhs + f_glue_rk4, last ? "" : ",");
+      f_init, f_back, f_prob, f_cert, 8 * f_rhs + f_glue_v6 + f_err + f_ctrl, 4 * f_rhs + f_glue_rk4, last ? "" : ",");
 }
 
 int main() {
