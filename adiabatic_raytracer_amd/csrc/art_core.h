@@ -235,16 +235,15 @@ __host__ __device__ inline void rhs_photon(const KParams& P, const T* u, const T
   const T ast = mabs(st);
   const T sgn_st = msign(st);
   const T kr = u[3] * erg, kt = u[4] * erg, kp = u[5] * erg;
+  // one division for 1/r, 1/|sinθ|, 1/E and 1/erg (it needs only r, θ and u7, so it does not
+  // wait for ψ: a lone long ray is latency-bound), and one for 1/β
+  const T X1 = rc * ast, X2 = E * erg;
+  const T R = 1.0 / (X1 * X2);
+  const T inv_rs = R * X2;       // 1/(r |sinθ|)
+  const T iE = R * X1 * erg;     // 1/E
+  const T ierg = R * X1 * E;     // 1/erg
   const DipoleAng<T> d = dipole_ang(P, st, ct, sp, cp);
-  // ONE division for 1/r, 1/|sinθ|, 1/E, 1/β and 1/erg: R = 1/(r |sinθ| E β erg)
-  const T beta = 4.0 * d.a1 * d.a1 + d.a2 * d.a2 + d.a3 * d.a3;  // |B|²/B_n² = 1 + 3 a1² >= 1
-  const T X1 = rc * ast, X2 = E * beta;
-  const T R = 1.0 / (X1 * X2 * erg);
-  const T Re = R * erg;
-  const T inv_rs = Re * X2;      // 1/(r |sinθ|)
-  const T iE = Re * X1 * beta;   // 1/E
-  const T ibeta = Re * X1 * E;   // 1/β
-  const T ierg = R * (X1 * X2);  // 1/erg
+  const T ibeta = 1.0 / (4.0 * d.a1 * d.a1 + d.a2 * d.a2 + d.a3 * d.a3);  // |B|²/B_n² = 1 + 3 a1² >= 1
   const T ir = inv_rs * ast;
   const T ir2 = ir * ir;
   const T iast = inv_rs * rc;
