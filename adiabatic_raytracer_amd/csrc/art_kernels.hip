@@ -328,11 +328,31 @@ constexpr int SCAN_WORDS = 4;  // 2-bit codes for up to 64 grid points (interp_p
 // (init_kernel) and steps in the same iteration; lanes polishing a crossing (M_ROOT)
 // re-step from the step start. After the slots, the wave-cooperative scan and one per-lane
 // condition call site (brackets, Illinois, root polish) serve the ContinuousCallback.
-template <int INTEG>
-__global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(const KParams P, const int64_t n, const SegIn in,
-                                                           const SegOut out, const int32_t max_crossings,
-                                                           unsigned long long* __restrict__ queue,
-                                                           unsigned long long* __restrict__ stats) {
+// GEOM_FLAT: flat space, no boundary layer, anisotropic plasma (the headline workload). The
+// kernel then works on a copy of the parameters whose rs_eff, bndry_lyr and isotropic are
+// compile-time constants, so the Schwarzschild, boundary-layer and isotropic branches of
+// the physics fold away instead of holding registers. GEOM_ANY reads them at run time.
+enum { GEOM_ANY = 0, GEOM_FLAT = 1 };
+
+template <int GEOM>
+__device__ inline KParams specialize(const KParams& P) {
+  KParams Q = P;
+  if (GEOM == GEOM_FLAT) {
+    Q.rs_eff = 0.0;
+    Q.bndry_lyr = -1.0;
+    Q.isotropic = 0;
+    Q.cert_rmin = 0.0;
+  }
+  return Q;
+}
+
+template <int INTEG, int GEOM>
+__global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(const KParams P_in, const int64_t n,
+                                                                              const SegIn in, const SegOut out,
+                                                                              const int32_t max_crossings,
+                                                                              unsigned long long* __restrict__ queue,
+                                                                              unsigned long long* __restrict__ stats) {
+  const KParams P = specialize<GEOM>(P_in);
   constexpr bool RK4 = (INTEG == ART_RK4);
   constexpr int NSLOT = RK4 ? 4 : 8;
   const StageTable& T = RK4 ? c_rk4 : c_vern6;
@@ -1198,17 +1218,16 @@ hipError_t launch_propagate(const KParams& P, int64_t n, const SegIn& in, const 
   hipLaunchKernelGGL(init_kernel, dim3(g1), dim3(256), 0, s, P, n, in, stats);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  const void* fn = (P.integrator == ART_RK4) ? (const void*)propagate_kernel<ART_RK4>
-                                             : (const void*)propagate_kernel<ART_VERN6>;
-  const int grid = persistent_blocks(fn, n);
+  const bool flat = P.rs_eff == 0.0 && !(P.bndry_lyr > 0.0) && !P.isotropic;
+  const bool rk4 = P.integrator == ART_RK4;
+  using KFn = void (*)(const KParams, const int64_t, const SegIn, const SegOut, const int32_t, unsigned long long*,
+                       unsigned long long*);
+  const KFn fn = rk4 ? (flat ? propagate_kernel<ART_RK4, GEOM_FLAT> : propagate_kernel<ART_RK4, GEOM_ANY>)
+                     : (flat ? propagate_kernel<ART_VERN6, GEOM_FLAT> : propagate_kernel<ART_VERN6, GEOM_ANY>);
+  const int grid = persistent_blocks((const void*)fn, n);
   if (grid_out) *grid_out = grid;
   if (ev0 && (e = hipEventRecord(ev0, s)) != hipSuccess) return e;
-  if (P.integrator == ART_RK4)
-    hipLaunchKernelGGL(propagate_kernel<ART_RK4>, dim3(grid), dim3(BLOCK), 0, s, P, n, in, out, max_crossings, queue,
-                       stats);
-  else
-    hipLaunchKernelGGL(propagate_kernel<ART_VERN6>, dim3(grid), dim3(BLOCK), 0, s, P, n, in, out, max_crossings, queue,
-                       stats);
+  hipLaunchKernelGGL(fn, dim3(grid), dim3(BLOCK), 0, s, P, n, in, out, max_crossings, queue, stats);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   if (ev1 && (e = hipEventRecord(ev1, s)) != hipSuccess) return e;
   hipLaunchKernelGGL(finalize_kernel, dim3(g1), dim3(256), 0, s, P, n, in, out);
@@ -1268,9 +1287,13 @@ hipError_t launch_eval_condition(const KParams& P, int64_t n, const double* u, c
   return hipGetLastError();
 }
 
-template __global__ void propagate_kernel<ART_VERN6>(const KParams, const int64_t, const SegIn, const SegOut,
-                                                     const int32_t, unsigned long long*, unsigned long long*);
-template __global__ void propagate_kernel<ART_RK4>(const KParams, const int64_t, const SegIn, const SegOut,
-                                                   const int32_t, unsigned long long*, unsigned long long*);
+template __global__ void propagate_kernel<ART_VERN6, GEOM_ANY>(const KParams, const int64_t, const SegIn, const SegOut,
+                                                               const int32_t, unsigned long long*, unsigned long long*);
+template __global__ void propagate_kernel<ART_VERN6, GEOM_FLAT>(const KParams, const int64_t, const SegIn, const SegOut,
+                                                                const int32_t, unsigned long long*, unsigned long long*);
+template __global__ void propagate_kernel<ART_RK4, GEOM_ANY>(const KParams, const int64_t, const SegIn, const SegOut,
+                                                             const int32_t, unsigned long long*, unsigned long long*);
+template __global__ void propagate_kernel<ART_RK4, GEOM_FLAT>(const KParams, const int64_t, const SegIn, const SegOut,
+                                                              const int32_t, unsigned long long*, unsigned long long*);
 
 }  // namespace art
