@@ -386,6 +386,9 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
   int wnext = 0, wend = 0;
   bool exhausted = false;
   unsigned s_att = 0, s_acc = 0, s_root = 0, s_scan = 0, s_interp = 0, s_rays = 0, s_cert = 0;
+#ifdef ART_COUNT_LOOPS
+  unsigned s_lane_it = 0, s_main_it = 0;  // dev counters: wave iterations of the per-lane and main loops
+#endif
 #pragma unroll
   for (int i = 0; i < 7; ++i) { u[i] = 0.0; f[i] = 0.0; }
 
@@ -433,6 +436,9 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
       }
     }
     if (__ballot(mode != M_IDLE) == 0ull) break;  // every lane idle and the queue drained
+#ifdef ART_COUNT_LOOPS
+    if (lane == 0) s_main_it += 1;
+#endif
 
     // ---- this iteration's step size ----
     bool last = false, forced = false;
@@ -667,6 +673,9 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
     bool hit = false, root_done = false;
 #pragma unroll 1
     while (ph != 0) {
+#ifdef ART_COUNT_LOOPS
+      if (lane == __ffsll((long long)__ballot(1)) - 1) s_lane_it += 1;
+#endif
       if (ph == 2) {  // walk the codes from grid point ip
         bool found = false;
 #pragma unroll 1
@@ -849,7 +858,11 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
   }
 
   // wave-reduce the statistics and add them once per wave
+#ifdef ART_COUNT_LOOPS
+  const unsigned v[7] = {s_att, s_acc, s_root, s_scan, s_main_it, s_rays, s_lane_it};
+#else
   const unsigned v[7] = {s_att, s_acc, s_root, s_scan, s_interp, s_rays, s_cert};
+#endif
   const int slot[7] = {ST_ATTEMPTS, ST_ACCEPTED, ST_ROOT_STEPS, ST_SCAN_EVALS, ST_INTERP_EVALS, ST_RAYS, ST_CERT};
 #pragma unroll
   for (int k = 0; k < 7; ++k) {
