@@ -47,7 +47,7 @@ def main():
     c16_read = truth["copy16_read_bytes"] / (c16["FETCH_SIZE"][0] * kb)
 
     k = read_counters(os.path.join(pmc_dir, "kernel"))
-    name, pc = pick(k, "art::propagate_kernel<0>")
+    name, pc = pick(k, "art::propagate_kernel<0,")
     fetch = pc["FETCH_SIZE"][-1] * kb
     write = pc["WRITE_SIZE"][-1] * kb
     import hashlib
