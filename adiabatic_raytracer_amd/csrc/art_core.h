@@ -500,9 +500,10 @@ __host__ __device__ inline Hull bernstein_hull(double a, double fa, double b, do
   return {fmin(fmin(a, b), fmin(c1, c2)) - s, fmax(fmax(a, b), fmax(c1, c2)) + s};
 }
 
-// Returns the certified sign code of every grid point of the step: 2 (negative, above), 3
-// (NaN: u7² (-g^tt) < m_a² all along the step, where the reference's √NrmSq is undefined and
-// condition_nd returns NaN), or 0 when nothing is certain.
+// Returns the certified sign code of every grid point of the step: 2 (negative, above), 1
+// (positive: ωp² g^rr > u7² all along the step, below), 3 (NaN: u7² (-g^tt) < m_a² all along
+// the step, where the reference's √NrmSq is undefined and condition_nd returns NaN), or 0
+// when nothing is certain.
 __host__ __device__ inline int scan_certified_code(const KParams& P, const double* u0, const double* f0,
                                                    const double* u1, const double* f1, double h, double tau) {
   if (!(P.cert_fac < 1e300)) return 0;
@@ -524,8 +525,18 @@ __host__ __device__ inline int scan_certified_code(const KParams& P, const doubl
   const double b1 = P.cm * (3.0 * ct * ct - 1.0) + 3.0 * P.sm * st * ct * cp;
   const double dth = fmax(th.hi - u1[1], u1[1] - th.lo);
   const double dps = fmax(ph.hi - u1[2], u1[2] - ph.lo) + fabs(P.omega) * (t1 - t0) * (1.0 + 1e-12);
-  const double bmax = fmin(2.0, fabs(b1) + 3.0 * dth + 1.5 * fabs(P.sm) * dps) + 1e-12;
-  return P.wp2n * bmax * P.cert_fac < P.mass_a2 * (r.lo * r.lo * r.lo) ? 2 : 0;
+  const double db = 3.0 * dth + 1.5 * fabs(P.sm) * dps + 1e-12;
+  const double bmax = fmin(2.0, fabs(b1) + db);
+  if (P.wp2n * bmax * P.cert_fac < P.mass_a2 * (r.lo * r.lo * r.lo)) return 2;
+  // positive: with ωp² g^rr > u7² everywhere. Cauchy-Schwarz gives B/A = g^rr num PP²/(DEN β E²)
+  // <= g^rr num / E² = 1 - g^rr m_a² / E² (g^rr (-g^tt) = 1 outside 10 km), so
+  // N / (r³ A) >= ωp² g^rr m_a² / E² - m_a² > 0. It needs r > rNS everywhere (zeroIn).
+  const double bmin = fabs(b1) - db;
+  const double grr_lo = P.rs_eff == 0.0 ? 1.0 : 1.0 - P.rs_eff / r.lo;
+  if (r.lo > P.rNS && bmin > 0.0 &&
+      P.wp2n * bmin * grr_lo > ehi * ehi * P.cert_fac * (r.hi * r.hi * r.hi))
+    return 1;
+  return 0;
 }
 
 template <class T>

@@ -556,7 +556,7 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
     //     Each item leaves a 2-bit sign code in the source lane's LDS words.
     const int nper = npts - 1;
     // (0) certified steps (scan_certified_code, art_core.h): every grid point of the step
-    //     provably has a negative (2) or an undefined (3, NaN) condition, so its codes are
+    //     provably has a positive (1), negative (2) or undefined (3, NaN) condition, so its codes are
     //     known without evaluating them; its end value is not needed unless the next step
     //     opens a bracket at its start (then it is recomputed there, bit-identically:
     //     cprev_ok = false).
@@ -632,7 +632,7 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
     if (ph == 2) {
 #pragma unroll
       for (int w = 0; w < SCAN_WORDS; ++w)
-        cw[w] = cert ? (ccode == 3 ? 0xFFFFFFFFu : 0xAAAAAAAAu) : codes[w * BLOCK + threadIdx.x];
+        cw[w] = cert ? 0x55555555u * (unsigned)ccode : codes[w * BLOCK + threadIdx.x];
       // fast path: every grid point has the previous sign (or the previous sign is unknown
       // and every point has one common nonzero sign)
       const unsigned s0 = cw[0] & 3u;

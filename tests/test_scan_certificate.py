@@ -3,7 +3,8 @@ on the host build of the product header (tools/corecheck): for random steps
 (u0, f(u0)) -> (u1, f(u1)) over h, whenever the certificate returns "negative" the ORACLE's
 condition (RayTracer.jl:254-298) is negative -- not NaN, not zero -- at every grid point the
 kernel would have scanned (interp_points = 50 on the cubic Hermite interpolant,
-RayTracer.jl:358), and whenever it returns "NaN" the condition is NaN at every grid point.
+RayTracer.jl:358), whenever it returns "positive" it is positive at every point, and
+whenever it returns "NaN" the condition is NaN at every grid point.
 Both must fire on a good share of the steps, and "negative" never where |u7| < m_a or where
 the step can reach the conversion surface."""
 import os
@@ -32,9 +33,11 @@ def test_certificate_is_sound(cfg, oracle_lib):
     mr = oracle_lib.find_conversion_surface(p)
     erg = kw["mass_a"] * 1.0000002692622573
     rng = np.random.default_rng(7)
-    U, tau = random_states(600, seed=11, rmin=10.5, rmax=12 * mr, erg=erg)
+    U1, tau1 = random_states(400, seed=11, rmin=10.5, rmax=12 * mr, erg=erg)
+    U2, tau2 = random_states(400, seed=12, rmin=10.5, rmax=mr, erg=erg)  # inside the surface
+    U, tau = np.concatenate([U1, U2], axis=1), np.concatenate([tau1, tau2])
     th_grid = np.arange(1, 50) / 49.0
-    fired = fired_nan = nan_side = 0
+    fired = fired_nan = fired_pos = nan_side = 0
     for i in range(U.shape[1]):
         u0, t0 = U[:, i], tau[i]
         f0 = oracle_lib.rhs(p, 1, u0, t0, erg)
@@ -47,26 +50,31 @@ def test_certificate_is_sound(cfg, oracle_lib):
         code = cc.certified_code(p, u0, f0, u1, f1, h, t0)
         if abs(u0[6]) < kw["mass_a"] or abs(u1[6]) < kw["mass_a"]:
             nan_side += 1
-            assert code != 2  # a step that reaches |u7| < m_a is never certified negative
+            assert code not in (1, 2)  # a step that reaches |u7| < m_a is never certified signed
         if code == 0:
             continue
         c = np.array([oracle_lib.condition(p, hermite(u0, f0, u1, f1, h, th), t0 + th * h) for th in th_grid])
         if code == 2:
             fired += 1
             assert np.all(c < 0.0), (i, c.max())
+        elif code == 1:
+            fired_pos += 1
+            assert np.all(c > 0.0), (i, c.min())
         else:
             fired_nan += 1
             assert code == 3 and np.all(np.isnan(c)), (i, code, c)
-    assert fired >= 100, fired
+    assert fired >= 100 and fired_pos >= 20, (fired, fired_pos)
     if kw["flat"]:  # in GR, -g^tt > 1 keeps NrmSq > 0 unless u7 drops by ~rs/r
         assert fired_nan >= 20, fired_nan
     assert nan_side > 0
 
 
 def test_certificate_rejects_the_conversion_surface(oracle_lib):
-    """A step that starts on the conversion surface (a sampled conversion point) is never
-    certified: its condition is ~0 there."""
-    kw = CONFIGS["flat"]
+    """A step that starts on the conversion surface (a sampled conversion point in GR, where
+    the sampler's metric is the propagation's) is never certified: its condition is ~0
+    there. (In flat space the sampler's GR surface lies 0.5-10% inside the flat one, so
+    flat-space roots start at a clearly positive condition.)"""
+    kw = CONFIGS["gr"]
     p = oracle_lib.make_params(**kw)
     s = oracle_lib.sample(p, oracle_lib.find_conversion_surface(p), 1769, 0, 64)
     n = 64
