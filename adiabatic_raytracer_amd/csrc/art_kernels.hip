@@ -388,6 +388,7 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
   unsigned s_att = 0, s_acc = 0, s_root = 0, s_scan = 0, s_interp = 0, s_rays = 0, s_cert = 0;
 #ifdef ART_COUNT_LOOPS
   unsigned s_lane_it = 0, s_main_it = 0;  // dev counters: wave iterations of the per-lane and main loops
+  unsigned s_ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // per-lane evaluations by phase
 #endif
 #pragma unroll
   for (int i = 0; i < 7; ++i) { u[i] = 0.0; f[i] = 0.0; }
@@ -671,6 +672,21 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
     double i_tha = 0.0, i_ca = 0.0, i_thb = 0.0, i_cb = 0.0, i_tr = 0.0, i_cg = 0.0;
     int i_side = 0, i_it = 0;
     bool hit = false, root_done = false;
+    // a crossing in (θ_last, θ_ip]: polish it on the true trajectory (mode ROOT), from t_int
+    auto open_root = [&](double t_int) {
+      const double thg = thgrid[ip];
+      const double last_th = thgrid[last_j];
+      hit = true;
+      hroot = hs;
+      r_tha = last_th; r_ca = last_c; r_thb = thg; r_cb = i_cg;
+      r_slope = (i_cg - last_c) / (thg - last_th);
+      r_t = (t_int > last_th && t_int < thg) ? t_int : 0.5 * (last_th + thg);
+      r_side = 0;
+      r_it = 0;
+      post_c = i_cg;
+      post_s = sgn(i_cg);
+      dt = dtnext;
+    };
 #pragma unroll 1
     while (ph != 0) {
 #ifdef ART_COUNT_LOOPS
@@ -720,6 +736,9 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
       // one condition call site: the fresh state (INIT), the re-stepped end (ROOT) or the
       // interpolant at th -- the latter exactly as scan_point forms it (bit-identical)
       double ci;
+#ifdef ART_COUNT_LOOPS
+      s_ph[mode == M_ROOT ? 1 : ph] += 1;
+#endif
       if (mode == M_ROOT) {  // the re-stepped end y (slot 2) at τ + h
         double ui[7];
 #pragma unroll
@@ -755,7 +774,7 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
         else last_c = ci;
         if (ph == 5 && !lc_ok) {
           ph = 6;
-        } else {  // open the Illinois search on the interpolant inside (θ_last, θ_ip]
+        } else {  // a bracket (θ_last, θ_ip] of the interpolant
           lc_ok = true;
           i_tha = thgrid[last_j];
           i_ca = last_c;
@@ -764,7 +783,17 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
           i_tr = i_tha - i_ca * (i_thb - i_tha) / (i_cb - i_ca);
           i_side = 0;
           i_it = 0;
-          ph = 3;
+          // The interpolant's root only seeds the polish on the true trajectory -- except
+          // right after an event, where DiffEq's repeat_nudge asks whether it lies below
+          // θ = 0.01. Only then is it refined by Illinois on the interpolant (ph 3);
+          // otherwise the polish starts from the secant point, which saves the ~6.6
+          // lone-lane Illinois iterations a bracket would cost the whole wave.
+          if (just_evented && i_tha < 0.01) {
+            ph = 3;
+          } else {
+            open_root(i_tr);
+            ph = 0;
+          }
         }
       } else {  // ph == 3: Illinois on the interpolant inside (i_tha, i_thb]
         bool stop = ci == 0.0 || isnan(ci) || (i_thb - i_tha) < 1e-12;
@@ -777,20 +806,9 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
           if (++i_it >= 40) stop = true;
         }
         if (stop) {
-          const double thg = thgrid[ip];
-          const double last_th = thgrid[last_j];
           const double t_int = i_tr;
           if (!(just_evented && t_int < 0.01)) {  // DiffEq repeat_nudge after an event
-            hit = true;
-            hroot = hs;
-            r_tha = last_th; r_ca = last_c; r_thb = thg; r_cb = i_cg;
-            r_slope = (i_cg - last_c) / (thg - last_th);
-            r_t = (t_int > last_th && t_int < thg) ? t_int : 0.5 * (last_th + thg);
-            r_side = 0;
-            r_it = 0;
-            post_c = i_cg;
-            post_s = sgn(i_cg);
-            dt = dtnext;
+            open_root(t_int);
             ph = 0;
           } else {  // ignored: continue the walk after the change point
             last_s = sgn(i_cg);
@@ -859,7 +877,7 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
 
   // wave-reduce the statistics and add them once per wave
 #ifdef ART_COUNT_LOOPS
-  const unsigned v[7] = {s_att, s_acc, s_root, s_scan, s_main_it, s_rays, s_lane_it};
+  const unsigned v[7] = {s_main_it, s_lane_it, s_ph[1], s_ph[3], s_ph[5], s_ph[6], s_ph[7]};
 #else
   const unsigned v[7] = {s_att, s_acc, s_root, s_scan, s_interp, s_rays, s_cert};
 #endif
