@@ -786,9 +786,11 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
           // The interpolant's root only seeds the polish on the true trajectory -- except
           // right after an event, where DiffEq's repeat_nudge asks whether it lies below
           // θ = 0.01. Only then is it refined by Illinois on the interpolant (ph 3);
-          // otherwise the polish starts from the secant point, which saves the ~6.6
-          // lone-lane Illinois iterations a bracket would cost the whole wave.
-          if (just_evented && i_tha < 0.01) {
+          // otherwise Vern6 starts the polish from the secant point, which saves the ~6.6
+          // lone-lane Illinois iterations a bracket would cost the whole wave. (The fixed-step
+          // RK4 path keeps the Illinois seed: with its tiny steps the oracle's own 1-ulp
+          // sensitivity is ~1e-12, and a different seed moves grazing crossings by more.)
+          if (RK4 || (just_evented && i_tha < 0.01)) {
             ph = 3;
           } else {
             open_root(i_tr);
