@@ -130,6 +130,8 @@ def main_runner_tree(params: Params, Ntajs: int, *, seed=1769, ntimes=1000, rho_
     trajectories at ntimes save points) is not supported: only segment end states are kept."""
     if saveMode > 2:
         raise NotImplementedError("saveMode > 2 (full-trajectory tree dumps) is not supported")
+    if saveMode < 3:
+        ntimes = 3  # "Times to store in ODE" (MainRunner.jl:379-381): also names the npy file
     import time
     t_start = time.perf_counter()
     n_ev = max(0, int(Ntajs) - 1)
@@ -179,3 +181,23 @@ def main_runner_tree(params: Params, Ntajs: int, *, seed=1769, ntimes=1000, rho_
         os.makedirs(os.path.dirname(path), exist_ok=True)
         np.save(path, rows)
     return rows
+
+
+def combine_files(Mass_a, Ax_g, θm, ωPul, B0, Ntajs, Nruns, file_tag, ntimes=3, dir_tag="results", num_cutoff=5,
+                  MC_nodes=5, max_nodes=50, remove=True):
+    """Gen_Samples.jl --run_Combine 1 (combine_files, Gen_Samples.jl:195-239): concatenate the
+    npy rows of runs file_tag + "0" .. file_tag + str(Nruns - 1), divide column 8 (1-based,
+    sln_prob) by Nruns, write them to dir_tag/<name with Ax_trajs = Ntajs * Nruns>.npy and
+    delete the inputs. Returns the combined path."""
+    files = [tree_file_name(dir_tag, Mass_a, Ax_g, θm, ωPul, B0, Ntajs, ntimes, num_cutoff, MC_nodes, max_nodes,
+                            f"{file_tag}{i}") for i in range(int(Nruns))]
+    hold = np.concatenate([np.load(f) for f in files], axis=0)
+    hold[:, 7] /= Nruns  # hold[:, 8] ./= Nruns (Julia 1-based, :220)
+    name = os.path.basename(tree_file_name(dir_tag, Mass_a, Ax_g, θm, ωPul, B0, Ntajs * Nruns, ntimes, num_cutoff,
+                                           MC_nodes, max_nodes, file_tag))
+    out = os.path.join(dir_tag, name[len("tree_"):])  # dir_tag/MassAx_... (:223-231)
+    np.save(out, hold)
+    if remove:
+        for f in files:
+            os.remove(f)
+    return out
