@@ -57,9 +57,10 @@ def run_point(kw: dict, rays: int, seed: int = 1769, nbins: int = 50, device: in
     out = eng.propagate(inp, max_crossings=-1)
     hist = eng.flux_histogram(out, inp["species"], None, nbins)
     torch.cuda.synchronize()
+    kernel_ms = eng.kernel_ms()  # synchronizes and latches the launch's counters
     st = A.raytracer.last_stats()
     status = torch.bincount(out["status"].long(), minlength=5).tolist()
-    return dict(rec, seconds=time.perf_counter() - t0, kernel_ms=eng.kernel_ms(), accepted=st["accepted"],
+    return dict(rec, seconds=time.perf_counter() - t0, kernel_ms=kernel_ms, accepted=st["accepted"],
                 attempts=st["attempts"], status_counts=status, flux_photon=hist[nbins:].tolist())
 
 
