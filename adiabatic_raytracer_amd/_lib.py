@@ -37,6 +37,11 @@ class TreeOpts(C.Structure):  # include/art.h art_tree_opts
                 ("prob_cutoff", C.c_double), ("seed", C.c_uint64)]
 
 
+class TreeTraj(C.Structure):  # include/art.h art_tree_traj
+    _fields_ = [("ntimes", C.c_int32), ("crossing_cap", C.c_int32), ("traj", C.c_void_p), ("times", C.c_void_p),
+                ("count", C.c_void_p), ("xc", C.c_void_p)]
+
+
 _P = C.POINTER(ArtParams)
 _v = C.c_void_p
 _i64, _i32, _d, _u64 = C.c_int64, C.c_int32, C.c_double, C.c_uint64
@@ -54,12 +59,18 @@ SIGNATURES = {
                                      C.POINTER(CrossingBuf)]),
     "art_propagate_device": (C.c_int, [_P, _i64, _v, _v, _v, _v, _v, _v, _i32, C.POINTER(SegmentOut),
                                        C.POINTER(CrossingBuf), _v]),
+    "art_propagate_traj_host": (C.c_int, [_P, _i64, _v, _v, _v, _v, _v, _v, _i32, C.POINTER(SegmentOut),
+                                          C.POINTER(CrossingBuf), _i32, _v, _v, _v]),
+    "art_propagate_traj_device": (C.c_int, [_P, _i64, _v, _v, _v, _v, _v, _v, _i32, C.POINTER(SegmentOut),
+                                            C.POINTER(CrossingBuf), _i32, _v, _v, _v, _v]),
     "art_get_prob_nonad_host": (C.c_int, [_P, _i64, _v, _v, _v, _i64, _v, _v]),
     "art_get_prob_nonad_device": (C.c_int, [_P, _i64, _v, _v, _v, _i64, _v, _v, _v]),
     "art_sample_conversion_points_host": (C.c_int, [_P, _d, _u64, _i64, _i64, _v, _v, _v, _v, _v, _v]),
     "art_sample_conversion_points_device": (C.c_int, [_P, _d, _u64, _i64, _i64, _v, _v, _v, _v, _v, _v, _v]),
     "art_flux_histogram_device": (C.c_int, [_P, _i64, _v, _v, _v, _v, _v, _i32, _v, _v]),
     "art_grow_trees": (C.c_int, [_P, _i64, _v, _v, _v, _v, C.POINTER(TreeOpts), _i64, _v, C.POINTER(_i64), _v, _v]),
+    "art_grow_trees_traj": (C.c_int, [_P, _i64, _v, _v, _v, _v, C.POINTER(TreeOpts), _i64, _v, C.POINTER(_i64), _v,
+                                      _v, C.POINTER(TreeTraj)]),
     "art_event_weight_host": (C.c_int, [_P, _d, _d, _d, _i64, _v, _v, _v, _v]),
     "art_event_weight_device": (C.c_int, [_P, _d, _d, _d, _i64, _v, _v, _v, _v, _v]),
     "art_eval_rhs_device": (C.c_int, [_P, _i64, _v, _v, _v, _v, _v, _v]),

@@ -95,9 +95,16 @@ int validate(const art_params* p) {
 // work. Only the *_host entry points use the library's own stream.
 hipStream_t pick(DeviceCtx*, void* stream) { return (hipStream_t)stream; }
 
+// saveat outputs (art_propagate_traj_*): ntimes >= 2 points per ray, or none (ntimes = 0)
+struct TrajArgs {
+  int32_t ntimes = 0;
+  double *traj = nullptr, *t = nullptr;
+  int32_t* count = nullptr;
+};
+
 int propagate_device_impl(const art_params* p, int64_t n, const double* x0, const double* k0, const double* erg,
                           const double* dw, const double* ln_t0, const int8_t* species, int32_t max_crossings,
-                          art_segment_out* out, art_crossing_buf* xc, void* stream) {
+                          art_segment_out* out, art_crossing_buf* xc, void* stream, const TrajArgs& tr = TrajArgs()) {
   int rc = validate(p);
   if (rc) return rc;
   if (n < 0 || n > 2147483647LL) return fail(ART_E_INVALID, "n must be in [0, 2^31)");
@@ -124,6 +131,13 @@ int propagate_device_impl(const art_params* p, int64_t n, const double* x0, cons
     so.cap = xc->capacity;
     so.xcount = xc->count;
     so.xpos = xc->pos; so.xk = xc->k; so.xt = xc->t; so.xdw = xc->dw; so.xp = xc->p_nonad;
+  }
+  if (tr.ntimes != 0) {
+    if (tr.ntimes < 2 || !tr.traj || !tr.t || !tr.count) return fail(ART_E_INVALID, "saveat needs ntimes >= 2 and buffers");
+    so.ntimes = tr.ntimes;
+    so.traj = tr.traj;
+    so.traj_t = tr.t;
+    so.traj_n = tr.count;
   }
   HIP_OK(hipMemsetAsync(c->scratch, 0, sizeof(unsigned long long) * (1 + art::N_STATS), s));
   HIP_OK(art::launch_propagate(K, n, in, so, max_crossings, c->scratch, c->scratch + 1, s, &g_last_grid, c->ev0,
@@ -228,10 +242,23 @@ int art_propagate_device(const art_params* p, int64_t n, const double* x0, const
   return propagate_device_impl(p, n, x0, k0, erg, dw, ln_t0, species, max_crossings, out, xc, stream);
 }
 
-int art_propagate_host(const art_params* p, int64_t n, const double* x0, const double* k0, const double* erg,
-                       const double* dw, const double* ln_t0, const int8_t* species, int32_t max_crossings,
-                       art_segment_out* out, art_crossing_buf* xc) {
+int art_propagate_traj_device(const art_params* p, int64_t n, const double* x0, const double* k0, const double* erg,
+                              const double* dw, const double* ln_t0, const int8_t* species, int32_t max_crossings,
+                              art_segment_out* out, art_crossing_buf* xc, int32_t ntimes, double* traj,
+                              double* traj_t, int32_t* traj_n, void* stream) {
   std::lock_guard<std::mutex> lk(g_mu);
+  if (ntimes < 2) return fail(ART_E_INVALID, "ntimes must be >= 2");
+  TrajArgs tr;
+  tr.ntimes = ntimes; tr.traj = traj; tr.t = traj_t; tr.count = traj_n;
+  return propagate_device_impl(p, n, x0, k0, erg, dw, ln_t0, species, max_crossings, out, xc, stream, tr);
+}
+
+}  // extern "C"
+
+namespace {
+int propagate_host_impl(const art_params* p, int64_t n, const double* x0, const double* k0, const double* erg,
+                        const double* dw, const double* ln_t0, const int8_t* species, int32_t max_crossings,
+                        art_segment_out* out, art_crossing_buf* xc, const TrajArgs& htr) {
   int rc = validate(p);
   if (rc) return rc;
   if (n == 0) return ART_OK;
@@ -267,9 +294,26 @@ int art_propagate_host(const art_params* p, int64_t n, const double* x0, const d
     dxb = art_crossing_buf{cap, cnt, xd, xd + 3 * cap * nd, xd + 6 * cap * nd, xd + 7 * cap * nd, xd + 8 * cap * nd};
     dxbp = &dxb;
   }
+  TrajArgs dtr;
+  if (htr.ntimes != 0) {
+    if (htr.ntimes < 2 || !htr.traj || !htr.t || !htr.count) return fail(ART_E_INVALID, "saveat needs ntimes >= 2 and buffers");
+    void* dt_ = nullptr;
+    const size_t nt = (size_t)htr.ntimes * nd;
+    if ((rc = pool_get(c, 7, nt * 4 * sizeof(double) + nd * sizeof(int32_t), &dt_))) return rc;
+    dtr.ntimes = htr.ntimes;
+    dtr.traj = (double*)dt_;
+    dtr.t = dtr.traj + 3 * nt;
+    dtr.count = (int32_t*)(dtr.t + nt);
+  }
   rc = propagate_device_impl(p, n, di, di + 3 * nd, di + 6 * nd, di + 7 * nd, di + 8 * nd, (const int8_t*)(di + 9 * nd),
-                             max_crossings, &dso, dxbp, s);
+                             max_crossings, &dso, dxbp, s, dtr);
   if (rc) return rc;
+  if (htr.ntimes != 0) {
+    const size_t nt = (size_t)htr.ntimes * nd;
+    HIP_OK(hipMemcpyAsync(htr.traj, dtr.traj, nt * 3 * sizeof(double), hipMemcpyDeviceToHost, s));
+    HIP_OK(hipMemcpyAsync(htr.t, dtr.t, nt * sizeof(double), hipMemcpyDeviceToHost, s));
+    HIP_OK(hipMemcpyAsync(htr.count, dtr.count, nd * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+  }
   HIP_OK(hipMemcpyAsync(out->x_end, dso.x_end, nd * 3 * sizeof(double), hipMemcpyDeviceToHost, s));
   HIP_OK(hipMemcpyAsync(out->k_end, dso.k_end, nd * 3 * sizeof(double), hipMemcpyDeviceToHost, s));
   HIP_OK(hipMemcpyAsync(out->u7_end, dso.u7_end, nd * sizeof(double), hipMemcpyDeviceToHost, s));
@@ -287,6 +331,27 @@ int art_propagate_host(const art_params* p, int64_t n, const double* x0, const d
   }
   HIP_OK(hipStreamSynchronize(s));
   return finish_timing(c);
+}
+}  // namespace
+
+extern "C" {
+
+int art_propagate_host(const art_params* p, int64_t n, const double* x0, const double* k0, const double* erg,
+                       const double* dw, const double* ln_t0, const int8_t* species, int32_t max_crossings,
+                       art_segment_out* out, art_crossing_buf* xc) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  return propagate_host_impl(p, n, x0, k0, erg, dw, ln_t0, species, max_crossings, out, xc, TrajArgs());
+}
+
+int art_propagate_traj_host(const art_params* p, int64_t n, const double* x0, const double* k0, const double* erg,
+                            const double* dw, const double* ln_t0, const int8_t* species, int32_t max_crossings,
+                            art_segment_out* out, art_crossing_buf* xc, int32_t ntimes, double* traj, double* traj_t,
+                            int32_t* traj_n) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (ntimes < 2) return fail(ART_E_INVALID, "ntimes must be >= 2");
+  TrajArgs tr;
+  tr.ntimes = ntimes; tr.traj = traj; tr.t = traj_t; tr.count = traj_n;
+  return propagate_host_impl(p, n, x0, k0, erg, dw, ln_t0, species, max_crossings, out, xc, tr);
 }
 
 int art_get_prob_nonad_device(const art_params* p, int64_t nc, const double* pos, const double* kpos,

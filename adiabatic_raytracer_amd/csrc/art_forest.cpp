@@ -38,6 +38,9 @@ struct Node {
   int status = -1, is_final = 0, n_cross = 0;
   double x_end[3] = {0, 0, 0}, k_end[3] = {0, 0, 0}, u7_end = 0.0, tau_end = 0.0;
   Cross first{};
+  // saveMode 3 (saveNode): the saved points and every kept crossing of the segment
+  std::vector<double> traj, times;
+  std::vector<Cross> xcs;
 };
 
 struct Tree {
@@ -72,12 +75,14 @@ Node make_child(const Cross& c, int species, double prob, double weight, double 
   return n;
 }
 
-}  // namespace
-
-extern "C" int art_grow_trees(const art_params* p, int64_t n, const double* x0, const double* k0, const double* erg,
-                              const int8_t* species, const art_tree_opts* opts, int64_t node_capacity,
-                              art_tree_node* nodes, int64_t* n_nodes, int32_t* counts, int32_t* infos) {
+int grow_trees_impl(const art_params* p, int64_t n, const double* x0, const double* k0, const double* erg,
+                    const int8_t* species, const art_tree_opts* opts, int64_t node_capacity, art_tree_node* nodes,
+                    int64_t* n_nodes, int32_t* counts, int32_t* infos, const art_tree_traj* tj) {
   if (!p || !opts || !n_nodes || n < 0) return ART_E_INVALID;
+  if (tj && (tj->ntimes < 2 || tj->crossing_cap < 0 || !tj->traj || !tj->times || !tj->count ||
+             (tj->crossing_cap > 0 && !tj->xc)))
+    return ART_E_INVALID;
+  const int nt = tj ? tj->ntimes : 0;
   *n_nodes = 0;
   if (n == 0) return ART_OK;
   if (!x0 || !k0 || !erg || !species) return ART_E_INVALID;
@@ -123,7 +128,8 @@ extern "C" int art_grow_trees(const art_params* p, int64_t n, const double* x0, 
   std::vector<Node> cur;
   std::vector<double> bx, bk, be, bdw, blt, sx, sk, su7, stau, cpos, ck, ct, cdw, cpn;
   std::vector<int8_t> bsp;
-  std::vector<int32_t> sst, sacc, srej, ccount;
+  std::vector<int32_t> sst, sacc, srej, ccount, trn;
+  std::vector<double> trx, trt;
   while (true) {
     idx.clear();
     cur.clear();
@@ -161,8 +167,15 @@ extern "C" int art_grow_trees(const art_params* p, int64_t n, const double* x0, 
     ct.assign(cap * m, 0.0); cdw.assign(cap * m, 0.0); cpn.assign(cap * m, 0.0);
     art_segment_out so{sx.data(), sk.data(), su7.data(), stau.data(), sst.data(), sacc.data(), srej.data()};
     art_crossing_buf xb{cap, ccount.data(), cpos.data(), ck.data(), ct.data(), cdw.data(), cpn.data()};
-    int rc = art_propagate_host(p, m, bx.data(), bk.data(), be.data(), bdw.data(), blt.data(), bsp.data(),
-                                opts->splittings_cutoff, &so, &xb);
+    int rc;
+    if (nt) {
+      trx.assign(3 * (size_t)nt * m, 0.0); trt.assign((size_t)nt * m, 0.0); trn.assign(m, 0);
+      rc = art_propagate_traj_host(p, m, bx.data(), bk.data(), be.data(), bdw.data(), blt.data(), bsp.data(),
+                                   opts->splittings_cutoff, &so, &xb, nt, trx.data(), trt.data(), trn.data());
+    } else {
+      rc = art_propagate_host(p, m, bx.data(), bk.data(), be.data(), bdw.data(), blt.data(), bsp.data(),
+                              opts->splittings_cutoff, &so, &xb);
+    }
     if (rc) return rc;
 
     // ---- crossings of each segment: merge near-duplicates, probabilities ----
@@ -242,6 +255,13 @@ extern "C" int art_grow_trees(const art_params* p, int64_t n, const double* x0, 
       const std::vector<Cross>& L = xcs[j];
       e.n_cross = (int)L.size();
       if (!L.empty()) e.first = L[0];
+      if (nt) {
+        for (int k = 0; k < trn[j]; ++k) {
+          for (int c = 0; c < 3; ++c) e.traj.push_back(trx[((size_t)c * nt + k) * m + j]);
+          e.times.push_back(trt[(size_t)k * m + j]);
+        }
+        e.xcs = L;
+      }
       if (L.empty()) {  // no crossings (:200-207)
         T.count_main += 1;
         T.tot_prob += e.weight;
@@ -336,7 +356,36 @@ extern "C" int art_grow_trees(const art_params* p, int64_t n, const double* x0, 
       r.tc = e.first.t;
       r.dwc = e.first.dw;
       r.pc = e.first.P;
+      if (tj) {
+        const int64_t q = o - 1;
+        const int cnt = (int)e.times.size();
+        tj->count[q] = cnt;
+        for (int k = 0; k < nt; ++k) {
+          for (int c = 0; c < 3; ++c) tj->traj[(q * nt + k) * 3 + c] = k < cnt ? e.traj[3 * k + c] : 0.0;
+          tj->times[q * nt + k] = k < cnt ? e.times[k] : 0.0;
+        }
+        for (int jx = 0; jx < tj->crossing_cap; ++jx) {
+          const bool have = jx < (int)e.xcs.size();
+          for (int c = 0; c < 3; ++c) tj->xc[(q * tj->crossing_cap + jx) * 4 + c] = have ? e.xcs[jx].pos[c] : 0.0;
+          tj->xc[(q * tj->crossing_cap + jx) * 4 + 3] = have ? e.xcs[jx].t : 0.0;
+        }
+      }
     }
   }
   return ART_OK;
+}
+
+}  // namespace
+
+extern "C" int art_grow_trees(const art_params* p, int64_t n, const double* x0, const double* k0, const double* erg,
+                              const int8_t* species, const art_tree_opts* opts, int64_t node_capacity,
+                              art_tree_node* nodes, int64_t* n_nodes, int32_t* counts, int32_t* infos) {
+  return grow_trees_impl(p, n, x0, k0, erg, species, opts, node_capacity, nodes, n_nodes, counts, infos, nullptr);
+}
+
+extern "C" int art_grow_trees_traj(const art_params* p, int64_t n, const double* x0, const double* k0,
+                                   const double* erg, const int8_t* species, const art_tree_opts* opts,
+                                   int64_t node_capacity, art_tree_node* nodes, int64_t* n_nodes, int32_t* counts,
+                                   int32_t* infos, const art_tree_traj* traj) {
+  return grow_trees_impl(p, n, x0, k0, erg, species, opts, node_capacity, nodes, n_nodes, counts, infos, traj);
 }

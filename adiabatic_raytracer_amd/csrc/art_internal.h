@@ -18,6 +18,12 @@ struct SegOut {
   int32_t cap;
   int32_t* xcount;
   double *xpos, *xk, *xt, *xdw, *xp;
+  // saveat (RayTracer.jl:176, 383), only with ntimes >= 2: ntimes points per ray, positions
+  // [(c * ntimes + k) * n + ray] (spherical from the integrator, Cartesian after finalize),
+  // ln t [k * n + ray], and the number of points of each ray
+  int32_t ntimes;
+  double *traj, *traj_t;
+  int32_t* traj_n;
 };
 constexpr int N_STATS = 8;  // propagate statistics: attempts, accepted, root re-steps, scan evals,
                             // interpolant-root evals, rays, init RHS, (reserved)

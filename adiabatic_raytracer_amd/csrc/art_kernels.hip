@@ -112,6 +112,11 @@ __host__ __device__ inline void hermite7(const T* u0, const T* f0, const T* u1, 
   for (int i = 0; i < 7; ++i) out[i] = a * u0[i] + th * u1[i] + b * (c1 * (u1[i] - u0[i]) + c2 * f0[i] + c3 * f1[i]);
 }
 
+// one component of hermite7
+__device__ inline double hermite1(double u0, double f0, double u1, double f1, double h, double th) {
+  return (1.0 - th) * u0 + th * u1 + th * (th - 1.0) * ((1.0 - 2.0 * th) * (u1 - u0) + (th - 1.0) * h * f0 + th * h * f1);
+}
+
 __device__ inline int sgn(double x) { return (x > 0.0) - (x < 0.0); }
 
 // One point of the resonance scan: the condition on the cubic Hermite interpolant of the
@@ -346,7 +351,7 @@ __device__ inline KParams specialize(const KParams& P) {
   return Q;
 }
 
-template <int INTEG, int GEOM>
+template <int INTEG, int GEOM, bool SAVE>
 __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(const KParams P_in, const int64_t n,
                                                                               const SegIn in, const SegOut out,
                                                                               const int32_t max_crossings,
@@ -384,6 +389,7 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
   double hroot = 0.0, r_tha = 0.0, r_ca = 0.0, r_thb = 0.0, r_cb = 0.0, r_t = 0.0, r_slope = 1.0, post_c = 0.0;
   int post_s = 0, r_side = 0, r_it = 0;
   int wnext = 0, wend = 0;
+  int save_k = 1;  // SAVE: the next interior saveat index
   bool exhausted = false;
   unsigned s_att = 0, s_acc = 0, s_root = 0, s_scan = 0, s_interp = 0, s_rays = 0, s_cert = 0;
 #ifdef ART_COUNT_LOOPS
@@ -428,6 +434,7 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
           sprev = isnan(cprev) ? 0 : sgn(cprev);
           tau = in.lnt0[ray];
           n_acc = n_rej = ncross = iter = 0;
+          save_k = 1;
           just_evented = false;
           qpow = qpow_init;  // qoldinit = 1e-4
           s_rays += 1;
@@ -823,6 +830,28 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
         }
       }
     }
+    if constexpr (SAVE) {
+      // saveat (RayTracer.jl:176, 383): the interior save times ln t0 + kΔ that this completed
+      // step passed -- an accepted step without a crossing, or the polish step that ends at a
+      // root -- from the step's parked interpolant. finalize_kernel adds the start and the end.
+      if (((scan && !hit) || root_done) && save_k < out.ntimes - 1) {
+        const double t0 = in.lnt0[ray];
+        const double D = (tend - t0) / double(out.ntimes - 1);
+        const double tb = (last && !root_done) ? tend : tau + hs;
+        while (save_k < out.ntimes - 1) {
+          const double ts = t0 + double(save_k) * D;
+          if (!(ts <= tb)) break;
+          const double th = (ts - tau) / hs;
+#pragma unroll
+          for (int c = 0; c < 3; ++c)
+            out.traj[(int64_t(c) * out.ntimes + save_k) * n + ray] =
+                hermite1(L[(0 * 7 + c) * BLOCK], L[(1 * 7 + c) * BLOCK], L[(2 * 7 + c) * BLOCK],
+                         L[(3 * 7 + c) * BLOCK], hs, th);
+          out.traj_t[int64_t(save_k) * n + ray] = ts;
+          ++save_k;
+        }
+      }
+    }
 #pragma unroll
     for (int i = 0; i < 7; ++i) {
       u[i] = L[(0 * 7 + i) * BLOCK];
@@ -872,6 +901,7 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
       out.n_acc[ray] = n_acc;
       out.n_rej[ray] = n_rej;
       if (out.xcount) out.xcount[ray] = ncross;
+      if constexpr (SAVE) out.traj_n[ray] = save_k + 1;  // start + interior + end
       ray = -1;
       mode = M_IDLE;
     }
@@ -955,6 +985,31 @@ __global__ __launch_bounds__(256) void finalize_kernel(const KParams P, const in
     for (int c = 0; c < 3; ++c) {
       out.x_end[c * n + i] = xe[c];
       out.k_end[c * n + i] = ke[c];
+    }
+  }
+  if (out.ntimes >= 2) {  // saveat: start (u0 back-transformed), interior to Cartesian, end
+    double u0[7], xs[3], ks[3];
+#pragma unroll
+    for (int c = 0; c < 7; ++c) u0[c] = in.u0[c * n + i];
+    back_transform(P, u0, erg, xs, ks);
+    const int m = out.traj_n[i];
+    for (int k = 0; k < m; ++k) {
+      double x[3];
+      if (k == 0) {
+        x[0] = xs[0]; x[1] = xs[1]; x[2] = xs[2];
+        out.traj_t[i] = in.lnt0[i];
+      } else if (k == m - 1) {
+        x[0] = out.x_end[i]; x[1] = out.x_end[n + i]; x[2] = out.x_end[2 * n + i];
+        out.traj_t[int64_t(k) * n + i] = out.tau_end[i];
+      } else {
+        const double r = out.traj[(int64_t(0) * out.ntimes + k) * n + i];
+        double st, ct, sp, cp;
+        msincos(out.traj[(int64_t(1) * out.ntimes + k) * n + i], st, ct);
+        msincos(out.traj[(int64_t(2) * out.ntimes + k) * n + i], sp, cp);
+        x[0] = r * st * cp; x[1] = r * st * sp; x[2] = r * ct;
+      }
+#pragma unroll
+      for (int c = 0; c < 3; ++c) out.traj[(int64_t(c) * out.ntimes + k) * n + i] = x[c];
     }
   }
   if (!out.xcount) return;
@@ -1255,8 +1310,13 @@ hipError_t launch_propagate(const KParams& P, int64_t n, const SegIn& in, const 
   const bool rk4 = P.integrator == ART_RK4;
   using KFn = void (*)(const KParams, const int64_t, const SegIn, const SegOut, const int32_t, unsigned long long*,
                        unsigned long long*);
-  const KFn fn = rk4 ? (flat ? propagate_kernel<ART_RK4, GEOM_FLAT> : propagate_kernel<ART_RK4, GEOM_ANY>)
-                     : (flat ? propagate_kernel<ART_VERN6, GEOM_FLAT> : propagate_kernel<ART_VERN6, GEOM_ANY>);
+  KFn fn;
+  if (out.ntimes >= 2)  // saveat requested: the saving instantiations
+    fn = rk4 ? propagate_kernel<ART_RK4, GEOM_ANY, true>
+             : (flat ? propagate_kernel<ART_VERN6, GEOM_FLAT, true> : propagate_kernel<ART_VERN6, GEOM_ANY, true>);
+  else
+    fn = rk4 ? (flat ? propagate_kernel<ART_RK4, GEOM_FLAT, false> : propagate_kernel<ART_RK4, GEOM_ANY, false>)
+             : (flat ? propagate_kernel<ART_VERN6, GEOM_FLAT, false> : propagate_kernel<ART_VERN6, GEOM_ANY, false>);
   const int grid = persistent_blocks((const void*)fn, n);
   if (grid_out) *grid_out = grid;
   if (ev0 && (e = hipEventRecord(ev0, s)) != hipSuccess) return e;
@@ -1320,13 +1380,19 @@ hipError_t launch_eval_condition(const KParams& P, int64_t n, const double* u, c
   return hipGetLastError();
 }
 
-template __global__ void propagate_kernel<ART_VERN6, GEOM_ANY>(const KParams, const int64_t, const SegIn, const SegOut,
-                                                               const int32_t, unsigned long long*, unsigned long long*);
-template __global__ void propagate_kernel<ART_VERN6, GEOM_FLAT>(const KParams, const int64_t, const SegIn, const SegOut,
-                                                                const int32_t, unsigned long long*, unsigned long long*);
-template __global__ void propagate_kernel<ART_RK4, GEOM_ANY>(const KParams, const int64_t, const SegIn, const SegOut,
-                                                             const int32_t, unsigned long long*, unsigned long long*);
-template __global__ void propagate_kernel<ART_RK4, GEOM_FLAT>(const KParams, const int64_t, const SegIn, const SegOut,
-                                                              const int32_t, unsigned long long*, unsigned long long*);
+template __global__ void propagate_kernel<ART_VERN6, GEOM_ANY, false>(const KParams, const int64_t, const SegIn, const SegOut,
+    const int32_t, unsigned long long*, unsigned long long*);
+template __global__ void propagate_kernel<ART_VERN6, GEOM_FLAT, false>(const KParams, const int64_t, const SegIn, const SegOut,
+    const int32_t, unsigned long long*, unsigned long long*);
+template __global__ void propagate_kernel<ART_RK4, GEOM_ANY, false>(const KParams, const int64_t, const SegIn, const SegOut,
+    const int32_t, unsigned long long*, unsigned long long*);
+template __global__ void propagate_kernel<ART_RK4, GEOM_FLAT, false>(const KParams, const int64_t, const SegIn, const SegOut,
+    const int32_t, unsigned long long*, unsigned long long*);
+template __global__ void propagate_kernel<ART_VERN6, GEOM_ANY, true>(const KParams, const int64_t, const SegIn, const SegOut,
+    const int32_t, unsigned long long*, unsigned long long*);
+template __global__ void propagate_kernel<ART_VERN6, GEOM_FLAT, true>(const KParams, const int64_t, const SegIn, const SegOut,
+    const int32_t, unsigned long long*, unsigned long long*);
+template __global__ void propagate_kernel<ART_RK4, GEOM_ANY, true>(const KParams, const int64_t, const SegIn, const SegOut,
+    const int32_t, unsigned long long*, unsigned long long*);
 
 }  // namespace art

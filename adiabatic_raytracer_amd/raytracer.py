@@ -161,8 +161,11 @@ def propagate(x0, k0, nsteps, Mvars, NumerP, rhs=func_photon, make_tree=True, is
         p_nonad=[sc(res["xc_p"], i) for i in range(n)])
 
 
-def propagate_batch(params: Params, x0, k0, erg, dw, ln_t0, species, max_crossings=-1, capacity=1) -> dict:
-    """Low-level host entry (art_propagate_host): SoA numpy inputs, dict of numpy outputs."""
+def propagate_batch(params: Params, x0, k0, erg, dw, ln_t0, species, max_crossings=-1, capacity=1,
+                    ntimes=None) -> dict:
+    """Low-level host entry (art_propagate_host): SoA numpy inputs, dict of numpy outputs.
+    With ntimes >= 2 (art_propagate_traj_host) also the saved points of RayTracer.jl:176,383:
+    traj (3, ntimes, n) Cartesian positions, traj_t (ntimes, n) ln t, traj_n (n) points."""
     lib = _lib.load()
     n = int(np.asarray(erg).size)
     f64 = lambda a: np.ascontiguousarray(a, np.float64)  # noqa: E731
@@ -179,8 +182,16 @@ def propagate_batch(params: Params, x0, k0, erg, dw, ln_t0, species, max_crossin
                                                "n_reject")])
     xb = CrossingBuf(capacity, *[_ptr(out[k]) for k in ("n_cross", "xc_pos", "xc_k", "xc_t", "xc_dw", "xc_p")])
     cp = params.to_c()
-    check(lib.art_propagate_host(C.byref(cp), n, _ptr(x0), _ptr(k0), _ptr(erg), _ptr(dw), _ptr(ln_t0), _ptr(species),
-                                 int(max_crossings), C.byref(so), C.byref(xb)))
+    if ntimes:
+        out.update(traj=np.zeros(3 * ntimes * n), traj_t=np.zeros(ntimes * n), traj_n=np.zeros(n, np.int32))
+        check(lib.art_propagate_traj_host(C.byref(cp), n, _ptr(x0), _ptr(k0), _ptr(erg), _ptr(dw), _ptr(ln_t0),
+                                          _ptr(species), int(max_crossings), C.byref(so), C.byref(xb), int(ntimes),
+                                          _ptr(out["traj"]), _ptr(out["traj_t"]), _ptr(out["traj_n"])))
+        out["traj"] = out["traj"].reshape(3, ntimes, n)
+        out["traj_t"] = out["traj_t"].reshape(ntimes, n)
+    else:
+        check(lib.art_propagate_host(C.byref(cp), n, _ptr(x0), _ptr(k0), _ptr(erg), _ptr(dw), _ptr(ln_t0),
+                                     _ptr(species), int(max_crossings), C.byref(so), C.byref(xb)))
     out["kernel_ms"] = lib.art_last_kernel_ms()
     out["stats"] = last_stats()
     return out

@@ -18,7 +18,7 @@ from dataclasses import replace
 import numpy as np
 
 from . import _lib
-from ._lib import TreeOpts, check
+from ._lib import TreeOpts, TreeTraj, check
 from .raytracer import Params, event_weight, sample_conversion_points
 
 AXION, PHOTON = 0, 1
@@ -37,10 +37,13 @@ NODE_DTYPE = np.dtype([
 
 
 def grow_trees(params: Params, x0, k0, erg, species, *, num_cutoff=5, mc_nodes=5, max_nodes=50,
-               splittings_cutoff=-1, crossing_cap=64, prob_cutoff=1e-10, seed=1769):
+               splittings_cutoff=-1, crossing_cap=64, prob_cutoff=1e-10, seed=1769, ntimes=None):
     """get_tree for n roots RT.node(x0, k0, 0, -1, species, 1, 1, -1, -1, -1) (MainRunner.jl:578-590,
     :653-667). x0, k0: (n, 3) or SoA 3n; erg: erg_inf_ini per root. Returns (nodes, counts,
-    infos): nodes is a NODE_DTYPE record array grouped by tree in get_tree's push order."""
+    infos): nodes is a NODE_DTYPE record array grouped by tree in get_tree's push order.
+    With ntimes (>= 2, saveMode 3) a fourth item holds every node's saveNode data
+    (art_grow_trees_traj): traj (nodes, ntimes, 3) Cartesian saved points, times (nodes,
+    ntimes) their ln t, count (nodes,), xc (nodes, cap, 4) the kept crossings (x, y, z, tc)."""
     x0, k0 = np.asarray(x0, np.float64), np.asarray(k0, np.float64)
     erg = np.ascontiguousarray(erg, np.float64).reshape(-1)
     n = erg.size
@@ -53,16 +56,27 @@ def grow_trees(params: Params, x0, k0, erg, species, *, num_cutoff=5, mc_nodes=5
     cap = max(1, n * per_tree)
     lib = _lib.load()
     ptr = lambda a: a.ctypes.data_as(C.c_void_p)  # noqa: E731
+    xcap = max(1, crossing_cap) if splittings_cutoff > 0 else 1
     while True:
         nodes = np.zeros(cap, NODE_DTYPE)
         nn = C.c_int64(0)
         counts, infos = np.zeros(n, np.int32), np.zeros(n, np.int32)
-        rc = lib.art_grow_trees(C.byref(params.to_c()), n, ptr(x0), ptr(k0), ptr(erg), ptr(sp), C.byref(opts), cap,
-                                ptr(nodes), C.byref(nn), ptr(counts), ptr(infos))
+        if ntimes:
+            tr = {"traj": np.zeros((cap, ntimes, 3)), "times": np.zeros((cap, ntimes)),
+                  "count": np.zeros(cap, np.int32), "xc": np.zeros((cap, xcap, 4))}
+            tt = TreeTraj(int(ntimes), xcap, *[ptr(tr[k]) for k in ("traj", "times", "count", "xc")])
+            rc = lib.art_grow_trees_traj(C.byref(params.to_c()), n, ptr(x0), ptr(k0), ptr(erg), ptr(sp),
+                                         C.byref(opts), cap, ptr(nodes), C.byref(nn), ptr(counts), ptr(infos),
+                                         C.byref(tt))
+        else:
+            rc = lib.art_grow_trees(C.byref(params.to_c()), n, ptr(x0), ptr(k0), ptr(erg), ptr(sp), C.byref(opts),
+                                    cap, ptr(nodes), C.byref(nn), ptr(counts), ptr(infos))
         if rc == -3 and nn.value > cap:  # ART_E_NOMEM: grow and redo (pathological trees only)
             cap = nn.value
             continue
         check(rc)
+        if ntimes:
+            return nodes[:nn.value], counts, infos, {k: v[:nn.value] for k, v in tr.items()}
         return nodes[:nn.value], counts, infos
 
 
@@ -119,6 +133,29 @@ def _write_event_text(dir_tag, file_tag, n_ev, s, w, x, k, tree, fin, ev, wgt, i
             ff.write(f"{int(ev[q]) + 1} {jl(wgt[q])} {int(ident[q])} " + " ".join(jl(a) for a in vals) + f" {t}\n")
 
 
+SPECIES_NAME = {AXION: "axion", PHOTON: "photon"}
+
+
+def save_node(fh, node, tr, q):
+    """saveNode(f, n) (MainRunner.jl:17-65) for node q of a grow_trees(..., ntimes) result:
+    species, weight, prob, parent_weight; the crossing x, y, z and tc lines (or "-" x 3);
+    the saved trajectory's x, y, z and ln t lines. Julia number formatting."""
+    fh.write(f"{SPECIES_NAME[int(node['species'])]} {jl(node['weight'])} {jl(node['prob'])} "
+             f"{jl(node['parent_weight'])}\n")
+    m = min(int(node["n_cross"]), tr["xc"].shape[1])
+    if m > 0:
+        for c in range(3):
+            fh.write("".join("  " + jl(tr["xc"][q, j, c]) for j in range(m)) + "\n")
+        fh.write("".join("  " + jl(tr["xc"][q, j, 3]) for j in range(m)))
+    else:
+        fh.write("-\n-\n-")
+    fh.write("\n")
+    cnt = int(tr["count"][q])
+    for c in range(3):
+        fh.write("".join("  " + jl(tr["traj"][q, k, c]) for k in range(cnt)) + "\n")
+    fh.write("".join("  " + jl(tr["times"][q, k]) for k in range(cnt)) + "\n")
+
+
 def main_runner_tree(params: Params, Ntajs: int, *, seed=1769, ntimes=1000, rho_DM=0.45, n_maxSample=6,
                      num_cutoff=5, MC_nodes=5, max_nodes=50, prob_cutoff=1e-10, saveMode=0, dir_tag=None,
                      file_tag="", backtrace_cap=256):
@@ -126,10 +163,9 @@ def main_runner_tree(params: Params, Ntajs: int, *, seed=1769, ntimes=1000, rho_
     `while photon_trajs < desired_trajs` loop), all events batched on the GPU. Returns the
     row matrix (13 columns, 29 with saveMode > 0) after the final division of column 8 by
     f_inx, and writes it to the reference's npy path when dir_tag is given; saveMode > 1
-    also writes the event_/final_ text files. saveMode > 2 (saveNode dumps of whole
-    trajectories at ntimes save points) is not supported: only segment end states are kept."""
-    if saveMode > 2:
-        raise NotImplementedError("saveMode > 2 (full-trajectory tree dumps) is not supported")
+    also writes the event_/final_ text files and saveMode > 2 one tree_<file_tag><event>
+    file per event with saveNode of the backtrace node and of every forward-tree node
+    (MainRunner.jl:573-577, :612, :671), each segment saved at ntimes points."""
     if saveMode < 3:
         ntimes = 3  # "Times to store in ODE" (MainRunner.jl:379-381): also names the npy file
     import time
@@ -146,14 +182,24 @@ def main_runner_tree(params: Params, Ntajs: int, *, seed=1769, ntimes=1000, rho_
     # f_inx: find_samples_new calls minus accepted samples (MainRunner.jl:463-481)
     f_inx = int(np.sum(s["attempts"].astype(np.int64) - 1))
     # backtrace: axion, -k, -B0, every crossing, only the root is processed (:578-590)
-    nb, c_bck, _ = grow_trees(replace(params, B0=-params.B0), x, -k, erg, AXION, num_cutoff=0,
-                              splittings_cutoff=100000, crossing_cap=backtrace_cap, prob_cutoff=prob_cutoff,
-                              seed=seed)
+    dumps = saveMode > 2 and dir_tag is not None
+    got = grow_trees(replace(params, B0=-params.B0), x, -k, erg, AXION, num_cutoff=0, splittings_cutoff=100000,
+                     crossing_cap=backtrace_cap, prob_cutoff=prob_cutoff, seed=seed, ntimes=ntimes if dumps else None)
+    nb, c_bck = got[0], got[1]
     samp_back_weight = nb["prob"] * nb["weight"]  # (:635)
     prob0 = nb["prob"]
     # forward photon tree from the sample (:653-667)
-    tree, counts, infos = grow_trees(params, x, k, erg, PHOTON, num_cutoff=num_cutoff, mc_nodes=MC_nodes,
-                                     max_nodes=max_nodes, prob_cutoff=prob_cutoff, seed=seed)
+    fwd = grow_trees(params, x, k, erg, PHOTON, num_cutoff=num_cutoff, mc_nodes=MC_nodes, max_nodes=max_nodes,
+                     prob_cutoff=prob_cutoff, seed=seed, ntimes=ntimes if dumps else None)
+    tree, counts, infos = fwd[:3]
+    if dumps:  # saveMode > 2: one file per event, the backtrace node then the forward tree
+        d = os.path.join(dir_tag, "tree")
+        os.makedirs(d, exist_ok=True)
+        for e in range(n_ev):
+            with open(os.path.join(d, f"tree_{file_tag}{e + 1}"), "w") as fh:
+                save_node(fh, nb[e], got[3], e)
+                for q in np.flatnonzero(tree["tree"] == e):
+                    save_node(fh, tree[q], fwd[3], q)
     fin = tree[tree["is_final"] != 0]
     ev = fin["tree"]
     θf, ϕf, _ = _angles(fin["k_end"])

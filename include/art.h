@@ -10,13 +10,15 @@
  *
  *   art_propagate_host / _device   RT.propagate              RayTracer.jl:171-452
  *       (callers MainRunner.jl:179-182 photon, :187-190 axion)
+ *   art_propagate_traj_host/_dev   RT.propagate with saveat points (RayTracer.jl:176,383,444)
  *   art_get_prob_nonad_host/_dev   get_Prob_nonAD            MainRunner.jl:67-124
  *       (-> RT.conversion_prob RayTracer.jl:1405-1473; callers MainRunner.jl:134,265)
  *   art_sample_conversion_points_* RT.find_samples_new + k_norm_Cart
  *                                  RayTracer.jl:1480-1653, MainRunner.jl:463-529
  *   art_find_conversion_surface    RT.Find_Conversion_Surface RayTracer.jl:1250-1263
  *   art_flux_histogram_device      plot/flux.py:38-48 (binned flux, reduced over ranks)
- *   art_grow_trees                 get_tree (MainRunner.jl:126-352) for n trees, batched
+ *   art_grow_trees[_traj]          get_tree (MainRunner.jl:126-352) for n trees, batched
+ *                                  (_traj: + saveNode data, MainRunner.jl:17-65)
  *   art_event_weight_*             sln_prob of a sampled point: dwp_ds cos_w + g_det
  *                                  (MainRunner.jl:498-557, RayTracer.jl:734-754,1327-1403)
  *   art_eval_*_device              pointwise physics (func!, func_axion!, hamiltonian,
@@ -157,6 +159,25 @@ int art_propagate_device(const art_params* p, int64_t n, const double* x0, const
                          const int8_t* species, int32_t max_crossings,
                          art_segment_out* out, art_crossing_buf* xc, void* stream);
 
+/* ---- RT.propagate with its saved points (saveat, RayTracer.jl:176, 383, 427-444) ----
+ * As art_propagate_*, plus up to ntimes (>= 2) saved points per ray: the start, the
+ * interior times ln_t0 + k (ln_t_end - ln_t0)/(ntimes - 1) that the segment reached before
+ * it ended (from the step's cubic Hermite interpolant), and the end state -- the
+ * reference's x_reshaped[:, :, k] and times = sol.t, without the duplicate points DiffEq
+ * adds at callback events. Used by saveMode 3 tree dumps (saveNode, MainRunner.jl:17-65).
+ * traj: 3*ntimes*n Cartesian positions [(c*ntimes + k)*n + i]; traj_t: ntimes*n ln t
+ * [k*n + i]; traj_n: n points per ray (2 .. ntimes). */
+int art_propagate_traj_host(const art_params* p, int64_t n, const double* x0, const double* k0,
+                            const double* erg, const double* dw, const double* ln_t0,
+                            const int8_t* species, int32_t max_crossings, art_segment_out* out,
+                            art_crossing_buf* xc, int32_t ntimes, double* traj, double* traj_t,
+                            int32_t* traj_n);
+int art_propagate_traj_device(const art_params* p, int64_t n, const double* x0, const double* k0,
+                              const double* erg, const double* dw, const double* ln_t0,
+                              const int8_t* species, int32_t max_crossings, art_segment_out* out,
+                              art_crossing_buf* xc, int32_t ntimes, double* traj, double* traj_t,
+                              int32_t* traj_n, void* stream);
+
 /* ---- get_Prob_nonAD (MainRunner.jl:67-124) ----
  * One call of the reference per group: group g covers crossings
  * [group_start[g], group_start[g+1]) and reproduces the reference's column-major
@@ -231,6 +252,23 @@ int art_grow_trees(const art_params* p, int64_t n, const double* x0, const doubl
                    const double* erg, const int8_t* species, const art_tree_opts* opts,
                    int64_t node_capacity, art_tree_node* nodes, int64_t* n_nodes,
                    int32_t* counts, int32_t* infos);
+
+/* saveMode 3 tree dumps (saveNode, MainRunner.jl:17-65, called at :612 and :671): per node,
+ * its saved trajectory points (art_propagate_traj_*) and all of its crossings after the
+ * 1e-5 km merge. Arrays are caller-owned, node_capacity records each. */
+typedef struct art_tree_traj {
+  int32_t ntimes;       /* saved points per segment, >= 2 (Gen_Samples.jl:164: 3)            */
+  int32_t crossing_cap; /* crossings kept per node in xc                                      */
+  double* traj;         /* node_capacity*ntimes*3 Cartesian positions [node][k][c]            */
+  double* times;        /* node_capacity*ntimes   ln t of each point (sol.t, RayTracer.jl:444) */
+  int32_t* count;       /* node_capacity          points of each node                         */
+  double* xc;           /* node_capacity*crossing_cap*4 (x, y, z, tc) [node][j][c]             */
+} art_tree_traj;
+/* art_grow_trees plus the saveNode data of every node. */
+int art_grow_trees_traj(const art_params* p, int64_t n, const double* x0, const double* k0,
+                        const double* erg, const int8_t* species, const art_tree_opts* opts,
+                        int64_t node_capacity, art_tree_node* nodes, int64_t* n_nodes,
+                        int32_t* counts, int32_t* infos, const art_tree_traj* traj);
 
 /* ---- event weight of sampled points (MainRunner.jl:498-557) ----
  * For n sampled conversion points (x, k_init, vifty: 3n SoA, as returned by the
