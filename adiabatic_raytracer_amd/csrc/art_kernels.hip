@@ -505,8 +505,8 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
 #pragma unroll
           for (int q = 1; q < LDS_SLOTS; ++q) e += T.e_L[q] * L[(q * 7 + i) * BLOCK];
           e *= hs;
-          const double sc = P.abstol + fmax(fabs(u[i]), fabs(y[i])) * P.reltol;
-          acc += (e / sc) * (e / sc);
+          const double q = e * frcp(P.abstol + fmax(fabs(u[i]), fabs(y[i])) * P.reltol);
+          acc += q * q;
         }
         EEst = sqrt(acc / 7.0);
       }

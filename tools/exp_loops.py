@@ -2,7 +2,7 @@ import json, os, sys
 sys.path.insert(0, "/root/repo")
 import adiabatic_raytracer_amd as A
 from adiabatic_raytracer_amd import Engine
-n = 1_000_000
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 1_000_000
 for name, kw in (("flat", dict(theta_m=0.2, mass_a=1e-5, flat=True)),):
     eng = Engine(A.Params(**kw))
     inp = eng.forward_roots(n, seed=1769)
