@@ -480,17 +480,24 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
 #pragma unroll
       for (int i = 0; i < 7; ++i) y[i] = u[i] + hs * acc[i];
       const double ty = tau + T.ct[s] * hs;
-      if (mode == M_STEP || mode == M_ROOT) {
-        rhs(P, photon, y, ty, erg, kk);
-        if (T.storeA[s]) {
+      // Every lane evaluates the photon RHS -- idle lanes (a draining wave) on stale state,
+      // whose results nothing reads -- so the slot has no divergent control flow. Axion
+      // segments (the tree driver's batches) take a wave-uniform detour and a select.
+      rhs_photon(P, y, ty, erg, kk);
+      if (__ballot(!photon) != 0ull) {
+        double ka[7];
+        rhs_axion(P, y, ty, erg, ka);
 #pragma unroll
-          for (int i = 0; i < 7; ++i) kA[i] = kk[i];
-        }
-        const int sl = T.storeL[s];
-        if (sl >= 0) {
+        for (int i = 0; i < 7; ++i) kk[i] = photon ? kk[i] : ka[i];
+      }
+      if (T.storeA[s]) {
 #pragma unroll
-          for (int i = 0; i < 7; ++i) L[(sl * 7 + i) * BLOCK] = kk[i];
-        }
+        for (int i = 0; i < 7; ++i) kA[i] = kk[i];
+      }
+      const int sl = T.storeL[s];
+      if (sl >= 0) {
+#pragma unroll
+        for (int i = 0; i < 7; ++i) L[(sl * 7 + i) * BLOCK] = kk[i];
       }
     }
     // y = u_{n+1}, kk = f(u_{n+1}) for stepping lanes
