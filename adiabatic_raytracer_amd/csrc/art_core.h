@@ -236,7 +236,8 @@ __host__ __device__ inline T layer_wp(const KParams& P, const T& r, double rmax)
 // radius clamped to rNS (:531) while the prefactor's g^rr uses the raw radius (:82).
 // bndry_lyr enters only the ∂t pass (:84-88).
 template <class T>
-__host__ __device__ inline void rhs_photon(const KParams& P, const T* u, const T& tau, double erg, T* du) {
+__host__ __device__ inline void rhs_photon(const KParams& P, const T* u, const T& tau, double erg, T* du,
+                                           T* aux = nullptr) {
   const T t = mexp(tau);
   const T r = u[0];
   const T E = -u[6];
@@ -321,6 +322,10 @@ __host__ __device__ inline void rhs_photon(const KParams& P, const T* u, const T
   }
   const T H_T = 0.5 * (dwp2_T * omQ + wp2_T * P.omega * Q_p);
   du[6] = H_T * t * grr_u * iE;
+  if (aux) {  // for the scan certificate: Bz/B_n and t at this point
+    aux[0] = d.b;
+    aux[1] = t;
+  }
 }
 
 // func_axion! (RayTracer.jl:95-123) with hamiltonian_axion (:632-640): H = K/2 at fixed
@@ -518,8 +523,11 @@ __host__ __device__ inline Hull bernstein_hull(double a, double fa, double b, do
 // (positive: ωp² g^rr > u7² all along the step, below), 3 (NaN: u7² (-g^tt) < m_a² all along
 // the step, where the reference's √NrmSq is undefined and condition_nd returns NaN), or 0
 // when nothing is certain.
+// b1 = Bz/B_n and t1 = e^(τ + h) at the end point come from the step's last RHS evaluation
+// (rhs_photon's aux), so the certificate needs no transcendental of its own.
 __host__ __device__ inline int scan_certified_code(const KParams& P, const double* u0, const double* f0,
-                                                   const double* u1, const double* f1, double h, double tau) {
+                                                   const double* u1, const double* f1, double h, double b1,
+                                                   double t1) {
   if (!(P.cert_fac < 1e300)) return 0;
   const Hull r = bernstein_hull(u0[0], f0[0], u1[0], f1[0], h);
   if (!(r.lo > P.cert_rmin)) return 0;
@@ -532,13 +540,9 @@ __host__ __device__ inline int scan_certified_code(const KParams& P, const doubl
   if (!(elo * elo > P.cert_e2)) return 0;
   const Hull th = bernstein_hull(u0[1], f0[1], u1[1], f1[1], h);
   const Hull ph = bernstein_hull(u0[2], f0[2], u1[2], f1[2], h);
-  const double t0 = exp(tau), t1 = exp(tau + h);  // t = e^(τ + θh) is monotone over the step
-  double st, ct, sp, cp;
-  msincos(u1[1], st, ct);
-  msincos(u1[2] - P.omega * t1, sp, cp);
-  const double b1 = P.cm * (3.0 * ct * ct - 1.0) + 3.0 * P.sm * st * ct * cp;
+  // t = e^(τ + θh) rises monotonically over the step, by t1 - t0 = t1 (1 - e^-h) <= t1 h
   const double dth = fmax(th.hi - u1[1], u1[1] - th.lo);
-  const double dps = fmax(ph.hi - u1[2], u1[2] - ph.lo) + fabs(P.omega) * (t1 - t0) * (1.0 + 1e-12);
+  const double dps = fmax(ph.hi - u1[2], u1[2] - ph.lo) + fabs(P.omega) * t1 * h * (1.0 + 1e-12);
   const double db = 3.0 * dth + 1.5 * fabs(P.sm) * dps + 1e-12;
   const double bmax = fmin(2.0, fabs(b1) + db);
   if (P.wp2n * bmax * P.cert_fac < P.mass_a2 * (r.lo * r.lo * r.lo)) return 2;

@@ -363,7 +363,8 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
   const StageTable& T = RK4 ? c_rk4 : c_vern6;
   __shared__ double lds[LDS_SLOTS * 7 * BLOCK];  // [slot][component][lane]: conflict-free ds_read_b64
   __shared__ unsigned codes[SCAN_WORDS * BLOCK];  // [word][lane]: 2-bit sign codes of the grid scan
-  __shared__ double lastv[BLOCK];                 // value at the last grid point
+  __shared__ double lastv[BLOCK];                 // value at the last grid point (before: b at the step's end)
+  __shared__ double lastt[BLOCK];                 // t at the step's end (the scan certificate)
   __shared__ int srcl[BLOCK];                     // compact list of the wave's scanning lanes
   __shared__ double thgrid[SCAN_WORDS * 16 + 1];  // Θs = j/(npts-1): range(0, 1, length = npts)
   double* const L = lds + threadIdx.x;
@@ -483,7 +484,12 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
       // Every lane evaluates the photon RHS -- idle lanes (a draining wave) on stale state,
       // whose results nothing reads -- so the slot has no divergent control flow. Axion
       // segments (the tree driver's batches) take a wave-uniform detour and a select.
-      rhs_photon(P, y, ty, erg, kk);
+      double aux[2];
+      rhs_photon(P, y, ty, erg, kk, aux);
+      if (s == NSLOT - 1) {  // the end point's b and t for the scan certificate (lastv and codes are free)
+        lastv[threadIdx.x] = aux[0];
+        lastt[threadIdx.x] = aux[1];
+      }
       if (__ballot(!photon) != 0ull) {
         double ka[7];
         rhs_axion(P, y, ty, erg, ka);
@@ -543,13 +549,13 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
           } else {
             lE = log(EEst);
             q11 = exp((7.0 / 60.0) * lE);
-            q = q11 / qpow;
-            q = fmax(0.1, fmin(5.0, q / 0.9));
+            q = q11 * frcp(qpow);
+            q = fmax(0.1, fmin(5.0, q * (1.0 / 0.9)));
           }
           accept = (EEst <= 1.0) || forced;
         }
         if (!accept) {
-          dt = hs / fmin(5.0, q11 / 0.9);
+          dt = hs * frcp(fmin(5.0, q11 * (1.0 / 0.9)));
           ++n_rej;
           if (iter >= P.maxiters) finish = ART_STATUS_MAXITERS;
         } else {
@@ -557,7 +563,7 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
           s_acc += 1;
           if (!RK4) {
             qpow = exp(fmax(lE, -9.210340371976182) * (1.0 / 15.0));  // log(1e-4)
-            dtnext = hs / q;
+            dtnext = hs * frcp(q);
           }
           scan = true;
         }
@@ -575,7 +581,7 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
     //     known without evaluating them; its end value is not needed unless the next step
     //     opens a bracket at its start (then it is recomputed there, bit-identically:
     //     cprev_ok = false).
-    const int ccode = scan ? scan_certified_code(P, u, f, y, kk, hs, tau) : 0;
+    const int ccode = scan ? scan_certified_code(P, u, f, y, kk, hs, lastv[threadIdx.x], lastt[threadIdx.x]) : 0;
     const bool cert = ccode != 0;
     s_cert += cert ? 1u : 0u;
     // every lane parks (u, f, y, kk, h, τ) in its LDS slots (free after the error estimate):

@@ -59,6 +59,8 @@ extern "C" {
 int cc_certified_code(const art_params* p, const double* u0, const double* f0, const double* u1,
                           const double* f1, double h, double tau) {
   KParams K = make_kparams(*p);
-  return scan_certified_code(K, u0, f0, u1, f1, h, tau);
+  double du[7], aux[2];  // b and t at the end point, as the kernel takes them from its last RHS
+  rhs_photon(K, u1, tau + h, 1.0, du, aux);
+  return scan_certified_code(K, u0, f0, u1, f1, h, aux[0], aux[1]);
 }
 }
