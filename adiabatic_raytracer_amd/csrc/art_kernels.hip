@@ -145,6 +145,8 @@ __device__ inline void scan_nd_lds(const KParams& P, const double* S, int stride
   }
   const double h = S[(4 * 7 + 0) * stride], tau = S[(4 * 7 + 1) * stride];
   hermite7(u0, f0, u1, f1, h, th, ui);
+#pragma unroll
+  for (int i = 0; i < 7; ++i) ui[i] = (th == 1.0) ? u1[i] : ui[i];  // the step's end point exactly
   condition_nd(P, ui, exp(tau + th * h), N, D);
 }
 
@@ -707,116 +709,168 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
       post_s = sgn(i_cg);
       dt = dtnext;
     };
+    // the values at the change point (i_cg) and at the bracket start (last_c) are known
+    auto open_bracket = [&]() {
+      lc_ok = true;
+      i_tha = thgrid[last_j];
+      i_ca = last_c;
+      i_thb = thgrid[ip];
+      i_cb = i_cg;
+      i_tr = i_tha - i_ca * (i_thb - i_tha) / (i_cb - i_ca);
+      i_side = 0;
+      i_it = 0;
+      // The interpolant's root only seeds the polish on the true trajectory -- except right
+      // after an event, where DiffEq's repeat_nudge asks whether it lies below θ = 0.01. Only
+      // then is it refined by Illinois on the interpolant (ph 3); otherwise Vern6 starts the
+      // polish from the secant point, which saves the ~6.6 lone-lane Illinois iterations a
+      // bracket would cost the whole wave. (The fixed-step RK4 path keeps the Illinois seed:
+      // with its tiny steps the oracle's own 1-ulp sensitivity is ~1e-12, and a different seed
+      // moves grazing crossings by more.)
+      if (RK4 || (just_evented && i_tha < 0.01)) {
+        ph = 3;
+      } else {
+        open_root(i_tr);
+        ph = 0;
+      }
+    };
+    // walk the codes from grid point ip (no evaluations): ph 5 at a sign change, 7 when the
+    // value at the last nonzero point is still needed, else 0
+    auto walk = [&]() {
+      bool found = false;
+#pragma unroll 1
+      for (; ip <= nper; ++ip) {
+        const int w = (ip - 1) >> 4;
+        const unsigned word = (w == 0) ? cw[0] : (w == 1) ? cw[1] : (w == 2) ? cw[2] : cw[3];
+        const unsigned code = (word >> (2 * ((ip - 1) & 15))) & 3u;
+        if (code == 3u) {  // no resonance possible where |u7| < m_a
+          last_s = 0;
+          continue;
+        }
+        const int si = (code == 1u) ? 1 : (code == 2u ? -1 : 0);
+        if (last_s != 0 && si != 0 && si != last_s) {
+          found = true;
+          break;
+        }
+        if (si != 0) {
+          last_s = si;
+          last_j = ip;
+          lc_ok = false;
+        }
+      }
+      if (found) {
+        ph = 5;
+      } else if (!lc_ok && last_j == nper) {
+        if (!cert) {  // a certified step leaves it to the next step's start (th = 0)
+          last_c = lastv[threadIdx.x];
+          lc_ok = true;
+        }
+        ph = 0;
+      } else if (!lc_ok && last_s != 0) {
+        ph = 7;
+      } else {  // (with no sign remembered the bracket-start value is never read)
+        ph = 0;
+      }
+    };
+    // bracketed polish on the true trajectory (Newton with the interpolant slope, then Illinois)
+    auto polish = [&](double ci) {
+      ++r_it;
+      bool done = !(fabs(ci) > 1e-12);
+      if (!done) {
+        if (sgn(ci) == sgn(r_ca)) { r_tha = r_t; r_ca = ci; if (r_side == -1) r_cb *= 0.5; r_side = -1; }
+        else { r_thb = r_t; r_cb = ci; if (r_side == 1) r_ca *= 0.5; r_side = 1; }
+        done = (r_thb - r_tha) * hroot < 1e-13 || r_it >= 9;
+        if (!done) {
+          double tn = (r_it == 1) ? r_t - ci / r_slope : r_tha - r_ca * (r_thb - r_tha) / (r_cb - r_ca);
+          if (!(tn > r_tha && tn < r_thb)) tn = 0.5 * (r_tha + r_thb);
+          r_t = tn;
+        }
+      }
+      root_done = done;
+      ph = 0;
+    };
+    if (ph == 2) walk();
+    // (c) One cooperative pass evaluates the pending condition values of the whole wave at
+    //     once: the re-stepped end of polishing lanes (ph 1, th = 1 of their parked step), the
+    //     change point of a bracket (ph 5) and its start when unknown, and the step's last
+    //     nonzero grid point (ph 7). Requests (source lane, th) go to LDS and any lane
+    //     evaluates any request, so a lane with two values needs one pass, not two.
+    {
+      const int nq = (ph == 1 || ph == 7) ? 1 : (ph == 5 ? (lc_ok ? 1 : 2) : 0);
+      const unsigned long long lt = (1ull << lane) - 1ull;
+      const unsigned long long b1 = __ballot(nq >= 1), b2 = __ballot(nq == 2);
+      const int total = __popcll(b1) + __popcll(b2);
+      if (total > 0 && total <= 64) {
+        const int off = __popcll(b1 & lt) + __popcll(b2 & lt);
+        wave_lds_sync();  // the walk's lastv reads are done
+        if (nq >= 1) {
+          srcl[wbase + off] = lane;
+          lastv[wbase + off] = (ph == 1) ? 1.0 : (ph == 7 ? thgrid[last_j] : thgrid[ip]);
+        }
+        if (nq == 2) {
+          srcl[wbase + off + 1] = lane;
+          lastv[wbase + off + 1] = thgrid[last_j];
+        }
+        wave_lds_sync();
+        if (lane < total) {
+          const int src = srcl[wbase + lane];
+          lastt[wbase + lane] = scan_point_lds(P, lds + wbase + src, BLOCK, lastv[wbase + lane]);
+        }
+        wave_lds_sync();
+        if (nq >= 1) {
+          const double r1 = lastt[wbase + off];
+          if (ph == 1) {
+            s_root += 1;
+            polish(r1);
+          } else if (ph == 7) {  // value at the step's last nonzero grid point (next step's bracket start)
+            s_interp += 1;
+            last_c = r1;
+            lc_ok = true;
+            ph = 0;
+          } else {  // ph 5
+            s_interp += (unsigned)nq;
+            i_cg = r1;
+            if (nq == 2) last_c = lastt[wbase + off + 1];
+            open_bracket();
+          }
+        }
+      }
+    }
+    // (d) Per lane, for the rare rest: more than 64 pending values, Illinois on the interpolant
+    //     (repeat_nudge), and walking on after an ignored crossing.
+    //     ph: 0 done, 1 re-stepped end (ROOT), 2 walk codes, 3 Illinois, 5 value at the change
+    //     point, 6 value at the bracket start, 7 value at the step's last nonzero point.
 #pragma unroll 1
     while (ph != 0) {
 #ifdef ART_COUNT_LOOPS
       if (lane == __ffsll((long long)__ballot(1)) - 1) s_lane_it += 1;
 #endif
-      if (ph == 2) {  // walk the codes from grid point ip
-        bool found = false;
-#pragma unroll 1
-        for (; ip <= nper; ++ip) {
-          const int w = (ip - 1) >> 4;
-          const unsigned word = (w == 0) ? cw[0] : (w == 1) ? cw[1] : (w == 2) ? cw[2] : cw[3];
-          const unsigned code = (word >> (2 * ((ip - 1) & 15))) & 3u;
-          if (code == 3u) {  // no resonance possible where |u7| < m_a
-            last_s = 0;
-            continue;
-          }
-          const int si = (code == 1u) ? 1 : (code == 2u ? -1 : 0);
-          if (last_s != 0 && si != 0 && si != last_s) {
-            found = true;
-            break;
-          }
-          if (si != 0) {
-            last_s = si;
-            last_j = ip;
-            lc_ok = false;
-          }
-        }
-        if (found) {
-          ph = 5;
-        } else if (!lc_ok && last_j == nper) {
-          if (!cert) {  // a certified step leaves it to the next step's start (th = 0)
-            last_c = lastv[threadIdx.x];
-            lc_ok = true;
-          }
-          ph = 0;
-        } else if (!lc_ok && last_s != 0) {
-          ph = 7;
-        } else {  // (with no sign remembered the bracket-start value is never read)
-          ph = 0;
-        }
+      if (ph == 2) {
+        walk();
         if (ph == 0) break;
       }
-      double th = 0.0;
+      double th = 1.0;  // ph 1: the re-stepped end y at τ + h is the parked step's th = 1
       if (ph == 3) th = i_tr;
       else if (ph == 5) th = thgrid[ip];
       else if (ph == 6 || ph == 7) th = thgrid[last_j];
-      // one condition call site: the fresh state (INIT), the re-stepped end (ROOT) or the
-      // interpolant at th -- the latter exactly as scan_point forms it (bit-identical)
-      double ci;
 #ifdef ART_COUNT_LOOPS
-      s_ph[mode == M_ROOT ? 1 : ph] += 1;
+      s_ph[ph] += 1;
 #endif
-      if (mode == M_ROOT) {  // the re-stepped end y (slot 2) at τ + h
-        double ui[7];
-#pragma unroll
-        for (int i = 0; i < 7; ++i) ui[i] = L[(2 * 7 + i) * BLOCK];
-        ci = condition_t(P, ui, exp(tau + hs));
-      } else {
-        ci = scan_point_lds(P, L, BLOCK, th);
-        s_interp += 1;
-      }
-      if (mode == M_ROOT) {
-        // bracketed polish on the true trajectory (Newton with the interpolant slope, then Illinois)
+      const double ci = scan_point_lds(P, L, BLOCK, th);
+      if (ph == 1) {
         s_root += 1;
-        ++r_it;
-        bool done = !(fabs(ci) > 1e-12);
-        if (!done) {
-          if (sgn(ci) == sgn(r_ca)) { r_tha = r_t; r_ca = ci; if (r_side == -1) r_cb *= 0.5; r_side = -1; }
-          else { r_thb = r_t; r_cb = ci; if (r_side == 1) r_ca *= 0.5; r_side = 1; }
-          done = (r_thb - r_tha) * hroot < 1e-13 || r_it >= 9;
-          if (!done) {
-            double tn = (r_it == 1) ? r_t - ci / r_slope : r_tha - r_ca * (r_thb - r_tha) / (r_cb - r_ca);
-            if (!(tn > r_tha && tn < r_thb)) tn = 0.5 * (r_tha + r_thb);
-            r_t = tn;
-          }
-        }
-        root_done = done;
-        ph = 0;
-      } else if (ph == 7) {  // value at the step's last nonzero grid point (next step's bracket start)
+        polish(ci);
+        continue;
+      }
+      s_interp += 1;
+      if (ph == 7) {
         last_c = ci;
         lc_ok = true;
         ph = 0;
       } else if (ph == 5 || ph == 6) {
         if (ph == 5) i_cg = ci;
         else last_c = ci;
-        if (ph == 5 && !lc_ok) {
-          ph = 6;
-        } else {  // a bracket (θ_last, θ_ip] of the interpolant
-          lc_ok = true;
-          i_tha = thgrid[last_j];
-          i_ca = last_c;
-          i_thb = thgrid[ip];
-          i_cb = i_cg;
-          i_tr = i_tha - i_ca * (i_thb - i_tha) / (i_cb - i_ca);
-          i_side = 0;
-          i_it = 0;
-          // The interpolant's root only seeds the polish on the true trajectory -- except
-          // right after an event, where DiffEq's repeat_nudge asks whether it lies below
-          // θ = 0.01. Only then is it refined by Illinois on the interpolant (ph 3);
-          // otherwise Vern6 starts the polish from the secant point, which saves the ~6.6
-          // lone-lane Illinois iterations a bracket would cost the whole wave. (The fixed-step
-          // RK4 path keeps the Illinois seed: with its tiny steps the oracle's own 1-ulp
-          // sensitivity is ~1e-12, and a different seed moves grazing crossings by more.)
-          if (RK4 || (just_evented && i_tha < 0.01)) {
-            ph = 3;
-          } else {
-            open_root(i_tr);
-            ph = 0;
-          }
-        }
+        if (ph == 5 && !lc_ok) ph = 6;
+        else open_bracket();
       } else {  // ph == 3: Illinois on the interpolant inside (i_tha, i_thb]
         bool stop = ci == 0.0 || isnan(ci) || (i_thb - i_tha) < 1e-12;
         if (!stop) {
