@@ -71,6 +71,79 @@ __host__ __device__ inline double frcp(double x) {
   return 1.0 / x;
 #endif
 }
+// e^x in 19 FMA-pipe instructions (ocml's exp_f64: 34): Cody-Waite reduction by ln 2 with a
+// two-part constant (the first FMA is exact for |k| < 2^11), the degree-13 Taylor polynomial
+// on |r| <= ln2/2 (truncation < 0.05 ulp) and one ldexp. <= 1 ulp for |x| < 708
+// (tests/test_corecheck.py); no overflow/underflow/NaN special-casing beyond what the
+// arithmetic propagates (the integrator's arguments are moderate ln t and ln EEst values).
+__host__ __device__ inline double exp_fma(double x) {
+  const double k = rint(x * 1.4426950408889634);
+  double r = fma(-k, 0.6931471805599453, x);
+  r = fma(-k, 2.3190468138462996e-17, r);
+  double p = 1.0 / 6227020800.0;  // 1/13!
+  p = fma(p, r, 1.0 / 479001600.0);
+  p = fma(p, r, 1.0 / 39916800.0);
+  p = fma(p, r, 1.0 / 3628800.0);
+  p = fma(p, r, 1.0 / 362880.0);
+  p = fma(p, r, 1.0 / 40320.0);
+  p = fma(p, r, 1.0 / 5040.0);
+  p = fma(p, r, 1.0 / 720.0);
+  p = fma(p, r, 1.0 / 120.0);
+  p = fma(p, r, 1.0 / 24.0);
+  p = fma(p, r, 1.0 / 6.0);
+  p = fma(p, r, 0.5);
+  p = fma(p, r, 1.0);
+  p = fma(p, r, 1.0);
+  return ldexp(p, (int)k);
+}
+// ln x for finite x > 0 (the step-size controller's ln EEst): x = m 2^e with m in
+// [√½, √2), ln m = 2 atanh(s), s = (m - 1)/(m + 1), |s| <= 0.1716, odd series to s^21.
+// ~30 instructions against ocml's 105; <= 2 ulp (tests/test_corecheck.py).
+__host__ __device__ inline double log_fma(double x) {
+  int e;
+  double m = frexp(x, &e);  // [0.5, 1)
+  if (m < 0.70710678118654752) { m += m; e -= 1; }
+  const double f = m - 1.0;
+#if defined(__HIP_DEVICE_COMPILE__)
+  const double d = 2.0 + f;
+  double id = __builtin_amdgcn_rcp(d);
+  id = fma(id, fma(-d, id, 1.0), id);
+  id = fma(id, fma(-d, id, 1.0), id);
+  const double s = f * id;
+#else
+  const double s = f / (2.0 + f);
+#endif
+  const double z = s * s;
+  double p = 1.0 / 21.0;
+  p = fma(p, z, 1.0 / 19.0);
+  p = fma(p, z, 1.0 / 17.0);
+  p = fma(p, z, 1.0 / 15.0);
+  p = fma(p, z, 1.0 / 13.0);
+  p = fma(p, z, 1.0 / 11.0);
+  p = fma(p, z, 1.0 / 9.0);
+  p = fma(p, z, 1.0 / 7.0);
+  p = fma(p, z, 1.0 / 5.0);
+  p = fma(p, z, 1.0 / 3.0);
+  // ln m = 2s + 2s z p; e ln2 in two parts so the sum keeps the small terms
+  const double de = (double)e;
+  const double lo = fma(2.0 * s * z, p, de * 2.3190468138462996e-17);
+  return fma(de, 0.6931471805599453, fma(2.0, s, lo));
+}
+// device: exp_fma / log_fma; host (the CPU tests against the oracle): libm
+__host__ __device__ inline double fexp(double x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return exp_fma(x);
+#else
+  return exp(x);
+#endif
+}
+__host__ __device__ inline double flog(double x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return log_fma(x);
+#else
+  return log(x);
+#endif
+}
 __host__ __device__ inline double msin(double x) { return sin(x); }
 __host__ __device__ inline double mcos(double x) { return cos(x); }
 __host__ __device__ inline double macos(double x) { return acos(x); }
@@ -238,7 +311,7 @@ __host__ __device__ inline T layer_wp(const KParams& P, const T& r, double rmax)
 template <class T>
 __host__ __device__ inline void rhs_photon(const KParams& P, const T* u, const T& tau, double erg, T* du,
                                            T* aux = nullptr) {
-  const T t = mexp(tau);
+  const T t = fexp(tau);
   const T r = u[0];
   const T E = -u[6];
   T gtt_u, grr_u;
@@ -332,7 +405,7 @@ __host__ __device__ inline void rhs_photon(const KParams& P, const T* u, const T
 // energy erg, no clamp, no NS cut, du[7] = 0.
 template <class T>
 __host__ __device__ inline void rhs_axion(const KParams& P, const T* u, const T& tau, double erg, T* du) {
-  const T t = mexp(tau);
+  const T t = fexp(tau);
   const T r = u[0];
   T st, ct;
   msincos(u[1], st, ct);
@@ -559,7 +632,7 @@ __host__ __device__ inline int scan_certified_code(const KParams& P, const doubl
 
 template <class T>
 __host__ __device__ inline T condition(const KParams& P, const T* u, const T& tau) {
-  return condition_t(P, u, mexp(tau));
+  return condition_t(P, u, fexp(tau));
 }
 
 // ---------------------------------------------------------------------------

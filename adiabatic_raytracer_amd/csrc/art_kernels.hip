@@ -128,7 +128,7 @@ __device__ inline double scan_point(const KParams& P, const double* u0, const do
   double ui[7];
   hermite7(u0, f0, u1, f1, h, th, ui);
   const double tt = tau + th * h;
-  return condition_t(P, ui, exp(tt));
+  return condition_t(P, ui, fexp(tt));
 }
 
 // scan_point on an interpolant parked in LDS: S = the lane's base in the [slot][component]
@@ -147,7 +147,7 @@ __device__ inline void scan_nd_lds(const KParams& P, const double* S, int stride
   hermite7(u0, f0, u1, f1, h, th, ui);
 #pragma unroll
   for (int i = 0; i < 7; ++i) ui[i] = (th == 1.0) ? u1[i] : ui[i];  // the step's end point exactly
-  condition_nd(P, ui, exp(tau + th * h), N, D);
+  condition_nd(P, ui, fexp(tau + th * h), N, D);
 }
 
 __device__ inline double scan_point_lds(const KParams& P, const double* S, int stride, double th) {
@@ -288,6 +288,7 @@ constexpr int LDS_SLOTS = 5;
 struct StageTable {
   double cf[8], cA[8], cL[8][LDS_SLOTS], ct[8];
   int storeA[8], storeL[8];  // after slot s: kk -> kA? kk -> L[storeL]? (-1: neither)
+  int lmask[8];              // bit q: cL[s][q] != 0 (the LDS slots stage s reads)
   double e_f, e_A, e_L[LDS_SLOTS], e_k;  // error weights (Vern6): btilde of f, kA(=k8), L, k9
 };
 
@@ -308,6 +309,7 @@ __constant__ StageTable c_vern6 = {
     {Vern6::c2, Vern6::c3, Vern6::c4, Vern6::c5, Vern6::c6, Vern6::c7, 1.0, 1.0},
     {1, 0, 0, 0, 0, 0, 1, 0},
     {-1, 0, 1, 2, 3, 4, -1, -1},
+    {0, 0, 0x1, 0x3, 0x7, 0xf, 0x1f, 0x1e},
     Vern6::e1, Vern6::e8, {0.0, Vern6::e4, Vern6::e5, Vern6::e6, Vern6::e7}, Vern6::e9};
 
 __constant__ StageTable c_rk4 = {
@@ -318,6 +320,7 @@ __constant__ StageTable c_rk4 = {
     {0.5, 0.5, 1.0, 1.0, 0, 0, 0, 0},
     {1, 0, 0, 0, 0, 0, 0, 0},
     {-1, 0, 1, -1, -1, -1, -1, -1},
+    {0, 0, 0x1, 0x3, 0, 0, 0, 0},
     0.0, 0.0, {0, 0, 0, 0, 0}, 0.0};
 
 enum LaneMode { M_IDLE = 0, M_STEP = 2, M_ROOT = 3 };
@@ -472,10 +475,14 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
       double acc[7];
 #pragma unroll
       for (int i = 0; i < 7; ++i) acc[i] = cf * f[i] + cA * kA[i];
+      // the LDS slots this stage reads form one contiguous range [qlo, qhi) (lmask): no
+      // per-slot load-compare-branch, and each coefficient load overlaps the slot's LDS reads
+      const int lm = T.lmask[s];
+      if (lm != 0) {
+        const int qhi = 32 - __builtin_clz(lm);
 #pragma unroll 1
-      for (int q = 0; q < LDS_SLOTS; ++q) {
-        const double c = T.cL[s][q];
-        if (c != 0.0) {
+        for (int q = __builtin_ctz(lm); q < qhi; ++q) {
+          const double c = T.cL[s][q];
 #pragma unroll
           for (int i = 0; i < 7; ++i) acc[i] += c * L[(q * 7 + i) * BLOCK];
         }
@@ -509,7 +516,9 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
       }
     }
     // y = u_{n+1}, kk = f(u_{n+1}) for stepping lanes
-    double EEst = 0.0;
+    // EEst² = mean of the 7 squared scaled errors: the controller needs EEst only through
+    // EEst <= 1 and its logarithm (ln EEst = ½ ln EEst²), so no square root is taken
+    double EEst2 = 0.0;
     if (mode == M_STEP || mode == M_ROOT) {
       if (photon && y[0] < P.rNS) y[0] = P.rNS;  // clamp on the FSAL stage (:531)
       if (!RK4) {
@@ -523,7 +532,7 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
           const double q = e * frcp(P.abstol + fmax(fabs(u[i]), fabs(y[i])) * P.reltol);
           acc += q * q;
         }
-        EEst = sqrt(acc / 7.0);
+        EEst2 = acc * (1.0 / 7.0);
       }
     }
 
@@ -534,27 +543,29 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
     if (mode == M_STEP) {
       s_att += 1;
       ++iter;
-      bool finite = !isnan(EEst) && !isinf(EEst);
+      bool finite = !isnan(EEst2) && !isinf(EEst2);
 #pragma unroll
       for (int i = 0; i < 7; ++i) finite = finite && !isnan(y[i]) && !isinf(y[i]);
       if (!finite) {
         finish = ART_STATUS_NONFINITE;
       } else {
         // PI controller (OrdinaryDiffEq: beta1 = 7/60, beta2 = 1/15, gamma = 0.9, qmin = 0.2, qmax = 10)
-        // (EEst^(7/60) and max(EEst, 1e-4)^(1/15) from one logarithm; OrdinaryDiffEq itself
-        // uses FastPower.fastpower, an exp2/log2 approximation)
-        double q = 1.0, q11 = 1.0, lE = -INFINITY;
+        // EEst^(7/60) and max(EEst, 1e-4)^(1/15) are the 7th and 4th powers of y = EEst^(1/60)
+        // = (EEst²)^(1/120): one logarithm and one exponential (OrdinaryDiffEq itself uses
+        // FastPower.fastpower, an exp2/log2 approximation)
+        double q = 1.0, q11 = 1.0, y60 = 0.0;
         bool accept = true;
         if (!RK4) {
-          if (EEst == 0.0) {
+          if (EEst2 == 0.0) {
             q = 0.1;
           } else {
-            lE = log(EEst);
-            q11 = exp((7.0 / 60.0) * lE);
+            y60 = fexp(flog(EEst2) * (1.0 / 120.0));
+            const double y2 = y60 * y60;
+            q11 = (y2 * y2) * (y2 * y60);
             q = q11 * frcp(qpow);
             q = fmax(0.1, fmin(5.0, q * (1.0 / 0.9)));
           }
-          accept = (EEst <= 1.0) || forced;
+          accept = (EEst2 <= 1.0) || forced;
         }
         if (!accept) {
           dt = hs * frcp(fmin(5.0, q11 * (1.0 / 0.9)));
@@ -564,7 +575,8 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
           ++n_acc;
           s_acc += 1;
           if (!RK4) {
-            qpow = exp(fmax(lE, -9.210340371976182) * (1.0 / 15.0));  // log(1e-4)
+            const double ym = fmax(y60, 0.8576958985908941);  // (1e-4)^(1/60)
+            qpow = (ym * ym) * (ym * ym);
             dtnext = hs * frcp(q);
           }
           scan = true;
@@ -997,9 +1009,8 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
 // crowd. Out: in.u0 = 16n doubles [u0 (7) | f0 (7) | dt | c0].
 __global__ __launch_bounds__(256) void init_kernel(const KParams P, const int64_t n, const SegIn in,
                                                    unsigned long long* __restrict__ stats) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  unsigned nrhs = 0;
-  if (i < n) {
+  unsigned nrhs = 0;  // grid-stride over the rays: one stats atomic per wave
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const double xs[3] = {in.x0[i], in.x0[n + i], in.x0[2 * n + i]};
     const double ks[3] = {in.k0[i], in.k0[n + i], in.k0[2 * n + i]};
     const double erg = in.erg[i], tau = in.lnt0[i];
@@ -1007,7 +1018,7 @@ __global__ __launch_bounds__(256) void init_kernel(const KParams P, const int64_
     double u[7], f[7];
     initial_state(P, xs, ks, erg, in.dw[i], u);
     rhs(P, photon, u, tau, erg, f);
-    nrhs = 1;
+    nrhs += 1;
     if (photon && u[0] < P.rNS) u[0] = P.rNS;  // hamiltonian's in-place clamp (:531)
     double dt;
     if (P.integrator == ART_RK4) {
@@ -1017,7 +1028,7 @@ __global__ __launch_bounds__(256) void init_kernel(const KParams P, const int64_
       dt = initdt(P, photon, erg, u, f, tau, P.ln_t_end - tau, probe);
       nrhs += probe;
     }
-    const double c0 = condition_t(P, u, exp(tau));
+    const double c0 = condition_t(P, u, fexp(tau));
 #pragma unroll
     for (int c = 0; c < 7; ++c) {
       in.u0[c * n + i] = u[c];
@@ -1369,8 +1380,9 @@ int persistent_blocks(const void* func, int64_t work) {
 hipError_t launch_propagate(const KParams& P, int64_t n, const SegIn& in, const SegOut& out, int32_t max_crossings,
                             unsigned long long* queue, unsigned long long* stats, hipStream_t s, int* grid_out,
                             hipEvent_t ev0, hipEvent_t ev1) {
+  const int64_t gr = (n + 255) / 256;
   const unsigned g1 = (unsigned)((n + 255) / 256);
-  hipLaunchKernelGGL(init_kernel, dim3(g1), dim3(256), 0, s, P, n, in, stats);
+  hipLaunchKernelGGL(init_kernel, dim3((unsigned)(gr < 2048 ? gr : 2048)), dim3(256), 0, s, P, n, in, stats);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   const bool flat = P.rs_eff == 0.0 && !(P.bndry_lyr > 0.0) && !P.isotropic;

@@ -30,6 +30,26 @@ def test_sincos_within_one_ulp():
     assert np.max(np.abs(c - rc) / uc) <= 1.0
 
 
+def test_exp_fma_within_one_ulp():
+    """exp_fma (the device's e^x for ln t and the controller) against libm."""
+    rng = np.random.default_rng(1)
+    x = np.concatenate([rng.uniform(-700, 700, 200000), rng.uniform(-30, 5, 200000),
+                        rng.uniform(-1e-3, 1e-3, 20000), np.linspace(-2, 2, 10001), [0.0, -0.0]])
+    y, ref = cc.exp_fma(x), np.exp(x)
+    assert np.max(np.abs(y - ref) / np.spacing(ref)) <= 1.0
+
+
+def test_log_fma_within_two_ulp():
+    """log_fma (the controller's ln EEst²) against libm, normals and subnormals."""
+    rng = np.random.default_rng(2)
+    x = np.concatenate([10.0 ** rng.uniform(-300, 300, 200000), rng.uniform(0.5, 2.0, 200000),
+                        1.0 + rng.uniform(-1e-6, 1e-6, 20000), [1.0, 2.0, 0.5, 5e-324, 1e-310]])
+    y, ref = cc.log_fma(x), np.log(x)
+    err = np.abs(y - ref) / np.spacing(np.maximum(np.abs(ref), 1e-300))
+    assert np.max(err[ref != 0]) <= 2.0
+    assert cc.log_fma(np.array([1.0]))[0] == 0.0
+
+
 @pytest.mark.parametrize("cfg", sorted(CONFIGS))
 @pytest.mark.parametrize("species", [1, 0])
 @pytest.mark.parametrize("b0sign", [1.0, -1.0])  # main_runner_tree backtraces with -B0 (:585)

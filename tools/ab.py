@@ -1,5 +1,6 @@
-"""Dev A/B timing of the propagate kernel for the library named by ART_LIB: 1e6-ray
-batches of the flat (configs[1]) and GR (configs[3]) workloads. One JSON line per config."""
+"""Dev A/B timing of the propagate kernel for the library named by ART_LIB: 1e6-ray (argv[1])
+batches of the flat (configs[1]) and GR (configs[3]) workloads (argv[2]: only one of them).
+One JSON line per config; kernel_ms is the best of the timed launches after the first."""
 import json
 import os
 import sys
@@ -9,7 +10,10 @@ import adiabatic_raytracer_amd as A  # noqa: E402
 from adiabatic_raytracer_amd import Engine  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 1_000_000
+only = sys.argv[2] if len(sys.argv) > 2 else None  # "flat" or "gr"
 for name, kw in (("flat", dict(theta_m=0.2, mass_a=1e-5, flat=True)), ("gr", dict(theta_m=0.0, mass_a=1e-6, flat=False))):
+    if only and name != only:
+        continue
     eng = Engine(A.Params(**kw))
     inp = eng.forward_roots(n, seed=1769)
     out = eng.alloc_out(n)
@@ -17,6 +21,7 @@ for name, kw in (("flat", dict(theta_m=0.2, mass_a=1e-5, flat=True)), ("gr", dic
     for _ in range(3 if name == "flat" else 2):
         eng.propagate(inp, out)
         ms.append(eng.kernel_ms())
+    ms[-1] = min(ms[1:])
     st = A.raytracer.last_stats()
     att = (out["n_accept"] + out["n_reject"]).max().item()
     print(json.dumps({"lib": os.environ.get("ART_LIB", "default"), "config": name, "kernel_ms": ms[-1],

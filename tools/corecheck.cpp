@@ -47,6 +47,12 @@ void cc_philox(const uint32_t* ctr, const uint32_t* key, uint32_t* out) {
 void cc_sincos(const double* x, int64_t n, double* s, double* c) {
   for (int64_t i = 0; i < n; ++i) msincos(x[i], s[i], c[i]);
 }
+void cc_exp_fma(const double* x, int64_t n, double* y) {
+  for (int64_t i = 0; i < n; ++i) y[i] = exp_fma(x[i]);
+}
+void cc_log_fma(const double* x, int64_t n, double* y) {
+  for (int64_t i = 0; i < n; ++i) y[i] = log_fma(x[i]);
+}
 void cc_metric_d(double r, double rs, double* out) {
   double gtt, grr, dgtt, dgrr;
   metric_tr_d(r, rs, gtt, grr, dgtt, dgrr);

@@ -98,6 +98,20 @@ def sincos(x):
     return s, c
 
 
+def exp_fma(x):
+    x = np.ascontiguousarray(x, np.float64)
+    y = np.zeros_like(x)
+    lib().cc_exp_fma(P(x), C.c_int64(x.size), P(y))
+    return y
+
+
+def log_fma(x):
+    x = np.ascontiguousarray(x, np.float64)
+    y = np.zeros_like(x)
+    lib().cc_log_fma(P(x), C.c_int64(x.size), P(y))
+    return y
+
+
 def metric_d(r, rs):
     o = np.zeros(4)
     lib().cc_metric_d(C.c_double(r), C.c_double(rs), P(o))

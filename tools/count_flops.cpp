@@ -39,6 +39,7 @@ inline bool operator<(OC a, OC b) { return a.v < b.v; }
 inline OC msqrt(OC x) { ++OC::n; return OC(sqrt(x.v)); }
 inline OC frcp(OC x) { ++OC::n; return OC(1.0 / x.v); }
 inline OC mexp(OC x) { ++OC::n; return OC(exp(x.v)); }
+inline OC fexp(OC x) { ++OC::n; return OC(exp(x.v)); }
 inline OC mabs(OC x) { return OC(fabs(x.v)); }
 inline OC msign(OC x) { return OC(copysign(1.0, x.v)); }
 inline void msincos(OC x, OC& s, OC& c) { OC::n += 2; s = OC(sin(x.v)); c = OC(cos(x.v)); }
