@@ -285,18 +285,32 @@ __device__ inline int affect(const KParams& P, const SegIn& in, const SegOut& ou
 // overlap) and L_0..L_4 are stage vectors parked in LDS (k3..k7 for Vern6; k3, k4 for RK4).
 // Coefficients are wave-uniform scalar loads; the RHS is inlined once.
 constexpr int LDS_SLOTS = 5;
+// The wave-uniform scalars of one slot in one 48-byte row: a single scalar load and wait at
+// the slot's start (the cL coefficients are loaded inside the LDS loop, where their latency
+// overlaps the LDS reads).
+struct alignas(16) SlotRow {
+  double cf, cA, ct;
+  int lmask;   // bit q: cL[s][q] != 0 -- the LDS slots stage s reads, one contiguous range
+  int storeA;  // after the slot: kk -> kA?
+  int storeL;  // after the slot: kk -> L[storeL] (-1: no)
+  int pad;
+};
 struct StageTable {
-  double cf[8], cA[8], cL[8][LDS_SLOTS], ct[8];
-  int storeA[8], storeL[8];  // after slot s: kk -> kA? kk -> L[storeL]? (-1: neither)
-  int lmask[8];              // bit q: cL[s][q] != 0 (the LDS slots stage s reads)
+  SlotRow row[8];
+  double cL[8][LDS_SLOTS];
   double e_f, e_A, e_L[LDS_SLOTS], e_k;  // error weights (Vern6): btilde of f, kA(=k8), L, k9
 };
 
 __constant__ StageTable c_vern6 = {
-    // cf: a_{s+2,1}
-    {Vern6::a21, Vern6::a31, Vern6::a41, Vern6::a51, Vern6::a61, Vern6::a71, Vern6::a81, Vern6::a91},
-    // cA: coefficient of kA (k2 for slots 0..6, k8 for slot 7)
-    {0.0, Vern6::a32, 0.0, 0.0, 0.0, 0.0, 0.0, Vern6::a98},
+    // {cf = a_{s+2,1}, cA (k2 for slots 0..6, k8 for slot 7), ct, lmask, storeA, storeL}
+    {{Vern6::a21, 0.0, Vern6::c2, 0x0, 1, -1, 0},
+     {Vern6::a31, Vern6::a32, Vern6::c3, 0x0, 0, 0, 0},
+     {Vern6::a41, 0.0, Vern6::c4, 0x1, 0, 1, 0},
+     {Vern6::a51, 0.0, Vern6::c5, 0x3, 0, 2, 0},
+     {Vern6::a61, 0.0, Vern6::c6, 0x7, 0, 3, 0},
+     {Vern6::a71, 0.0, Vern6::c7, 0xf, 0, 4, 0},
+     {Vern6::a81, 0.0, 1.0, 0x1f, 1, -1, 0},
+     {Vern6::a91, Vern6::a98, 1.0, 0x1e, 0, -1, 0}},
     // cL: coefficients of k3..k7
     {{0, 0, 0, 0, 0},
      {0, 0, 0, 0, 0},
@@ -306,21 +320,16 @@ __constant__ StageTable c_vern6 = {
      {Vern6::a73, Vern6::a74, Vern6::a75, Vern6::a76, 0},
      {Vern6::a83, Vern6::a84, Vern6::a85, Vern6::a86, Vern6::a87},
      {0, Vern6::a94, Vern6::a95, Vern6::a96, Vern6::a97}},
-    {Vern6::c2, Vern6::c3, Vern6::c4, Vern6::c5, Vern6::c6, Vern6::c7, 1.0, 1.0},
-    {1, 0, 0, 0, 0, 0, 1, 0},
-    {-1, 0, 1, 2, 3, 4, -1, -1},
-    {0, 0, 0x1, 0x3, 0x7, 0xf, 0x1f, 0x1e},
     Vern6::e1, Vern6::e8, {0.0, Vern6::e4, Vern6::e5, Vern6::e6, Vern6::e7}, Vern6::e9};
 
 __constant__ StageTable c_rk4 = {
-    {0.5, 0.0, 0.0, 1.0 / 6.0, 0, 0, 0, 0},
-    {0.0, 0.5, 0.0, 2.0 / 6.0, 0, 0, 0, 0},
+    {{0.5, 0.0, 0.5, 0x0, 1, -1, 0},
+     {0.0, 0.5, 0.5, 0x0, 0, 0, 0},
+     {0.0, 0.0, 1.0, 0x1, 0, 1, 0},
+     {1.0 / 6.0, 2.0 / 6.0, 1.0, 0x3, 0, -1, 0},
+     {0, 0, 0, 0, 0, -1, 0}, {0, 0, 0, 0, 0, -1, 0}, {0, 0, 0, 0, 0, -1, 0}, {0, 0, 0, 0, 0, -1, 0}},
     {{0, 0, 0, 0, 0}, {0, 0, 0, 0, 0}, {1.0, 0, 0, 0, 0}, {2.0 / 6.0, 1.0 / 6.0, 0, 0, 0},
      {0, 0, 0, 0, 0}, {0, 0, 0, 0, 0}, {0, 0, 0, 0, 0}, {0, 0, 0, 0, 0}},
-    {0.5, 0.5, 1.0, 1.0, 0, 0, 0, 0},
-    {1, 0, 0, 0, 0, 0, 0, 0},
-    {-1, 0, 1, -1, -1, -1, -1, -1},
-    {0, 0, 0x1, 0x3, 0, 0, 0, 0},
     0.0, 0.0, {0, 0, 0, 0, 0}, 0.0};
 
 enum LaneMode { M_IDLE = 0, M_STEP = 2, M_ROOT = 3 };
@@ -471,13 +480,14 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
     for (int i = 0; i < 7; ++i) kA[i] = 0.0;  // read (times a zero coefficient) before its first store
 #pragma unroll 1
     for (int s = 0; s < NSLOT; ++s) {
-      const double cf = T.cf[s], cA = T.cA[s];
+      const SlotRow R = T.row[s];
+      const double cf = R.cf, cA = R.cA;
       double acc[7];
 #pragma unroll
       for (int i = 0; i < 7; ++i) acc[i] = cf * f[i] + cA * kA[i];
       // the LDS slots this stage reads form one contiguous range [qlo, qhi) (lmask): no
       // per-slot load-compare-branch, and each coefficient load overlaps the slot's LDS reads
-      const int lm = T.lmask[s];
+      const int lm = R.lmask;
       if (lm != 0) {
         const int qhi = 32 - __builtin_clz(lm);
 #pragma unroll 1
@@ -489,7 +499,7 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
       }
 #pragma unroll
       for (int i = 0; i < 7; ++i) y[i] = u[i] + hs * acc[i];
-      const double ty = tau + T.ct[s] * hs;
+      const double ty = tau + R.ct * hs;
       // Every lane evaluates the photon RHS -- idle lanes (a draining wave) on stale state,
       // whose results nothing reads -- so the slot has no divergent control flow. Axion
       // segments (the tree driver's batches) take a wave-uniform detour and a select.
@@ -505,11 +515,11 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
 #pragma unroll
         for (int i = 0; i < 7; ++i) kk[i] = photon ? kk[i] : ka[i];
       }
-      if (T.storeA[s]) {
+      if (R.storeA) {
 #pragma unroll
         for (int i = 0; i < 7; ++i) kA[i] = kk[i];
       }
-      const int sl = T.storeL[s];
+      const int sl = R.storeL;
       if (sl >= 0) {
 #pragma unroll
         for (int i = 0; i < 7; ++i) L[(sl * 7 + i) * BLOCK] = kk[i];
