@@ -636,6 +636,112 @@ __host__ __device__ inline T condition(const KParams& P, const T* u, const T& ta
 }
 
 // ---------------------------------------------------------------------------
+// The ContinuousCallback's sign walk over one step's grid codes (DiffEqBase's sequential
+// scan of interp_points values, RayTracer.jl:357-358): 2-bit codes (0 zero, 1 positive,
+// 2 negative, 3 NaN) of points 1..nper, 16 per word. A NaN resets the remembered sign; a
+// nonzero point of the other sign than the remembered one is a change. State: the next
+// point ip, the remembered sign last_s, the last nonzero point last_j, and lc_ok (the value
+// at last_j is known: cleared by every nonzero point passed).
+struct WalkState {
+  int ip, last_s, last_j;
+  bool lc_ok;
+};
+
+// The sequential reference form.
+__host__ __device__ inline void walk_codes_loop(const unsigned cw[4], int nper, WalkState& st, bool& found) {
+  found = false;
+  for (; st.ip <= nper; ++st.ip) {
+    const unsigned code = (cw[(st.ip - 1) >> 4] >> (2 * ((st.ip - 1) & 15))) & 3u;
+    if (code == 3u) {
+      st.last_s = 0;
+      continue;
+    }
+    const int si = (code == 1u) ? 1 : (code == 2u ? -1 : 0);
+    if (st.last_s != 0 && si != 0 && si != st.last_s) {
+      found = true;
+      return;
+    }
+    if (si != 0) {
+      st.last_s = si;
+      st.last_j = st.ip;
+      st.lc_ok = false;
+    }
+  }
+}
+
+// Bit-parallel form for the usual case, no exact-zero code from ip on: every remaining
+// point is then positive, negative or NaN, its predecessor is the point before it (at ip:
+// the remembered sign), and a change is a P after an N or an N after a P. 32 points per
+// 64-bit word (bit 2(p-1) of word 0 for p <= 32, bit 2(p-33) of word 1 above). Returns
+// false, with st untouched, when a zero code needs the sequential form; otherwise leaves
+// exactly the state walk_codes_loop would (tests/test_walk_codes.py). nper <= 64.
+__host__ __device__ inline bool walk_codes_bits(const unsigned cw[4], int nper, WalkState& st, bool& found) {
+  constexpr unsigned long long M = 0x5555555555555555ull;
+  const int ip = st.ip;
+  if (ip > nper) {
+    found = false;
+    return true;
+  }
+  const unsigned long long c[2] = {(unsigned long long)cw[0] | ((unsigned long long)cw[1] << 32),
+                                   (unsigned long long)cw[2] | ((unsigned long long)cw[3] << 32)};
+  unsigned long long Pm[2], Nm[2], R[2];
+  unsigned long long zero = 0ull;
+  for (int k = 0; k < 2; ++k) {
+    int a = ip - 1 - 32 * k, b = nper - 1 - 32 * k;  // the range ip..nper in chunk positions
+    a = a < 0 ? 0 : a;
+    b = b > 31 ? 31 : b;
+    unsigned long long r = 0ull;
+    if (a <= b) {
+      const unsigned long long hi = (b == 31) ? ~0ull : ((1ull << (2 * b + 2)) - 1ull);
+      r = hi & ~((1ull << (2 * a)) - 1ull) & M;
+    }
+    R[k] = r;
+    const unsigned long long x = c[k], xs = c[k] >> 1;
+    Pm[k] = x & ~xs & M;
+    Nm[k] = xs & ~x & M;
+    zero |= ~(x | xs) & M & r;
+  }
+  if (zero != 0ull) return false;
+  const int q = ip - 1;
+  const unsigned long long ib0 = (q < 32) ? (1ull << (2 * q)) : 0ull;
+  const unsigned long long ib1 = (q >= 32) ? (1ull << (2 * (q - 32))) : 0ull;
+  const unsigned long long sP = st.last_s > 0 ? ~0ull : 0ull, sN = st.last_s < 0 ? ~0ull : 0ull;
+  const unsigned long long Pp0 = ((Pm[0] << 2) & ~ib0) | (ib0 & sP);
+  const unsigned long long Np0 = ((Nm[0] << 2) & ~ib0) | (ib0 & sN);
+  const unsigned long long Pp1 = (((Pm[1] << 2) | (Pm[0] >> 62)) & ~ib1) | (ib1 & sP);
+  const unsigned long long Np1 = (((Nm[1] << 2) | (Nm[0] >> 62)) & ~ib1) | (ib1 & sN);
+  const unsigned long long T0 = R[0] & ((Pm[0] & Np0) | (Nm[0] & Pp0));
+  const unsigned long long T1 = R[1] & ((Pm[1] & Np1) | (Nm[1] & Pp1));
+  if ((T0 | T1) != 0ull) {
+    const int j = T0 ? 1 + (__builtin_ctzll(T0) >> 1) : 33 + (__builtin_ctzll(T1) >> 1);
+    const bool jp = T0 ? ((Pm[0] >> (2 * (j - 1))) & 1ull) : ((Pm[1] >> (2 * (j - 33))) & 1ull);
+    if (j > ip) {  // the point before j is nonzero, of the other sign
+      st.last_j = j - 1;
+      st.lc_ok = false;
+    }
+    st.last_s = jp ? -1 : 1;
+    st.ip = j;
+    found = true;
+    return true;
+  }
+  const unsigned long long g0 = (Pm[0] | Nm[0]) & R[0], g1 = (Pm[1] | Nm[1]) & R[1];
+  if (g1) {
+    st.last_j = 33 + ((63 - __builtin_clzll(g1)) >> 1);
+    st.lc_ok = false;
+  } else if (g0) {
+    st.last_j = 1 + ((63 - __builtin_clzll(g0)) >> 1);
+    st.lc_ok = false;
+  }
+  // the sign remembered after the last point: its own (no zeros), none after a NaN
+  const int e = nper - 1;
+  const unsigned code = (unsigned)(((e < 32) ? (c[0] >> (2 * e)) : (c[1] >> (2 * (e - 32)))) & 3ull);
+  st.last_s = (code == 1u) ? 1 : (code == 2u ? -1 : 0);
+  st.ip = nper + 1;
+  found = false;
+  return true;
+}
+
+// ---------------------------------------------------------------------------
 // Cartesian -> (r, θ, φ) and the covariant "celerity" of k (RayTracer.jl:193-212,
 // k_norm_Cart :656-664, k_sphere :995-1007).
 template <class T>

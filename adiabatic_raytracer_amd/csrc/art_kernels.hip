@@ -407,6 +407,19 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
   int save_k = 1;  // SAVE: the next interior saveat index
   bool exhausted = false;
   unsigned s_att = 0, s_acc = 0, s_root = 0, s_scan = 0, s_interp = 0, s_rays = 0, s_cert = 0;
+#ifdef ART_SECTION_TIMING
+  // dev build: s_memtime cycles per main-loop section, summed over the wave's iterations
+  unsigned long long t_sec[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long t_last = __builtin_amdgcn_s_memtime();
+#define ART_TMARK(k)                                                  \
+  {                                                                   \
+    const unsigned long long t_now_ = __builtin_amdgcn_s_memtime();   \
+    t_sec[k] += t_now_ - t_last;                                      \
+    t_last = t_now_;                                                  \
+  }
+#else
+#define ART_TMARK(k)
+#endif
 #ifdef ART_COUNT_LOOPS
   unsigned s_lane_it = 0, s_main_it = 0;  // dev counters: wave iterations of the per-lane and main loops
   unsigned s_ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // per-lane evaluations by phase
@@ -459,6 +472,7 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
       }
     }
     if (__ballot(mode != M_IDLE) == 0ull) break;  // every lane idle and the queue drained
+    ART_TMARK(0)  // refill
 #ifdef ART_COUNT_LOOPS
     if (lane == 0) s_main_it += 1;
 #endif
@@ -525,6 +539,7 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
         for (int i = 0; i < 7; ++i) L[(sl * 7 + i) * BLOCK] = kk[i];
       }
     }
+    ART_TMARK(1)  // step size and stage slots
     // y = u_{n+1}, kk = f(u_{n+1}) for stepping lanes
     // EEst² = mean of the 7 squared scaled errors: the controller needs EEst only through
     // EEst <= 1 and its logarithm (ln EEst = ½ ln EEst²), so no square root is taken
@@ -622,6 +637,7 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
     L[(4 * 7 + 1) * BLOCK] = tau;
     const bool grid = scan && !cert;
     const unsigned long long smask = __ballot(grid);
+    ART_TMARK(2)  // error norm, controller, certificate and parking
     if (smask != 0ull) {
       const int ns = __popcll(smask);
       if (grid) {
@@ -661,6 +677,7 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
       wave_lds_sync();
     }
 
+    ART_TMARK(3)  // grid pass
     // (b) Per lane: walk the sign codes exactly as the sequential scan would (NaN resets the
     //     sign memory; a sign change opens an Illinois search on the interpolant, ignored
     //     right after an event -- DiffEq repeat_nudge), plus the single evaluations of fresh
@@ -758,27 +775,13 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
     // walk the codes from grid point ip (no evaluations): ph 5 at a sign change, 7 when the
     // value at the last nonzero point is still needed, else 0
     auto walk = [&]() {
+      WalkState ws{ip, last_s, last_j, lc_ok};
       bool found = false;
-#pragma unroll 1
-      for (; ip <= nper; ++ip) {
-        const int w = (ip - 1) >> 4;
-        const unsigned word = (w == 0) ? cw[0] : (w == 1) ? cw[1] : (w == 2) ? cw[2] : cw[3];
-        const unsigned code = (word >> (2 * ((ip - 1) & 15))) & 3u;
-        if (code == 3u) {  // no resonance possible where |u7| < m_a
-          last_s = 0;
-          continue;
-        }
-        const int si = (code == 1u) ? 1 : (code == 2u ? -1 : 0);
-        if (last_s != 0 && si != 0 && si != last_s) {
-          found = true;
-          break;
-        }
-        if (si != 0) {
-          last_s = si;
-          last_j = ip;
-          lc_ok = false;
-        }
-      }
+      if (!walk_codes_bits(cw, nper, ws, found)) walk_codes_loop(cw, nper, ws, found);
+      ip = ws.ip;
+      last_s = ws.last_s;
+      last_j = ws.last_j;
+      lc_ok = ws.lc_ok;
       if (found) {
         ph = 5;
       } else if (!lc_ok && last_j == nper) {
@@ -810,7 +813,9 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
       root_done = done;
       ph = 0;
     };
+    ART_TMARK(4)  // sign-code fast paths
     if (ph == 2) walk();
+    ART_TMARK(5)  // code walk
     // (c) One cooperative pass evaluates the pending condition values of the whole wave at
     //     once: the re-stepped end of polishing lanes (ph 1, th = 1 of their parked step), the
     //     change point of a bracket (ph 5) and its start when unknown, and the step's last
@@ -857,6 +862,7 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
         }
       }
     }
+    ART_TMARK(6)  // cooperative pass
     // (d) Per lane, for the rare rest: more than 64 pending values, Illinois on the interpolant
     //     (repeat_nudge), and walking on after an ignored crossing.
     //     ph: 0 done, 1 re-stepped end (ROOT), 2 walk codes, 3 Illinois, 5 value at the change
@@ -919,6 +925,7 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
         }
       }
     }
+    ART_TMARK(7)  // per-lane fallback loop
     if constexpr (SAVE) {
       // saveat (RayTracer.jl:176, 383): the interior save times ln t0 + kΔ that this completed
       // step passed -- an accepted step without a crossing, or the polish step that ends at a
@@ -994,10 +1001,17 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
       ray = -1;
       mode = M_IDLE;
     }
+    ART_TMARK(0)  // saveat, reload, events, finish and the output stores (+ refill)
   }
 
   // wave-reduce the statistics and add them once per wave
-#ifdef ART_COUNT_LOOPS
+#if defined(ART_SECTION_TIMING)
+  if (lane == 0) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) atomicAdd(&stats[k], t_sec[k]);
+  }
+#else
+#if defined(ART_COUNT_LOOPS)
   const unsigned v[7] = {s_main_it, s_lane_it, s_ph[1], s_ph[3], s_ph[5], s_ph[6], s_ph[7]};
 #else
   const unsigned v[7] = {s_att, s_acc, s_root, s_scan, s_interp, s_rays, s_cert};
@@ -1009,6 +1023,7 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
     for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off);
     if (lane == 0 && x) atomicAdd(&stats[slot[k]], x);
   }
+#endif
 }
 
 // Fresh state of every segment, one thread per ray: u0 (RayTracer.jl:179-216: k_norm_Cart

@@ -47,6 +47,19 @@ void cc_philox(const uint32_t* ctr, const uint32_t* key, uint32_t* out) {
 void cc_sincos(const double* x, int64_t n, double* s, double* c) {
   for (int64_t i = 0; i < n; ++i) msincos(x[i], s[i], c[i]);
 }
+// walk_codes_loop / walk_codes_bits (art_core.h); st = {ip, last_s, last_j, lc_ok} in/out.
+// Returns found (0/1), or -1 when the bit-parallel form declines (a zero code).
+int cc_walk(const unsigned* cw, int nper, int* st, int bits) {
+  WalkState w{st[0], st[1], st[2], st[3] != 0};
+  bool found = false;
+  if (bits) {
+    if (!walk_codes_bits(cw, nper, w, found)) return -1;
+  } else {
+    walk_codes_loop(cw, nper, w, found);
+  }
+  st[0] = w.ip; st[1] = w.last_s; st[2] = w.last_j; st[3] = w.lc_ok ? 1 : 0;
+  return found ? 1 : 0;
+}
 void cc_exp_fma(const double* x, int64_t n, double* y) {
   for (int64_t i = 0; i < n; ++i) y[i] = exp_fma(x[i]);
 }

@@ -98,6 +98,14 @@ def sincos(x):
     return s, c
 
 
+def walk(cw, nper, st, bits):
+    """(found or -1, [ip, last_s, last_j, lc_ok]) of walk_codes_bits (bits) or walk_codes_loop."""
+    c = (C.c_uint * 4)(*[int(v) & 0xFFFFFFFF for v in cw])
+    s = (C.c_int * 4)(*st)
+    r = lib().cc_walk(c, C.c_int(nper), s, C.c_int(1 if bits else 0))
+    return r, list(s)
+
+
 def exp_fma(x):
     x = np.ascontiguousarray(x, np.float64)
     y = np.zeros_like(x)
