@@ -948,19 +948,20 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
         }
       }
     }
+    // reload the state each lane continues from: the step's end (y, kk: slots 2-3) after an
+    // accepted step or a finished polish, else its start (u, f: slots 0-1)
+    {
+      const double* Ls = L + ((root_done || (scan && !hit)) ? 2 * 7 * BLOCK : 0);
 #pragma unroll
-    for (int i = 0; i < 7; ++i) {
-      u[i] = L[(0 * 7 + i) * BLOCK];
-      f[i] = L[(1 * 7 + i) * BLOCK];
-      y[i] = L[(2 * 7 + i) * BLOCK];
-      kk[i] = L[(3 * 7 + i) * BLOCK];
+      for (int i = 0; i < 7; ++i) {
+        u[i] = Ls[i * BLOCK];
+        f[i] = Ls[(7 + i) * BLOCK];
+      }
     }
     if (hit) mode = M_ROOT;
     if (root_done) {
       const double tau_r = tau + hs;
-      const int a = affect(P, in, out, n, ray, y, tau_r, erg, ncross, max_crossings);
-#pragma unroll
-      for (int i = 0; i < 7; ++i) { u[i] = y[i]; f[i] = kk[i]; }
+      const int a = affect(P, in, out, n, ray, u, tau_r, erg, ncross, max_crossings);
       tau = tau_r;
       cprev = post_c;  // the post-event side (DiffEq repeat_nudge): the root is not re-found
       cprev_ok = true;
@@ -972,8 +973,6 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
       else if (iter >= P.maxiters) finish = ART_STATUS_MAXITERS;
     }
     if (scan && !hit) {
-#pragma unroll
-      for (int i = 0; i < 7; ++i) { u[i] = y[i]; f[i] = kk[i]; }
       tau = last ? tend : tau + hs;
       cprev = last_c;
       cprev_ok = lc_ok;
