@@ -122,6 +122,8 @@ int propagate_device_impl(const art_params* p, int64_t n, const double* x0, cons
     if (e[0] == '0') K.cert_fac = __builtin_inf();
   void* u0 = nullptr;  // 16n doubles of fresh state: u0, f0, dt, c0 (init_kernel -> the integrator)
   if ((rc = pool_get(c, 6, (size_t)n * 16 * sizeof(double), &u0))) return rc;
+  void* rec = nullptr;  // END_REC n doubles: the integrator's AoS end records (-> finalize_kernel)
+  if ((rc = pool_get(c, 9, (size_t)n * art::END_REC * sizeof(double), &rec))) return rc;
   art::SegIn in{x0, k0, erg, dw, ln_t0, species, (double*)u0};
   art::SegOut so{out->x_end, out->k_end, out->u7_end, out->tau_end, out->status, out->n_accept, out->n_reject,
                  0, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
@@ -131,6 +133,9 @@ int propagate_device_impl(const art_params* p, int64_t n, const double* x0, cons
     so.cap = xc->capacity;
     so.xcount = xc->count;
     so.xpos = xc->pos; so.xk = xc->k; so.xt = xc->t; so.xdw = xc->dw; so.xp = xc->p_nonad;
+    void* xrec = nullptr;  // the integrator's AoS crossing records (-> finalize_kernel)
+    if ((rc = pool_get(c, 10, (size_t)n * (size_t)xc->capacity * art::X_REC * sizeof(double), &xrec))) return rc;
+    so.xrec = (double*)xrec;
   }
   if (tr.ntimes != 0) {
     if (tr.ntimes < 2 || !tr.traj || !tr.t || !tr.count) return fail(ART_E_INVALID, "saveat needs ntimes >= 2 and buffers");
@@ -139,6 +144,7 @@ int propagate_device_impl(const art_params* p, int64_t n, const double* x0, cons
     so.traj_t = tr.t;
     so.traj_n = tr.count;
   }
+  so.rec = (double*)rec;
   HIP_OK(hipMemsetAsync(c->scratch, 0, sizeof(unsigned long long) * (1 + art::N_STATS), s));
   HIP_OK(art::launch_propagate(K, n, in, so, max_crossings, c->scratch, c->scratch + 1, s, &g_last_grid, c->ev0,
                                 c->ev1));

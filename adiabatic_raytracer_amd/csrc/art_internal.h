@@ -24,7 +24,19 @@ struct SegOut {
   int32_t ntimes;
   double *traj, *traj_t;
   int32_t* traj_n;
+  // END_REC doubles of device scratch per ray: the integrator's raw end state as one AoS
+  // record per ray, [u (7) | tau | int4 {status, n_acc, n_rej, ncross} | int4 {traj_n, 0, 0, 0}],
+  // which finalize_kernel spreads into the SoA outputs above with coalesced stores. A finishing
+  // lane then writes 5 (saveat: 6) 16-byte stores into its own 128-byte line instead of 12
+  // 4/8-byte stores into as many partly written lines.
+  double* rec;
+  // X_REC doubles of device scratch per (ray, crossing j < cap), the same idea for the
+  // crossings affect! records: [x (3) | k (3) | t | Δω] at ((ray cap + j) X_REC), spread into
+  // xpos / xk / xt / xdw by finalize_kernel
+  double* xrec;
 };
+constexpr int END_REC = 16;
+constexpr int X_REC = 8;
 constexpr int N_STATS = 8;  // propagate statistics: attempts, accepted, root re-steps, scan evals,
                             // interpolant-root evals, rays, init RHS, (reserved)
 int persistent_blocks(const void* func, int64_t work);

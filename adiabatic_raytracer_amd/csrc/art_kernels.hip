@@ -264,14 +264,12 @@ __device__ inline int affect(const KParams& P, const SegIn& in, const SegOut& ou
   if (sqrt(x[0] * x[0] + x[1] * x[1] + x[2] * x[2]) < P.rNS101) return 0;  // :322-324
   const int j = ncross;
   if (out.xcount && j < out.cap) {
-    const double dwc = u[6] / erg;
-#pragma unroll
-    for (int c = 0; c < 3; ++c) {
-      out.xpos[(int64_t(c) * out.cap + j) * n + ray] = x[c];
-      out.xk[(int64_t(c) * out.cap + j) * n + ray] = k[c];
-    }
-    out.xt[int64_t(j) * n + ray] = exp(tau);
-    out.xdw[int64_t(j) * n + ray] = dwc;  // P_nonAD: crossing_prob_kernel
+    const double dwc = u[6] / erg;  // P_nonAD: finalize_kernel
+    double2* rq = reinterpret_cast<double2*>(out.xrec + ((int64_t)ray * out.cap + j) * X_REC);
+    rq[0] = make_double2(x[0], x[1]);
+    rq[1] = make_double2(x[2], k[0]);
+    rq[2] = make_double2(k[1], k[2]);
+    rq[3] = make_double2(exp(tau), dwc);
   }
   ncross = j + 1;
   const int maxc = max_crossings <= 0 ? -1 : max_crossings;
@@ -984,19 +982,15 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
       else if (iter >= P.maxiters) finish = ART_STATUS_MAXITERS;
     }
 
-    if (finish >= 0) {  // the raw state; finalize_kernel back-transforms it in place (RayTracer.jl:393-416)
-#pragma unroll
-      for (int c = 0; c < 3; ++c) {
-        out.x_end[c * n + ray] = u[c];
-        out.k_end[c * n + ray] = u[3 + c];
-      }
-      out.u7_end[ray] = u[6];
-      out.tau_end[ray] = tau;
-      out.status[ray] = finish;
-      out.n_acc[ray] = n_acc;
-      out.n_rej[ray] = n_rej;
-      if (out.xcount) out.xcount[ray] = ncross;
-      if constexpr (SAVE) out.traj_n[ray] = save_k + 1;  // start + interior + end
+    if (finish >= 0) {  // the raw end record; finalize_kernel back-transforms it (RayTracer.jl:393-416)
+      double2* rq = reinterpret_cast<double2*>(out.rec + (int64_t)ray * END_REC);
+      rq[0] = make_double2(u[0], u[1]);
+      rq[1] = make_double2(u[2], u[3]);
+      rq[2] = make_double2(u[4], u[5]);
+      rq[3] = make_double2(u[6], tau);
+      int4* ri = reinterpret_cast<int4*>(rq + 4);
+      ri[0] = make_int4(finish, n_acc, n_rej, ncross);
+      if constexpr (SAVE) ri[1] = make_int4(save_k + 1, 0, 0, 0);  // start + interior + end
       ray = -1;
       mode = M_IDLE;
     }
@@ -1066,28 +1060,35 @@ __global__ __launch_bounds__(256) void init_kernel(const KParams P, const int64_
   if ((threadIdx.x & 63) == 0 && x) atomicAdd(&stats[6], x);
 }
 
-// End state in Cartesian form (back-transform, RayTracer.jl:393-416) from the raw state the
-// integrator left in x_end / k_end / u7_end, and the conversion probability of every
+// End state in Cartesian form (back-transform, RayTracer.jl:393-416) from the raw end record
+// the integrator left in out.rec (spread into the SoA outputs here), and the conversion probability of every
 // recorded crossing (get_Prob_nonAD with Nc = 1, MainRunner.jl:265). One thread per ray.
 __global__ __launch_bounds__(256) void finalize_kernel(const KParams P, const int64_t n, const SegIn in,
                                                        const SegOut out) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const double erg = in.erg[i];
+  int ncross = 0;
   {
+    const double2* rq = reinterpret_cast<const double2*>(out.rec + i * END_REC);
     double u[7], xe[3], ke[3];
-#pragma unroll
-    for (int c = 0; c < 3; ++c) {
-      u[c] = out.x_end[c * n + i];
-      u[3 + c] = out.k_end[c * n + i];
-    }
-    u[6] = out.u7_end[i];
+    const double2 q0 = rq[0], q1 = rq[1], q2 = rq[2], q3 = rq[3];
+    const int4 ri = reinterpret_cast<const int4*>(rq + 4)[0];
+    u[0] = q0.x; u[1] = q0.y; u[2] = q1.x; u[3] = q1.y; u[4] = q2.x; u[5] = q2.y; u[6] = q3.x;
     back_transform(P, u, erg, xe, ke);
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
       out.x_end[c * n + i] = xe[c];
       out.k_end[c * n + i] = ke[c];
     }
+    out.u7_end[i] = u[6];
+    out.tau_end[i] = q3.y;
+    out.status[i] = ri.x;
+    out.n_acc[i] = ri.y;
+    out.n_rej[i] = ri.z;
+    ncross = ri.w;
+    if (out.xcount) out.xcount[i] = ncross;
+    if (out.ntimes >= 2) out.traj_n[i] = reinterpret_cast<const int4*>(rq + 4)[1].x;
   }
   if (out.ntimes >= 2) {  // saveat: start (u0 back-transformed), interior to Cartesian, end
     double u0[7], xs[3], ks[3];
@@ -1115,15 +1116,19 @@ __global__ __launch_bounds__(256) void finalize_kernel(const KParams P, const in
     }
   }
   if (!out.xcount) return;
-  const int m = out.xcount[i] < out.cap ? out.xcount[i] : out.cap;
+  const int m = ncross < out.cap ? ncross : out.cap;
   for (int j = 0; j < m; ++j) {
-    double x[3], k[3];
+    const double2* rq = reinterpret_cast<const double2*>(out.xrec + (i * out.cap + j) * X_REC);
+    const double2 q0 = rq[0], q1 = rq[1], q2 = rq[2], q3 = rq[3];
+    const double x[3] = {q0.x, q0.y, q1.x}, k[3] = {q1.y, q2.x, q2.y};
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
-      x[c] = out.xpos[(int64_t(c) * out.cap + j) * n + i];
-      k[c] = out.xk[(int64_t(c) * out.cap + j) * n + i];
+      out.xpos[(int64_t(c) * out.cap + j) * n + i] = x[c];
+      out.xk[(int64_t(c) * out.cap + j) * n + i] = k[c];
     }
-    const double dwc = out.xdw[int64_t(j) * n + i];
+    out.xt[int64_t(j) * n + i] = q3.x;
+    const double dwc = q3.y;
+    out.xdw[int64_t(j) * n + i] = dwc;
     out.xp[int64_t(j) * n + i] = prob_nonad_single(P, x, k, erg * fabs(dwc));  // erg_inf_ini .* abs.(Δωc)
   }
 }
