@@ -349,7 +349,9 @@ constexpr int SCAN_WORDS = 4;  // 2-bit codes for up to 64 grid points (interp_p
 // kernel then works on a copy of the parameters whose rs_eff, bndry_lyr and isotropic are
 // compile-time constants, so the Schwarzschild, boundary-layer and isotropic branches of
 // the physics fold away instead of holding registers. GEOM_ANY reads them at run time.
-enum { GEOM_ANY = 0, GEOM_FLAT = 1 };
+// GEOM_GR: Schwarzschild (rs > 0), no boundary layer, anisotropic (configs[3]): only the
+// boundary-layer and isotropic branches fold away, and rs != 0 is assumed.
+enum { GEOM_ANY = 0, GEOM_FLAT = 1, GEOM_GR = 2 };
 
 template <int GEOM>
 __device__ inline KParams specialize(const KParams& P) {
@@ -359,6 +361,10 @@ __device__ inline KParams specialize(const KParams& P) {
     Q.bndry_lyr = -1.0;
     Q.isotropic = 0;
     Q.cert_rmin = 0.0;
+  } else if (GEOM == GEOM_GR) {
+    __builtin_assume(Q.rs_eff > 0.0);
+    Q.bndry_lyr = -1.0;
+    Q.isotropic = 0;
   }
   return Q;
 }
@@ -1415,16 +1421,19 @@ hipError_t launch_propagate(const KParams& P, int64_t n, const SegIn& in, const 
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   const bool flat = P.rs_eff == 0.0 && !(P.bndry_lyr > 0.0) && !P.isotropic;
+  const bool sch = P.rs_eff > 0.0 && !(P.bndry_lyr > 0.0) && !P.isotropic;
   const bool rk4 = P.integrator == ART_RK4;
   using KFn = void (*)(const KParams, const int64_t, const SegIn, const SegOut, const int32_t, unsigned long long*,
                        unsigned long long*);
   KFn fn;
   if (out.ntimes >= 2)  // saveat requested: the saving instantiations
     fn = rk4 ? propagate_kernel<ART_RK4, GEOM_ANY, true>
-             : (flat ? propagate_kernel<ART_VERN6, GEOM_FLAT, true> : propagate_kernel<ART_VERN6, GEOM_ANY, true>);
+             : (flat ? propagate_kernel<ART_VERN6, GEOM_FLAT, true>
+                     : (sch ? propagate_kernel<ART_VERN6, GEOM_GR, true> : propagate_kernel<ART_VERN6, GEOM_ANY, true>));
   else
     fn = rk4 ? (flat ? propagate_kernel<ART_RK4, GEOM_FLAT, false> : propagate_kernel<ART_RK4, GEOM_ANY, false>)
-             : (flat ? propagate_kernel<ART_VERN6, GEOM_FLAT, false> : propagate_kernel<ART_VERN6, GEOM_ANY, false>);
+             : (flat ? propagate_kernel<ART_VERN6, GEOM_FLAT, false>
+                     : (sch ? propagate_kernel<ART_VERN6, GEOM_GR, false> : propagate_kernel<ART_VERN6, GEOM_ANY, false>));
   const int grid = persistent_blocks((const void*)fn, n);
   if (grid_out) *grid_out = grid;
   if (ev0 && (e = hipEventRecord(ev0, s)) != hipSuccess) return e;
@@ -1492,6 +1501,8 @@ template __global__ void propagate_kernel<ART_VERN6, GEOM_ANY, false>(const KPar
     const int32_t, unsigned long long*, unsigned long long*);
 template __global__ void propagate_kernel<ART_VERN6, GEOM_FLAT, false>(const KParams, const int64_t, const SegIn, const SegOut,
     const int32_t, unsigned long long*, unsigned long long*);
+template __global__ void propagate_kernel<ART_VERN6, GEOM_GR, false>(const KParams, const int64_t, const SegIn, const SegOut,
+    const int32_t, unsigned long long*, unsigned long long*);
 template __global__ void propagate_kernel<ART_RK4, GEOM_ANY, false>(const KParams, const int64_t, const SegIn, const SegOut,
     const int32_t, unsigned long long*, unsigned long long*);
 template __global__ void propagate_kernel<ART_RK4, GEOM_FLAT, false>(const KParams, const int64_t, const SegIn, const SegOut,
@@ -1499,6 +1510,8 @@ template __global__ void propagate_kernel<ART_RK4, GEOM_FLAT, false>(const KPara
 template __global__ void propagate_kernel<ART_VERN6, GEOM_ANY, true>(const KParams, const int64_t, const SegIn, const SegOut,
     const int32_t, unsigned long long*, unsigned long long*);
 template __global__ void propagate_kernel<ART_VERN6, GEOM_FLAT, true>(const KParams, const int64_t, const SegIn, const SegOut,
+    const int32_t, unsigned long long*, unsigned long long*);
+template __global__ void propagate_kernel<ART_VERN6, GEOM_GR, true>(const KParams, const int64_t, const SegIn, const SegOut,
     const int32_t, unsigned long long*, unsigned long long*);
 template __global__ void propagate_kernel<ART_RK4, GEOM_ANY, true>(const KParams, const int64_t, const SegIn, const SegOut,
     const int32_t, unsigned long long*, unsigned long long*);
