@@ -144,6 +144,16 @@ __host__ __device__ inline double flog(double x) {
   return log(x);
 #endif
 }
+// 1/x for the templated physics: frcp for double, a plain division for the counting and
+// dual types of tools/ and oracle/
+template <class T>
+__host__ __device__ inline T trcp(const T& x) {
+  return T(1.0) / x;
+}
+template <>
+__host__ __device__ inline double trcp<double>(const double& x) {
+  return frcp(x);
+}
 __host__ __device__ inline double msin(double x) { return sin(x); }
 __host__ __device__ inline double mcos(double x) { return cos(x); }
 __host__ __device__ inline double macos(double x) { return acos(x); }
@@ -254,10 +264,10 @@ __host__ __device__ inline void metric_tr_d(const T& r, double rs, T& gtt, T& gr
     gtt = -4.0 * iD * iD;
     dgtt = 8.0 * (3.0 * dS1 - dS2) * iD * iD * iD;
   } else {
-    const T ir = 1.0 / r;
+    const T ir = trcp(r);
     grr = 1.0 - rs * ir;
     dgrr = rs * ir * ir;
-    const T ig = 1.0 / grr;
+    const T ig = trcp(grr);
     gtt = -ig;
     dgtt = dgrr * ig * ig;
   }
@@ -314,8 +324,6 @@ __host__ __device__ inline void rhs_photon(const KParams& P, const T* u, const T
   const T t = fexp(tau);
   const T r = u[0];
   const T E = -u[6];
-  T gtt_u, grr_u;
-  metric_tr(r, P.rs_eff, gtt_u, grr_u);
   const T rc = (r < P.rNS) ? T(P.rNS) : r;
   T st, ct, sp, cp;
   msincos(u[1], st, ct);
@@ -343,6 +351,13 @@ __host__ __device__ inline void rhs_photon(const KParams& P, const T* u, const T
   const T dwp2_p = cB * sgb * d.bp;
   T gtt, grr, dgtt, dgrr;
   metric_tr_d(rc, P.rs_eff, gtt, grr, dgtt, dgrr);
+  // the prefactor's g^rr at the raw radius (:82) differs from the clamped one only inside the
+  // star: a second metric evaluation only for lanes there
+  T grr_u = grr;
+  if (!(P.rs_eff == 0.0) && r < P.rNS) {
+    T gtt_u;
+    metric_tr(r, P.rs_eff, gtt_u, grr_u);
+  }
   const T gpp = ir2 * iast * iast;
   const T E2 = E * E;
   const T iE2 = iE * iE;
@@ -462,6 +477,13 @@ __host__ __device__ inline void hamiltonian_full(const KParams& P, const T* x, c
   }
   T gtt, grr, dgtt, dgrr;
   metric_tr_d(rc, P.rs_eff, gtt, grr, dgtt, dgrr);
+  // the prefactor's g^rr at the raw radius (:82) differs from the clamped one only inside the
+  // star: a second metric evaluation only for lanes there
+  T grr_u = grr;
+  if (!(P.rs_eff == 0.0) && r < P.rNS) {
+    T gtt_u;
+    metric_tr(r, P.rs_eff, gtt_u, grr_u);
+  }
   const T gpp = ir2 * iast * iast;
   const T E2 = E * E, iE2 = 1.0 / E2, sq = msqrt(grr);
   T Q = 0.0, Q_r = 0.0, Q_t = 0.0, Q_p = 0.0, Q_kr = 0.0, Q_kt = 0.0, Q_kp = 0.0;
