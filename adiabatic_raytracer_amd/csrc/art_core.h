@@ -1010,29 +1010,30 @@ __host__ __device__ inline T prob_nonad_single(const KParams& P, const T* pos, c
 // Sampler condition (find_samples_new :1547-1583, thick_surface = true) at the Cartesian
 // line point x with local velocity direction vl. sinθ, cosθ, sinφ, cosφ are taken
 // algebraically from x instead of through acos/atan2 + sin/cos (identical values up to
-// rounding); the metric always uses the GR mass (the sampler gets no `flat`).
+// rounding); the metric always uses the GR mass (the sampler gets no `flat`). Divisions are
+// hardware reciprocals with two Newton steps (trcp) on the device.
 template <class T>
 __host__ __device__ inline T sampler_condition(const KParams& P, const T* x, const T* vl, double E) {
   const T rho2 = x[0] * x[0] + x[1] * x[1];
   const T r = msqrt(rho2 + x[2] * x[2]);
-  const T ir = 1.0 / r;
+  const T ir = trcp(r);
   const T rho = msqrt(rho2);
   const T st = rho * ir, ct = x[2] * ir;
-  const T irho = 1.0 / rho;
+  const T irho = trcp(rho);
   const T cp = x[0] * irho, sp = x[1] * irho;  // ψ = φ at t0 = 0
   T AA = 1.0 - P.rs_gr * ir;
   if (r < P.rNS) AA = 1.0;
-  const T iAA = 1.0 / AA;
+  const T iAA = trcp(AA);
   const T dr_dt = (x[0] * vl[0] + x[1] * vl[1] + x[2] * vl[2]) * ir;
-  T w0 = dr_dt / msqrt(AA) * iAA;
-  T w1 = (x[2] * dr_dt - r * vl[2]) / st * iAA;
+  T w0 = dr_dt * trcp(msqrt(AA)) * iAA;
+  T w1 = (x[2] * dr_dt - r * vl[2]) * trcp(st) * iAA;
   T w2 = (x[0] * vl[1] - x[1] * vl[0]) * iAA;
   T gtt, grr;
   metric_tr(r, P.rs_gr, gtt, grr);
   const T ir2 = ir * ir;
-  const T gpp = ir2 / (st * st);
+  const T gpp = ir2 * trcp(st * st);
   const double E2 = E * E;
-  const T nrm = (-E2 * gtt - P.mass_a2) / (grr * w0 * w0 + ir2 * w1 * w1 + gpp * w2 * w2);
+  const T nrm = (-E2 * gtt - P.mass_a2) * trcp(grr * w0 * w0 + ir2 * w1 * w1 + gpp * w2 * w2);
   const T f = msqrt(nrm);
   w0 = w0 * f; w1 = w1 * f; w2 = w2 * f;
   const DipoleAng<T> d = dipole_ang(P, st, ct, sp, cp);
@@ -1043,11 +1044,12 @@ __host__ __device__ inline T sampler_condition(const KParams& P, const T* x, con
   }
   T kpar2 = 0.0;
   if (!P.isotropic) {
-    const T p = 2.0 * msqrt(grr) * w0 * d.a1 + ir * (w1 * d.a2 + w2 * d.a3 / mabs(st));
-    kpar2 = p * p / (4.0 * d.a1 * d.a1 + d.a2 * d.a2 + d.a3 * d.a3);
+    const T p = 2.0 * msqrt(grr) * w0 * d.a1 + ir * (w1 * d.a2 + w2 * d.a3 * trcp(mabs(st)));
+    kpar2 = p * p * trcp(4.0 * d.a1 * d.a1 + d.a2 * d.a2 + d.a3 * d.a3);
   }
   const T ksqr = gtt * E2 + grr * w0 * w0 + ir2 * w1 * w1 + gpp * w2 * w2;
-  return 0.5 * (ksqr + wp2 * (1.0 - grr * kpar2 / E2)) / E2;
+  const double iE2 = 1.0 / E2;  // per attempt: hoisted out of the scan by the compiler
+  return 0.5 * (ksqr + wp2 * (1.0 - grr * kpar2 * iE2)) * iE2;
 }
 
 // ωp from GJ_Model_ωp_vec (no zeroIn) at Cartesian x, t = 0 (sampler affect!, :1587)
@@ -1055,9 +1057,9 @@ template <class T>
 __host__ __device__ inline T wp_cart(const KParams& P, const T* x) {
   const T rho2 = x[0] * x[0] + x[1] * x[1];
   const T r = msqrt(rho2 + x[2] * x[2]);
-  const T ir = 1.0 / r;
+  const T ir = trcp(r);
   const T rho = msqrt(rho2);
-  const T irho = 1.0 / rho;
+  const T irho = trcp(rho);
   const DipoleAng<T> d = dipole_ang(P, rho * ir, x[2] * ir, x[1] * irho, x[0] * irho);
   T wp = msqrt(P.wp2n * ir * ir * ir * mabs(d.b));
   if (P.bndry_lyr > 0.0 && r >= P.rNS) wp = wp + layer_wp(P, r, P.rmax);
