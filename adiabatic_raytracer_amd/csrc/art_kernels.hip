@@ -1155,6 +1155,9 @@ __global__ __launch_bounds__(256) void sample_kernel(const KParams P, const doub
   const double send = 2.2 * maxR;
   const int nsteps = (int)ceil(send / 0.5);
   const int np = 20;  // ContinuousCallback(interp_points=20) (:1603)
+  // certified-negative scan steps (below): GJ plasma without a boundary layer only
+  const bool cert_ok = !(P.bndry_lyr > 0.0) && P.mass_a > 0.0;
+  const double cert_lhs = 2.0 * P.wp2n, cert_rhs = P.mass_a2 * (1.0 - 1e-6);
   while (true) {
     if (!exhausted) {
       unsigned long long need = __ballot(ray < 0);
@@ -1215,6 +1218,29 @@ __global__ __launch_bounds__(256) void sample_kernel(const KParams P, const doub
     for (int st = 0; st < nsteps; ++st) {
       const double s0 = st * 0.5;
       const double s1 = fmin(s0 + 0.5, send);
+      // Certified-negative step: with the axion shell imposed (w normalised), the condition
+      // is ½(-m_a² + ωp² (1 - g^rr k∥²/E²))/E² with 0 <= g^rr k∥² <= E² (Cauchy-Schwarz, the
+      // factor is at most 1), and ωp² = wp2n |b| / r³ <= 2 wp2n / r³ (|b| <= √(4a1² + a2²)
+      // <= 2). Where 2 wp2n / r_min³ stays below m_a² on the whole segment (r_min: the line's
+      // closest approach to the centre within [s0, s1]), all its points are negative. If the
+      // point before is negative too, no sign change can occur: only the last point is
+      // evaluated, for the value a bracket opening at the next step's first point starts from.
+      if (cert_ok && c_prev < 0.0) {
+        const double sd = -(x0[0] * va[0] + x0[1] * va[1] + x0[2] * va[2]);
+        const double sm = fmin(fmax(sd, s0), s1);
+        double xm[3];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) xm[i] = x0[i] + va[i] * sm;
+        const double rm2 = xm[0] * xm[0] + xm[1] * xm[1] + xm[2] * xm[2];
+        if (cert_lhs < cert_rhs * (rm2 * sqrt(rm2))) {
+          const double sc = s0 + (s1 - s0) * double(np - 1) / double(np - 1);
+#pragma unroll
+          for (int i = 0; i < 3; ++i) xl[i] = x0[i] + va[i] * sc;
+          s_prev = sc;
+          c_prev = sampler_condition(P, xl, vl, E);
+          continue;
+        }
+      }
       for (int ip = 1; ip < np; ++ip) {
         const double sc = s0 + (s1 - s0) * double(ip) / double(np - 1);
 #pragma unroll
