@@ -17,4 +17,7 @@ def __getattr__(name):
     if name == "Engine":
         from .engine import Engine
         return Engine
+    if name in ("trees", "scan", "shard", "engine"):
+        import importlib
+        return importlib.import_module(f".{name}", __name__)
     raise AttributeError(name)

@@ -33,7 +33,7 @@ class CrossingBuf(C.Structure):
 # name -> (restype, argtypes); the test suite checks this table against include/art.h
 class TreeOpts(C.Structure):  # include/art.h art_tree_opts
     _fields_ = [("num_cutoff", C.c_int32), ("mc_nodes", C.c_int32), ("max_nodes", C.c_int32),
-                ("splittings_cutoff", C.c_int32), ("crossing_cap", C.c_int32), ("pad", C.c_int32),
+                ("splittings_cutoff", C.c_int32), ("crossing_cap", C.c_int32), ("tree_offset", C.c_int32),
                 ("prob_cutoff", C.c_double), ("seed", C.c_uint64)]
 
 
@@ -73,6 +73,13 @@ SIGNATURES = {
                                       _v, C.POINTER(TreeTraj)]),
     "art_event_weight_host": (C.c_int, [_P, _d, _d, _d, _i64, _v, _v, _v, _v]),
     "art_event_weight_device": (C.c_int, [_P, _d, _d, _d, _i64, _v, _v, _v, _v, _v]),
+    "art_recent_kernel_ms": (C.c_int, [_i32, _v]),
+    "art_flux_histogram_phi_device": (C.c_int, [_i64, _v, _v, _v, _i32, _v, _v]),
+    "art_comm_unique_id": (C.c_int, [_v]),
+    "art_comm_init": (C.c_int, [_i32, _i32, _v]),
+    "art_flux_allreduce": (C.c_int, [_v, _i64, _v]),
+    "art_flux_allreduce_host": (C.c_int, [_v, _i64]),
+    "art_comm_destroy": (C.c_int, []),
     "art_eval_rhs_device": (C.c_int, [_P, _i64, _v, _v, _v, _v, _v, _v]),
     "art_eval_hamiltonian_device": (C.c_int, [_P, _i64, _v, _v, _v, _v, _v, _v, _v, _v, _v]),
     "art_eval_condition_device": (C.c_int, [_P, _i64, _v, _v, _v, _v]),
@@ -94,6 +101,13 @@ def load(path=None):
     if not os.path.exists(path):
         raise ArtError(f"libart.so not found at {path}: the HIP engine must be built "
                        f"(python -m adiabatic_raytracer_amd.build); there is no CPU fallback")
+    # PyTorch ships its own HIP runtime under the same soname (libamdhip64.so.7). Whichever is
+    # loaded first serves the whole process; torch refuses a foreign one ("No HIP GPUs are
+    # available"), so when torch is present it is imported first and libart binds to torch's.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = C.CDLL(path)
     for name, (res, args) in SIGNATURES.items():
         fn = getattr(lib, name)

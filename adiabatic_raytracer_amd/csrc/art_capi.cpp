@@ -5,6 +5,8 @@
 // asynchronously on the caller's stream. No torch types cross this boundary.
 #include <hip/hip_runtime.h>
 
+#include <dlfcn.h>
+
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -26,12 +28,26 @@ double g_last_ms = 0.0;
 unsigned long long g_last_stats[art::N_STATS] = {0};
 int g_last_grid = 0;
 
+// One propagate launch's bookkeeping: the HIP events around the integrator kernel, an event
+// after its statistics were copied to pinned host memory, and that memory. A ring of them per
+// device lets launches on different streams be in flight together; a slot is reused only after
+// its previous launch completed.
+constexpr int RING = 64;
+struct LaunchRec {
+  hipEvent_t ev0 = nullptr, ev1 = nullptr, done = nullptr;
+  unsigned long long* host_stats = nullptr;  // N_STATS words (pinned)
+  int grid = 0;
+  bool pending = false;
+};
+
 struct DeviceCtx {
   int device = -1;
-  hipStream_t stream = nullptr;
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
-  unsigned long long* scratch = nullptr;  // [0] queue head, [1..N_STATS] statistics
-  std::vector<std::pair<void*, size_t>> pool;  // host-entry staging buffers (grow-only)
+  hipStream_t stream = nullptr;  // the *_host entry points' stream
+  LaunchRec ring[RING];
+  int next = 0, last = -1;       // next ring slot; the most recent propagate launch
+  int64_t launches = 0;          // propagate launches issued so far
+  std::vector<std::pair<void*, size_t>> pool;  // host-entry staging buffers (grow-only, used under g_mu by the
+                                               // synchronous *_host calls only)
 };
 std::vector<DeviceCtx> g_ctx;
 
@@ -54,13 +70,36 @@ int current_ctx(DeviceCtx** out) {
   if ((int)g_ctx.size() <= dev) g_ctx.resize(dev + 1);
   DeviceCtx& c = g_ctx[dev];
   if (c.device < 0) {
-    c.device = dev;
     HIP_OK(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking));
-    HIP_OK(hipEventCreate(&c.ev0));
-    HIP_OK(hipEventCreate(&c.ev1));
-    HIP_OK(hipMalloc(&c.scratch, sizeof(unsigned long long) * (1 + art::N_STATS)));
+    unsigned long long* hs = nullptr;
+    HIP_OK(hipHostMalloc((void**)&hs, sizeof(unsigned long long) * art::N_STATS * RING, hipHostMallocDefault));
+    for (int i = 0; i < RING; ++i) {
+      HIP_OK(hipEventCreate(&c.ring[i].ev0));
+      HIP_OK(hipEventCreate(&c.ring[i].ev1));
+      HIP_OK(hipEventCreateWithFlags(&c.ring[i].done, hipEventDisableTiming));
+      c.ring[i].host_stats = hs + i * art::N_STATS;
+    }
+    // per-launch scratch comes from the stream-ordered allocator: keep what it frees cached
+    // so a steady stream of launches does not go back to the driver
+    hipMemPool_t mp;
+    if (hipDeviceGetDefaultMemPool(&mp, dev) == hipSuccess) {
+      uint64_t thr = ~0ull;
+      (void)hipMemPoolSetAttribute(mp, hipMemPoolAttrReleaseThreshold, &thr);
+    }
+    c.device = dev;
   }
   *out = &c;
+  return ART_OK;
+}
+
+// The next launch record: waits for the launch that used the slot RING launches ago.
+int take_slot(DeviceCtx* c, LaunchRec** out) {
+  LaunchRec& L = c->ring[c->next];
+  if (L.pending) {
+    HIP_OK(hipEventSynchronize(L.done));
+    L.pending = false;
+  }
+  *out = &L;
   return ART_OK;
 }
 
@@ -78,6 +117,14 @@ int pool_get(DeviceCtx* c, size_t slot, size_t bytes, void** p) {
   return ART_OK;
 }
 
+// Device scratch of ONE launch, allocated and freed in the order of its stream (hipMallocAsync /
+// hipFreeAsync), so concurrent launches never share a work-queue word or a state buffer.
+int scratch_alloc(hipStream_t s, size_t bytes, void** p) {
+  if (hipMallocAsync(p, bytes, s) != hipSuccess)
+    return fail(ART_E_NOMEM, "hipMallocAsync of %s bytes failed", std::to_string(bytes).c_str());
+  return ART_OK;
+}
+
 int validate(const art_params* p) {
   if (!p) return fail(ART_E_INVALID, "params is NULL");
   if (!p->melrose) return fail(ART_E_UNSUPPORTED, "melrose=0 (Ctheta_B_sphere form) is not supported; the reference hard-codes melrose=true (Gen_Samples.jl:167)");
@@ -88,6 +135,16 @@ int validate(const art_params* p) {
   if (p->maxiters < 1) return fail(ART_E_INVALID, "maxiters must be >= 1");
   if (p->interp_points > 65) return fail(ART_E_INVALID, "interp_points must be <= 65 (the reference uses 50)");
   return ART_OK;
+}
+
+// Kernel parameters. ART_SCAN_CERT=0 switches the certified scan steps of the integrator and
+// of the sampler off (A/B tests: the results are bit-identical either way,
+// tests/test_gpu_scan_cert.py).
+art::KParams kparams(const art_params& p) {
+  art::KParams K = art::make_kparams(p);
+  if (const char* e = std::getenv("ART_SCAN_CERT"))
+    if (e[0] == '0') K.cert_fac = __builtin_inf();
+  return K;
 }
 
 // *_device entry points run on the caller's stream exactly as given: NULL is the HIP null
@@ -115,48 +172,63 @@ int propagate_device_impl(const art_params* p, int64_t n, const double* x0, cons
   DeviceCtx* c;
   if ((rc = current_ctx(&c))) return rc;
   hipStream_t s = pick(c, stream);
-  art::KParams K = art::make_kparams(*p);
-  // ART_SCAN_CERT=0 switches the certified-negative scan off (A/B tests: the results are
-  // bit-identical either way, tests/test_gpu_scan_cert.py)
-  if (const char* e = std::getenv("ART_SCAN_CERT"))
-    if (e[0] == '0') K.cert_fac = __builtin_inf();
-  void* u0 = nullptr;  // 16n doubles of fresh state: u0, f0, dt, c0 (init_kernel -> the integrator)
-  if ((rc = pool_get(c, 6, (size_t)n * 16 * sizeof(double), &u0))) return rc;
-  void* rec = nullptr;  // END_REC n doubles: the integrator's AoS end records (-> finalize_kernel)
-  if ((rc = pool_get(c, 9, (size_t)n * art::END_REC * sizeof(double), &rec))) return rc;
-  art::SegIn in{x0, k0, erg, dw, ln_t0, species, (double*)u0};
+  const art::KParams K = kparams(*p);
+  const int cap = (xc && xc->count) ? xc->capacity : 0;
+  if (cap && (cap < 1 || !xc->pos || !xc->k || !xc->t || !xc->dw || !xc->p_nonad))
+    return fail(ART_E_INVALID, "crossing buffer incomplete");
+  if (tr.ntimes != 0 && (tr.ntimes < 2 || !tr.traj || !tr.t || !tr.count))
+    return fail(ART_E_INVALID, "saveat needs ntimes >= 2 and buffers");
+  // this launch's scratch: [queue head + statistics (256 B) | u0: 16n doubles of fresh state
+  // (init_kernel -> the integrator) | END_REC n doubles of end records | X_REC cap n doubles of
+  // crossing records (the integrator -> finalize_kernel)]
+  const size_t nd = (size_t)n;
+  const size_t head = 256, u0b = nd * 16 * sizeof(double), recb = nd * art::END_REC * sizeof(double);
+  const size_t xrb = (size_t)cap * nd * art::X_REC * sizeof(double);
+  LaunchRec* L;
+  if ((rc = take_slot(c, &L))) return rc;
+  void* blk = nullptr;
+  if ((rc = scratch_alloc(s, head + u0b + recb + xrb, &blk))) return rc;
+  unsigned long long* words = (unsigned long long*)blk;
+  double* u0 = (double*)((char*)blk + head);
+  double* rec = (double*)((char*)blk + head + u0b);
+  art::SegIn in{x0, k0, erg, dw, ln_t0, species, u0};
   art::SegOut so{out->x_end, out->k_end, out->u7_end, out->tau_end, out->status, out->n_accept, out->n_reject,
                  0, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
-  if (xc && xc->count) {
-    if (xc->capacity < 1 || !xc->pos || !xc->k || !xc->t || !xc->dw || !xc->p_nonad)
-      return fail(ART_E_INVALID, "crossing buffer incomplete");
-    so.cap = xc->capacity;
+  if (cap) {
+    so.cap = cap;
     so.xcount = xc->count;
     so.xpos = xc->pos; so.xk = xc->k; so.xt = xc->t; so.xdw = xc->dw; so.xp = xc->p_nonad;
-    void* xrec = nullptr;  // the integrator's AoS crossing records (-> finalize_kernel)
-    if ((rc = pool_get(c, 10, (size_t)n * (size_t)xc->capacity * art::X_REC * sizeof(double), &xrec))) return rc;
-    so.xrec = (double*)xrec;
+    so.xrec = (double*)((char*)blk + head + u0b + recb);
   }
   if (tr.ntimes != 0) {
-    if (tr.ntimes < 2 || !tr.traj || !tr.t || !tr.count) return fail(ART_E_INVALID, "saveat needs ntimes >= 2 and buffers");
     so.ntimes = tr.ntimes;
     so.traj = tr.traj;
     so.traj_t = tr.t;
     so.traj_n = tr.count;
   }
-  so.rec = (double*)rec;
-  HIP_OK(hipMemsetAsync(c->scratch, 0, sizeof(unsigned long long) * (1 + art::N_STATS), s));
-  HIP_OK(art::launch_propagate(K, n, in, so, max_crossings, c->scratch, c->scratch + 1, s, &g_last_grid, c->ev0,
-                                c->ev1));
+  so.rec = rec;
+  HIP_OK(hipMemsetAsync(words, 0, head, s));
+  HIP_OK(art::launch_propagate(K, n, in, so, max_crossings, words, words + 1, s, &L->grid, L->ev0, L->ev1));
+  HIP_OK(hipMemcpyAsync(L->host_stats, words + 1, sizeof(unsigned long long) * art::N_STATS, hipMemcpyDeviceToHost, s));
+  HIP_OK(hipEventRecord(L->done, s));
+  HIP_OK(hipFreeAsync(blk, s));
+  L->pending = true;
+  c->last = c->next;
+  c->next = (c->next + 1) % RING;
+  c->launches += 1;
   return ART_OK;
 }
 
+// Latch the most recent propagate launch: its integrator kernel's duration and statistics.
 int finish_timing(DeviceCtx* c) {
-  HIP_OK(hipEventSynchronize(c->ev1));
+  if (c->last < 0) return ART_OK;
+  LaunchRec& L = c->ring[c->last];
+  HIP_OK(hipEventSynchronize(L.done));
   float ms = 0.f;
-  HIP_OK(hipEventElapsedTime(&ms, c->ev0, c->ev1));
+  HIP_OK(hipEventElapsedTime(&ms, L.ev0, L.ev1));
   g_last_ms = ms;
-  HIP_OK(hipMemcpy(g_last_stats, c->scratch + 1, sizeof(g_last_stats), hipMemcpyDeviceToHost));
+  g_last_grid = L.grid;
+  for (int i = 0; i < art::N_STATS; ++i) g_last_stats[i] = L.host_stats[i];
   return ART_OK;
 }
 
@@ -199,6 +271,28 @@ int art_last_stats(uint64_t* stats, int32_t* grid) {
   for (int i = 0; i < art::N_STATS; ++i) stats[i] = g_last_stats[i];
   if (grid) *grid = g_last_grid;
   return ART_OK;
+}
+
+// Integrator-kernel durations [ms] of the last min(n, issued, RING) propagate launches on the
+// current device, oldest first (each from the HIP events around that launch on its own
+// stream); waits for them. Returns the count written, or a negative ART_E* code.
+int art_recent_kernel_ms(int32_t n, double* ms) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  DeviceCtx* c;
+  int rc = current_ctx(&c);
+  if (rc) return rc;
+  if (n < 0 || (n > 0 && !ms)) return fail(ART_E_INVALID, "bad buffer");
+  int64_t m = n;
+  if (m > c->launches) m = c->launches;
+  if (m > RING) m = RING;
+  for (int64_t j = 0; j < m; ++j) {
+    LaunchRec& L = c->ring[(int)(((int64_t)c->last - (m - 1 - j) + RING) % RING)];
+    HIP_OK(hipEventSynchronize(L.done));
+    float f = 0.f;
+    HIP_OK(hipEventElapsedTime(&f, L.ev0, L.ev1));
+    ms[j] = f;
+  }
+  return (int)m;
 }
 
 int art_vern6_tableau(double* c, double* A, double* b, double* bhat) {
@@ -406,43 +500,74 @@ int art_get_prob_nonad_host(const art_params* p, int64_t nc, const double* pos, 
   return ART_OK;
 }
 
+}  // extern "C"
+
+namespace {
+int sample_device_impl(const art_params* p, double max_r, uint64_t seed, int64_t ray_offset, int64_t n, double* x,
+                       double* k_init, double* erg_inf, double* vifty, int32_t* weights, int32_t* attempts,
+                       hipStream_t s) {
+  int rc = validate(p);
+  if (rc) return rc;
+  if (n == 0) return ART_OK;
+  if (n < 0 || n > 2147483647LL) return fail(ART_E_INVALID, "n must be in [0, 2^31)");
+  if (!(max_r > p->rNS)) return fail(ART_E_INVALID, "max_r must exceed rNS (MainRunner.jl:389-396 quits otherwise)");
+  if (!x || !k_init || !erg_inf || !vifty || !weights || !attempts) return fail(ART_E_INVALID, "NULL buffer");
+  DeviceCtx* c;
+  if ((rc = current_ctx(&c))) return rc;
+  void* q = nullptr;  // this launch's work-queue word
+  if ((rc = scratch_alloc(s, 256, &q))) return rc;
+  HIP_OK(hipMemsetAsync(q, 0, sizeof(unsigned long long), s));
+  HIP_OK(art::launch_sample(kparams(*p), max_r, seed, ray_offset, n, x, k_init, erg_inf, vifty, weights,
+                            attempts, (unsigned long long*)q, s));
+  HIP_OK(hipFreeAsync(q, s));
+  return ART_OK;
+}
+
+int event_weight_device_impl(const art_params* p, double max_r, double rho_dm, double mcmc_weight, int64_t n,
+                             const double* x, const double* k_init, const double* vifty, double* out, hipStream_t s) {
+  int rc = validate(p);
+  if (rc) return rc;
+  if (n == 0) return ART_OK;
+  if (n < 0) return fail(ART_E_INVALID, "n must be >= 0");
+  if (!x || !k_init || !vifty || !out) return fail(ART_E_INVALID, "NULL buffer");
+  DeviceCtx* c;
+  if ((rc = current_ctx(&c))) return rc;
+  HIP_OK(art::launch_event_weight(art::make_kparams(*p), n, x, k_init, vifty, max_r, rho_dm, mcmc_weight, out, s));
+  return ART_OK;
+}
+}  // namespace
+
+extern "C" {
+
 int art_sample_conversion_points_device(const art_params* p, double max_r, uint64_t seed, int64_t ray_offset,
                                         int64_t n, double* x, double* k_init, double* erg_inf, double* vifty,
                                         int32_t* weights, int32_t* attempts, void* stream) {
   std::lock_guard<std::mutex> lk(g_mu);
-  int rc = validate(p);
-  if (rc) return rc;
-  if (n == 0) return ART_OK;
-  if (n > 2147483647LL) return fail(ART_E_INVALID, "n must be < 2^31");
-  if (!(max_r > p->rNS)) return fail(ART_E_INVALID, "max_r must exceed rNS (MainRunner.jl:389-396 quits otherwise)");
-  DeviceCtx* c;
-  if ((rc = current_ctx(&c))) return rc;
-  hipStream_t s = pick(c, stream);
-  HIP_OK(hipMemsetAsync(c->scratch, 0, sizeof(unsigned long long), s));
-  HIP_OK(art::launch_sample(art::make_kparams(*p), max_r, seed, ray_offset, n, x, k_init, erg_inf, vifty, weights,
-                            attempts, c->scratch, s));
-  return ART_OK;
+  return sample_device_impl(p, max_r, seed, ray_offset, n, x, k_init, erg_inf, vifty, weights, attempts,
+                            (hipStream_t)stream);
 }
 
+// The whole stage-run-copy sequence holds the mutex, so no other thread can regrow the staging
+// buffer in between.
 int art_sample_conversion_points_host(const art_params* p, double max_r, uint64_t seed, int64_t ray_offset, int64_t n,
                                       double* x, double* k_init, double* erg_inf, double* vifty, int32_t* weights,
                                       int32_t* attempts) {
-  int rc;
+  std::lock_guard<std::mutex> lk(g_mu);
+  int rc = validate(p);
+  if (rc) return rc;
+  if (n == 0) return ART_OK;
+  if (n < 0 || n > 2147483647LL) return fail(ART_E_INVALID, "n must be in [0, 2^31)");
   DeviceCtx* c;
+  if ((rc = current_ctx(&c))) return rc;
   void* d;
   const size_t nd = (size_t)n;
-  {
-    std::lock_guard<std::mutex> lk(g_mu);
-    if ((rc = current_ctx(&c))) return rc;
-    if ((rc = pool_get(c, 4, nd * 10 * sizeof(double) + nd * 2 * sizeof(int32_t), &d))) return rc;
-  }
+  if ((rc = pool_get(c, 4, nd * 10 * sizeof(double) + nd * 2 * sizeof(int32_t), &d))) return rc;
   double* dd = (double*)d;
   int32_t* di = (int32_t*)(dd + 10 * nd);
-  if ((rc = art_sample_conversion_points_device(p, max_r, seed, ray_offset, n, dd, dd + 3 * nd, dd + 6 * nd, dd + 7 * nd,
-                                                di, di + nd, c->stream)))
-    return rc;
-  std::lock_guard<std::mutex> lk(g_mu);
   hipStream_t s = c->stream;
+  if ((rc = sample_device_impl(p, max_r, seed, ray_offset, n, dd, dd + 3 * nd, dd + 6 * nd, dd + 7 * nd, di, di + nd,
+                               s)))
+    return rc;
   HIP_OK(hipMemcpyAsync(x, dd, nd * 3 * sizeof(double), hipMemcpyDeviceToHost, s));
   HIP_OK(hipMemcpyAsync(k_init, dd + 3 * nd, nd * 3 * sizeof(double), hipMemcpyDeviceToHost, s));
   HIP_OK(hipMemcpyAsync(erg_inf, dd + 6 * nd, nd * sizeof(double), hipMemcpyDeviceToHost, s));
@@ -456,41 +581,30 @@ int art_sample_conversion_points_host(const art_params* p, double max_r, uint64_
 int art_event_weight_device(const art_params* p, double max_r, double rho_dm, double mcmc_weight, int64_t n,
                             const double* x, const double* k_init, const double* vifty, double* out, void* stream) {
   std::lock_guard<std::mutex> lk(g_mu);
-  int rc = validate(p);
-  if (rc) return rc;
-  if (n == 0) return ART_OK;
-  if (!x || !k_init || !vifty || !out) return fail(ART_E_INVALID, "NULL buffer");
-  DeviceCtx* c;
-  if ((rc = current_ctx(&c))) return rc;
-  HIP_OK(art::launch_event_weight(art::make_kparams(*p), n, x, k_init, vifty, max_r, rho_dm, mcmc_weight, out,
-                                  pick(c, stream)));
-  return ART_OK;
+  return event_weight_device_impl(p, max_r, rho_dm, mcmc_weight, n, x, k_init, vifty, out, (hipStream_t)stream);
 }
 
 int art_event_weight_host(const art_params* p, double max_r, double rho_dm, double mcmc_weight, int64_t n,
                           const double* x, const double* k_init, const double* vifty, double* out) {
-  int rc;
+  std::lock_guard<std::mutex> lk(g_mu);
+  int rc = validate(p);
+  if (rc) return rc;
+  if (n == 0) return ART_OK;
+  if (n < 0) return fail(ART_E_INVALID, "n must be >= 0");
   DeviceCtx* c;
+  if ((rc = current_ctx(&c))) return rc;
   void* d;
   const size_t nd = (size_t)n;
-  if (n == 0) return ART_OK;
-  {
-    std::lock_guard<std::mutex> lk(g_mu);
-    if ((rc = current_ctx(&c))) return rc;
-    if ((rc = pool_get(c, 5, nd * 14 * sizeof(double), &d))) return rc;
-    double* dd = (double*)d;
-    hipStream_t s = c->stream;
-    HIP_OK(hipMemcpyAsync(dd, x, nd * 3 * sizeof(double), hipMemcpyHostToDevice, s));
-    HIP_OK(hipMemcpyAsync(dd + 3 * nd, k_init, nd * 3 * sizeof(double), hipMemcpyHostToDevice, s));
-    HIP_OK(hipMemcpyAsync(dd + 6 * nd, vifty, nd * 3 * sizeof(double), hipMemcpyHostToDevice, s));
-  }
+  if ((rc = pool_get(c, 5, nd * 14 * sizeof(double), &d))) return rc;
   double* dd = (double*)d;
-  if ((rc = art_event_weight_device(p, max_r, rho_dm, mcmc_weight, n, dd, dd + 3 * nd, dd + 6 * nd, dd + 9 * nd,
-                                    c->stream)))
+  hipStream_t s = c->stream;
+  HIP_OK(hipMemcpyAsync(dd, x, nd * 3 * sizeof(double), hipMemcpyHostToDevice, s));
+  HIP_OK(hipMemcpyAsync(dd + 3 * nd, k_init, nd * 3 * sizeof(double), hipMemcpyHostToDevice, s));
+  HIP_OK(hipMemcpyAsync(dd + 6 * nd, vifty, nd * 3 * sizeof(double), hipMemcpyHostToDevice, s));
+  if ((rc = event_weight_device_impl(p, max_r, rho_dm, mcmc_weight, n, dd, dd + 3 * nd, dd + 6 * nd, dd + 9 * nd, s)))
     return rc;
-  std::lock_guard<std::mutex> lk(g_mu);
-  HIP_OK(hipMemcpyAsync(out, dd + 9 * nd, nd * 5 * sizeof(double), hipMemcpyDeviceToHost, c->stream));
-  HIP_OK(hipStreamSynchronize(c->stream));
+  HIP_OK(hipMemcpyAsync(out, dd + 9 * nd, nd * 5 * sizeof(double), hipMemcpyDeviceToHost, s));
+  HIP_OK(hipStreamSynchronize(s));
   return ART_OK;
 }
 
@@ -505,6 +619,20 @@ int art_flux_histogram_device(const art_params* p, int64_t n, const double* x_en
   DeviceCtx* c;
   if ((rc = current_ctx(&c))) return rc;
   HIP_OK(art::launch_flux(art::make_kparams(*p), n, x_end, k_end, status, species, w, nbins, hist, pick(c, stream)));
+  return ART_OK;
+}
+
+int art_flux_histogram_phi_device(int64_t n, const double* phi, const int8_t* species, const double* w, int32_t nbins,
+                                  double* hist, void* stream) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (nbins < 1 || nbins > 4096) return fail(ART_E_INVALID, "nbins must be in [1, 4096]");
+  if (n < 0) return fail(ART_E_INVALID, "n must be >= 0");
+  if (n == 0) return ART_OK;
+  if (!phi || !hist) return fail(ART_E_INVALID, "NULL buffer");
+  DeviceCtx* c;
+  int rc = current_ctx(&c);
+  if (rc) return rc;
+  HIP_OK(art::launch_flux_phi(n, phi, species, w, nbins, hist, (hipStream_t)stream));
   return ART_OK;
 }
 
@@ -542,6 +670,116 @@ int art_eval_condition_device(const art_params* p, int64_t n, const double* u, c
   if ((rc = current_ctx(&c))) return rc;
   HIP_OK(art::launch_eval_condition(art::make_kparams(*p), n, u, tau, out, pick(c, stream)));
   return ART_OK;
+}
+
+// ---- the radiated-flux reduction across ranks: one RCCL all-reduce ----
+// RCCL is opened at first use (dlopen), so libart.so loads and runs single-GPU work where it
+// is absent; a process that already loaded librccl.so.1 (e.g. PyTorch's) shares that copy.
+}  // extern "C"
+
+namespace {
+typedef int (*nccl_get_id_t)(void*);
+typedef int (*nccl_init_rank_t)(void**, int, art_rccl_id, int);
+typedef int (*nccl_allreduce_t)(const void*, void*, size_t, int, int, void*, hipStream_t);
+typedef int (*nccl_destroy_t)(void*);
+typedef const char* (*nccl_err_t)(int);
+struct Rccl {
+  void* h = nullptr;
+  nccl_get_id_t get_id = nullptr;
+  nccl_init_rank_t init_rank = nullptr;
+  nccl_allreduce_t allreduce = nullptr;
+  nccl_destroy_t destroy = nullptr;
+  nccl_err_t err = nullptr;
+  void* comm = nullptr;
+  int device = -1;
+};
+Rccl g_rccl;
+constexpr int NCCL_FLOAT64 = 8;  // ncclFloat64 (rccl.h)
+constexpr int NCCL_SUM = 0;      // ncclSum
+
+int rccl_open() {
+  if (g_rccl.h) return ART_OK;
+  void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+  if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_GLOBAL);
+  if (!h) return fail(ART_E_UNSUPPORTED, "RCCL (librccl.so.1) is not available: %s", dlerror());
+  g_rccl.get_id = (nccl_get_id_t)dlsym(h, "ncclGetUniqueId");
+  g_rccl.init_rank = (nccl_init_rank_t)dlsym(h, "ncclCommInitRank");
+  g_rccl.allreduce = (nccl_allreduce_t)dlsym(h, "ncclAllReduce");
+  g_rccl.destroy = (nccl_destroy_t)dlsym(h, "ncclCommDestroy");
+  g_rccl.err = (nccl_err_t)dlsym(h, "ncclGetErrorString");
+  if (!g_rccl.get_id || !g_rccl.init_rank || !g_rccl.allreduce || !g_rccl.destroy || !g_rccl.err)
+    return fail(ART_E_UNSUPPORTED, "librccl.so.1 lacks the nccl* entry points");
+  g_rccl.h = h;
+  return ART_OK;
+}
+
+int rccl_fail(int r, const char* what) {
+  return fail(ART_E_HIP, "%s: %s", what, g_rccl.err ? g_rccl.err(r) : "RCCL error");
+}
+}  // namespace
+
+extern "C" {
+
+int art_comm_unique_id(art_rccl_id* id) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (!id) return fail(ART_E_INVALID, "id is NULL");
+  int rc = rccl_open();
+  if (rc) return rc;
+  const int r = g_rccl.get_id(id);
+  return r ? rccl_fail(r, "ncclGetUniqueId") : ART_OK;
+}
+
+int art_comm_init(int32_t rank, int32_t world, const art_rccl_id* id) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (!id || world < 1 || rank < 0 || rank >= world) return fail(ART_E_INVALID, "bad rank/world/id");
+  if (g_rccl.comm) return fail(ART_E_INVALID, "communicator already initialised (art_comm_destroy first)");
+  int rc = rccl_open();
+  if (rc) return rc;
+  int dev = 0;
+  HIP_OK(hipGetDevice(&dev));
+  void* comm = nullptr;
+  const int r = g_rccl.init_rank(&comm, world, *id, rank);
+  if (r) return rccl_fail(r, "ncclCommInitRank");
+  g_rccl.comm = comm;
+  g_rccl.device = dev;
+  return ART_OK;
+}
+
+int art_flux_allreduce(double* buf, int64_t count, void* stream) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (!g_rccl.comm) return fail(ART_E_INVALID, "no communicator: art_comm_init first");
+  if (count < 0 || (count > 0 && !buf)) return fail(ART_E_INVALID, "bad buffer");
+  if (count == 0) return ART_OK;
+  const int r = g_rccl.allreduce(buf, buf, (size_t)count, NCCL_FLOAT64, NCCL_SUM, g_rccl.comm, (hipStream_t)stream);
+  return r ? rccl_fail(r, "ncclAllReduce") : ART_OK;
+}
+
+// The same for a host buffer (a Julia host's Vector{Float64}): staged through HBM on the
+// library's stream, reduced, copied back; synchronous.
+int art_flux_allreduce_host(double* buf, int64_t count) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (!g_rccl.comm) return fail(ART_E_INVALID, "no communicator: art_comm_init first");
+  if (count < 0 || (count > 0 && !buf)) return fail(ART_E_INVALID, "bad buffer");
+  if (count == 0) return ART_OK;
+  DeviceCtx* c;
+  int rc = current_ctx(&c);
+  if (rc) return rc;
+  void* d;
+  if ((rc = pool_get(c, 8, (size_t)count * sizeof(double), &d))) return rc;
+  HIP_OK(hipMemcpyAsync(d, buf, (size_t)count * sizeof(double), hipMemcpyHostToDevice, c->stream));
+  const int r = g_rccl.allreduce(d, d, (size_t)count, NCCL_FLOAT64, NCCL_SUM, g_rccl.comm, c->stream);
+  if (r) return rccl_fail(r, "ncclAllReduce");
+  HIP_OK(hipMemcpyAsync(buf, d, (size_t)count * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  HIP_OK(hipStreamSynchronize(c->stream));
+  return ART_OK;
+}
+
+int art_comm_destroy(void) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (!g_rccl.comm) return ART_OK;
+  const int r = g_rccl.destroy(g_rccl.comm);
+  g_rccl.comm = nullptr;
+  return r ? rccl_fail(r, "ncclCommDestroy") : ART_OK;
 }
 
 }  // extern "C"

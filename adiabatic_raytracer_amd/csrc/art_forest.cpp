@@ -180,6 +180,7 @@ int grow_trees_impl(const art_params* p, int64_t n, const double* x0, const doub
 
     // ---- crossings of each segment: merge near-duplicates, probabilities ----
     std::vector<std::vector<Cross>> xcs((size_t)m);
+    std::vector<char> rare((size_t)m, 0);  // the "rare fail" |kc| > 1 (:213-225), before the merge (:227)
     std::vector<int64_t> gstart(1, 0);
     std::vector<double> gpos, gk, ge;
     for (int64_t j = 0; j < m; ++j) {
@@ -195,6 +196,7 @@ int grow_trees_impl(const art_params* p, int64_t n, const double* x0, const doub
         c.dw = cdw[(int64_t)q * m + j];
         c.P = 1.0 - std::exp(-cpn[(int64_t)q * m + j]);  // Nc = 1 semantics (forward trees)
         L.push_back(c);
+        for (int a = 0; a < 3; ++a) rare[j] = rare[j] || std::abs(c.k[a]) > 1.0;
       }
       if (L.size() > 1) {  // two crossings at the same point are one (:227-245)
         std::vector<Cross> keep;
@@ -268,10 +270,7 @@ int grow_trees_impl(const art_params* p, int64_t n, const double* x0, const doub
         const double rr = std::sqrt(e.x_end[0] * e.x_end[0] + e.x_end[1] * e.x_end[1] + e.x_end[2] * e.x_end[2]);
         if (rr > rNS * 1.1) e.is_final = 1;
       } else {
-        bool rare = false;  // (:213-225)
-        for (const Cross& c : L)
-          for (int a = 0; a < 3; ++a) rare = rare || std::abs(c.k[a]) > 1.0;
-        if (rare) {
+        if (rare[j]) {  // (:213-225), judged on the unmerged crossings
           T.done.push_back(e);
           T.tot_prob += e.weight;
           continue;  // no stop checks, no sort (the reference's `continue`)
@@ -280,7 +279,7 @@ int grow_trees_impl(const art_params* p, int64_t n, const double* x0, const doub
         const double P1 = L[0].P;
         if (!split_all) {
           if (T.count > opts->mc_nodes) {  // pure MC (:281-292)
-            const double r = mc_uniform(opts->seed, (uint64_t)idx[j], (uint32_t)T.count);
+            const double r = mc_uniform(opts->seed, (uint64_t)(opts->tree_offset + idx[j]), (uint32_t)T.count);
             if (r < P1)
               T.events.push_back(make_child(L[0], new_species, P1, e.weight, e.weight, P1, P1));
             else

@@ -377,6 +377,8 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
                                                                               unsigned long long* __restrict__ stats) {
   const KParams P = specialize<GEOM>(P_in);
   constexpr bool RK4 = (INTEG == ART_RK4);
+  // the callbacks (RayTracer.jl:357-368) are installed only when make_tree (:361-377)
+  const bool cbs = max_crossings != ART_NO_CALLBACKS;
   constexpr int NSLOT = RK4 ? 4 : 8;
   const StageTable& T = RK4 ? c_rk4 : c_vern6;
   __shared__ double lds[LDS_SLOTS * 7 * BLOCK];  // [slot][component][lane]: conflict-free ds_read_b64
@@ -624,7 +626,10 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
     //     known without evaluating them; its end value is not needed unless the next step
     //     opens a bracket at its start (then it is recomputed there, bit-identically:
     //     cprev_ok = false).
-    const int ccode = scan ? scan_certified_code(P, u, f, y, kk, hs, lastv[threadIdx.x], lastt[threadIdx.x]) : 0;
+    // without callbacks (make_tree = false: ART_NO_CALLBACKS) every step is "certified NaN":
+    // no sign change can open a bracket, so nothing is scanned or recorded
+    const int ccode = !scan ? 0
+                      : (cbs ? scan_certified_code(P, u, f, y, kk, hs, lastv[threadIdx.x], lastt[threadIdx.x]) : 3);
     const bool cert = ccode != 0;
     s_cert += cert ? 1u : 0u;
     // every lane parks (u, f, y, kk, h, τ) in its LDS slots (free after the error estimate):
@@ -983,7 +988,7 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
       sprev = last_s;
       just_evented = false;
       dt = dtnext;
-      if (photon && u[0] < P.rNS101) finish = ART_STATUS_HIT_NS;  // cb_r (:352-368)
+      if (cbs && photon && u[0] < P.rNS101) finish = ART_STATUS_HIT_NS;  // cb_r (:352-368)
       else if (last) finish = ART_STATUS_SUCCESS;
       else if (iter >= P.maxiters) finish = ART_STATUS_MAXITERS;
     }
@@ -1156,7 +1161,7 @@ __global__ __launch_bounds__(256) void sample_kernel(const KParams P, const doub
   const int nsteps = (int)ceil(send / 0.5);
   const int np = 20;  // ContinuousCallback(interp_points=20) (:1603)
   // certified-negative scan steps (below): GJ plasma without a boundary layer only
-  const bool cert_ok = !(P.bndry_lyr > 0.0) && P.mass_a > 0.0;
+  const bool cert_ok = !(P.bndry_lyr > 0.0) && P.mass_a > 0.0 && P.cert_fac < 1e300;  // ART_SCAN_CERT=0: off
   const double cert_lhs = 2.0 * P.wp2n, cert_rhs = P.mass_a2 * (1.0 - 1e-6);
   while (true) {
     if (!exhausted) {
@@ -1343,6 +1348,25 @@ __global__ __launch_bounds__(256) void prob_kernel(const KParams P, const int64_
   }
 }
 
+// np.histogram's bin of x for `nbins` equal bins over [-π, π] (numpy 2.x histogram: the
+// index from (x - lo) / (hi - lo) * nbins, then corrected against the edges of
+// linspace(lo, hi, nbins + 1) = i * ((hi - lo) / nbins) + lo, the right edge in the last bin),
+// with the same roundings: no contraction into FMAs. -1 outside [lo, hi] (and for NaN).
+__device__ inline int np_hist_bin(double x, int nbins) {
+#pragma clang fp contract(off)  // numpy rounds every product and sum (HIP's __dmul_rn would still fuse)
+  const double lo = -PI, hi = PI;
+  if (!(x >= lo && x <= hi)) return -1;
+  const double span = hi - lo;
+  int i = (int)(((x - lo) / span) * (double)nbins);
+  if (i == nbins) i -= 1;
+  const double step = span / (double)nbins;
+  const double e0 = (double)i * step + lo;
+  if (x < e0) i -= 1;
+  const double e1 = (i + 1 == nbins) ? hi : (double)(i + 1) * step + lo;
+  if (x >= e1 && i != nbins - 1) i += 1;
+  return i;
+}
+
 // ---------------------------------------------------------------------------
 // Binned flux (plot/flux.py:38-48): φf = atan2(k_y, k_x) of final particles, per species.
 __global__ __launch_bounds__(256) void flux_kernel(const KParams P, const int64_t n, const double* __restrict__ x_end,
@@ -1356,9 +1380,27 @@ __global__ __launch_bounds__(256) void flux_kernel(const KParams P, const int64_
     const double xr = sqrt(x_end[i] * x_end[i] + x_end[n + i] * x_end[n + i] + x_end[2 * n + i] * x_end[2 * n + i]);
     // is_final: no crossing and escaped beyond 1.1 rNS (MainRunner.jl:203-209)
     if (status[i] == ART_STATUS_CROSSING || !(xr > 1.1 * P.rNS)) continue;
-    const double phi = atan2(k_end[n + i], k_end[i]);
-    int bin = (int)floor((phi + PI) / (2.0 * PI) * nbins);
-    bin = bin < 0 ? 0 : (bin >= nbins ? nbins - 1 : bin);
+    const int bin = np_hist_bin(atan2(k_end[n + i], k_end[i]), nbins);  // np.histogram(range = (-π, π))
+    if (bin < 0) continue;
+    const int row = (species && species[i] == ART_AXION) ? 0 : 1;
+    atomicAdd(&sh[row * nbins + bin], w ? w[i] : 1.0);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 2 * nbins; i += blockDim.x)
+    if (sh[i] != 0.0) atomicAdd(&hist[i], sh[i]);
+}
+
+// Binned flux of npy rows (plot/flux.py:38-48): histogram of the given φf with weights w.
+__global__ __launch_bounds__(256) void flux_phi_kernel(const int64_t n, const double* __restrict__ phi,
+                                                       const int8_t* __restrict__ species,
+                                                       const double* __restrict__ w, const int32_t nbins,
+                                                       double* __restrict__ hist) {
+  extern __shared__ __attribute__((aligned(16))) double sh[];
+  for (int i = threadIdx.x; i < 2 * nbins; i += blockDim.x) sh[i] = 0.0;
+  __syncthreads();
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int bin = np_hist_bin(phi[i], nbins);
+    if (bin < 0) continue;
     const int row = (species && species[i] == ART_AXION) ? 0 : 1;
     atomicAdd(&sh[row * nbins + bin], w ? w[i] : 1.0);
   }
@@ -1493,6 +1535,16 @@ hipError_t launch_flux(const KParams& P, int64_t n, const double* x_end, const d
   if (grid < 1) grid = 1;
   hipLaunchKernelGGL(flux_kernel, dim3((unsigned)grid), dim3(256), 2 * nbins * sizeof(double), s, P, n, x_end, k_end,
                      status, species, w, nbins, hist);
+  return hipGetLastError();
+}
+
+hipError_t launch_flux_phi(int64_t n, const double* phi, const int8_t* species, const double* w, int32_t nbins,
+                           double* hist, hipStream_t s) {
+  int64_t grid = (n + 255) / 256;
+  if (grid > 1024) grid = 1024;
+  if (grid < 1) grid = 1;
+  hipLaunchKernelGGL(flux_phi_kernel, dim3((unsigned)grid), dim3(256), 2 * nbins * sizeof(double), s, n, phi, species, w,
+                     nbins, hist);
   return hipGetLastError();
 }
 

@@ -23,6 +23,8 @@ import numpy as np
 from . import _lib
 from ._lib import ART_AXION, ART_PHOTON, ART_RK4, ART_VERN6, ArtParams, CrossingBuf, SegmentOut, check
 
+ART_NO_CALLBACKS = -(2 ** 31)  # include/art.h: max_crossings for make_tree = false
+
 # Constants.jl:3-5
 c_km = 2.99792e5
 hbar = 6.582119e-16
@@ -119,13 +121,24 @@ def _soa(a, n):
     return np.ascontiguousarray(a.T).reshape(-1)  # Julia column-major N x 3
 
 
-def propagate(x0, k0, nsteps, Mvars, NumerP, rhs=func_photon, make_tree=True, is_axion=False, Mass_a=1e-6,
-              max_crossings=3, Δω=-1.0, *, Ax_g=1e-12, capacity=None, **numerics) -> Propagated:
+class PropagatedPlain(NamedTuple):
+    """RayTracer.jl:450's 4-tuple (make_tree = false), final saved point only."""
+    x: np.ndarray          # (N, 3, 1)
+    v: np.ndarray          # (N, 3, 1)
+    dt: np.ndarray         # (N, 1)
+    fail: np.ndarray       # (N,)
+
+
+def propagate(x0, k0, nsteps, Mvars, NumerP, rhs=func_photon, make_tree=False, is_axion=False, Mass_a=1e-6,
+              max_crossings=3, Δω=-1.0, *, Ax_g=1e-12, capacity=None, **numerics):
     """Batched RT.propagate (RayTracer.jl:171-452): integrate N segments on the GPU.
 
-    Arguments keep the reference's meaning; `nsteps` only controls saved interior points
-    in the reference (saveat) and does not influence the integration, so only the final
-    point is returned. `Mass_a` is taken from Mvars, as the reference does."""
+    Arguments keep the reference's meaning and defaults; `nsteps` only controls saved
+    interior points in the reference (saveat) and does not influence the integration, so
+    only the final point is returned. `Mass_a` is taken from Mvars, as the reference does.
+    make_tree = true installs the resonance callback (and, for photons, the NS cut) and
+    returns the 14-tuple (:448, as `Propagated`, with status / step counts / P per row);
+    make_tree = false integrates with no callbacks and returns the 4-tuple (:450)."""
     del nsteps, Mass_a
     if (rhs == func_axion) != bool(is_axion):
         raise ValueError("rhs and is_axion disagree (func_axion! <=> is_axion)")
@@ -137,8 +150,13 @@ def propagate(x0, k0, nsteps, Mvars, NumerP, rhs=func_photon, make_tree=True, is
     lnt = np.full(n, ln_t0)
     species = np.full(n, ART_AXION if is_axion else ART_PHOTON, np.int8)
     res = propagate_batch(params, _soa(x0, n), _soa(k0, n), erg, dw, lnt, species,
-                          max_crossings=max_crossings if make_tree else 0x7FFFFFFF,
-                          capacity=capacity or (1 if max_crossings <= 1 else min(int(max_crossings), 64)))
+                          max_crossings=max_crossings if make_tree else ART_NO_CALLBACKS,
+                          capacity=capacity or (1 if max_crossings <= 1 or not make_tree else min(int(max_crossings), 64)))
+    xe, ke = res["x_end"].reshape(3, n).T, res["k_end"].reshape(3, n).T
+    r_end = np.linalg.norm(xe, axis=1)
+    fail = np.where(r_end <= params.rNS * 1.01, 0.0, 1.0)  # fail_indx (:436-437)
+    if not make_tree:
+        return PropagatedPlain(x=xe[:, :, None], v=ke[:, :, None], dt=res["u7_end"][:, None], fail=fail)
     cap = res["capacity"]
     cnt = np.minimum(res["n_cross"], cap)
 
@@ -148,11 +166,8 @@ def propagate(x0, k0, nsteps, Mvars, NumerP, rhs=func_photon, make_tree=True, is
     def sc(a, i):
         return np.array([a[j * n + i] for j in range(cnt[i])])
 
-    xe, ke = res["x_end"].reshape(3, n).T, res["k_end"].reshape(3, n).T
-    r_end = np.linalg.norm(xe, axis=1)
     return Propagated(
-        x=xe[:, :, None], v=ke[:, :, None], dt=res["u7_end"][:, None],
-        fail=np.where(r_end <= params.rNS * 1.01, 0.0, 1.0), cut_short=res["status"] == 1,
+        x=xe[:, :, None], v=ke[:, :, None], dt=res["u7_end"][:, None], fail=fail, cut_short=res["status"] == 1,
         xc=[col(res["xc_pos"], 0, i) for i in range(n)], yc=[col(res["xc_pos"], 1, i) for i in range(n)],
         zc=[col(res["xc_pos"], 2, i) for i in range(n)], kxc=[col(res["xc_k"], 0, i) for i in range(n)],
         kyc=[col(res["xc_k"], 1, i) for i in range(n)], kzc=[col(res["xc_k"], 2, i) for i in range(n)],

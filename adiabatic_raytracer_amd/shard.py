@@ -26,6 +26,18 @@ def allreduce_flux(hist, world: int):
     return hist
 
 
+def allreduce_sum(values):
+    """Element-wise sum of a float64 vector over all ranks (torch.distributed: RCCL on the GPU
+    for the nccl backend, gloo on the CPU). Returns a numpy array."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" else torch.device("cpu")
+    t = torch.as_tensor(np.asarray(values, np.float64)).to(dev)
+    dist.all_reduce(t)
+    return t.cpu().numpy()
+
+
 def reduce_totals(steps: float, elapsed_s: float, rays: int, world: int, device=None):
     """(Σ steps, max wall time, Σ rays) over ranks."""
     import torch

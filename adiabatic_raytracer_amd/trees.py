@@ -37,13 +37,14 @@ NODE_DTYPE = np.dtype([
 
 
 def grow_trees(params: Params, x0, k0, erg, species, *, num_cutoff=5, mc_nodes=5, max_nodes=50,
-               splittings_cutoff=-1, crossing_cap=64, prob_cutoff=1e-10, seed=1769, ntimes=None):
+               splittings_cutoff=-1, crossing_cap=64, prob_cutoff=1e-10, seed=1769, ntimes=None, tree_offset=0):
     """get_tree for n roots RT.node(x0, k0, 0, -1, species, 1, 1, -1, -1, -1) (MainRunner.jl:578-590,
     :653-667). x0, k0: (n, 3) or SoA 3n; erg: erg_inf_ini per root. Returns (nodes, counts,
     infos): nodes is a NODE_DTYPE record array grouped by tree in get_tree's push order.
     With ntimes (>= 2, saveMode 3) a fourth item holds every node's saveNode data
     (art_grow_trees_traj): traj (nodes, ntimes, 3) Cartesian saved points, times (nodes,
-    ntimes) their ln t, count (nodes,), xc (nodes, cap, 4) the kept crossings (x, y, z, tc)."""
+    ntimes) their ln t, count (nodes,), xc (nodes, cap, 4) the kept crossings (x, y, z, tc).
+    tree_offset: global id of root 0 (the Monte-Carlo draws are keyed by the global tree id)."""
     x0, k0 = np.asarray(x0, np.float64), np.asarray(k0, np.float64)
     erg = np.ascontiguousarray(erg, np.float64).reshape(-1)
     n = erg.size
@@ -51,7 +52,8 @@ def grow_trees(params: Params, x0, k0, erg, species, *, num_cutoff=5, mc_nodes=5
         x0, k0 = x0.T, k0.T
     x0, k0 = np.ascontiguousarray(x0).reshape(-1), np.ascontiguousarray(k0).reshape(-1)
     sp = np.ascontiguousarray(np.broadcast_to(np.asarray(species, np.int8), (n,)))
-    opts = TreeOpts(num_cutoff, mc_nodes, max_nodes, splittings_cutoff, crossing_cap, 0, prob_cutoff, seed)
+    opts = TreeOpts(num_cutoff, mc_nodes, max_nodes, splittings_cutoff, crossing_cap, int(tree_offset), prob_cutoff,
+                    seed)
     per_tree = 1 if (splittings_cutoff > 0 and num_cutoff <= 0) else max_nodes + 2
     cap = max(1, n * per_tree)
     lib = _lib.load()
@@ -108,7 +110,8 @@ def tree_file_name(dir_tag, Mass_a, Ax_g, θm, ωPul, B0, Ntajs, ntimes, num_cut
     return os.path.join(dir_tag, "npy", name)
 
 
-def _write_event_text(dir_tag, file_tag, n_ev, s, w, x, k, tree, fin, ev, wgt, ident, counts, elapsed=None):
+def _write_event_text(dir_tag, file_tag, n_ev, s, w, x, k, tree, fin, ev, wgt, ident, counts, elapsed=None,
+                      ev_offset=0):
     """event_<file_tag> and final_<file_tag> of saveMode > 1 (MainRunner.jl:438-444, 592-609,
     690-702, 735-741), Julia number formatting. The reference's per-event wall time
     time() - time0 has no per-event meaning in a batched run; the mean per event is written."""
@@ -119,7 +122,7 @@ def _write_event_text(dir_tag, file_tag, n_ev, s, w, x, k, tree, fin, ev, wgt, i
     with open(os.path.join(d, "event_" + file_tag), "w") as fe:
         for i in range(n_ev):
             vals = [*v[i], w["sln_prob"][i], *x[i], *(-k[i]), *x[i], *k[i]]
-            fe.write(f"{i + 1} " + " ".join(jl(a) for a in vals) + f" {jl(t_ev)} {int(counts[i])}\n")
+            fe.write(f"{ev_offset + i + 1} " + " ".join(jl(a) for a in vals) + f" {jl(t_ev)} {int(counts[i])}\n")
     θf, ϕf, absf = _angles(fin["k_end"])
     θfX, ϕfX, absfX = _angles(fin["x_end"])
     # node.t: the root's is the integer literal 0 of RT.node(..., 0, ...) (MainRunner.jl:661)
@@ -130,7 +133,7 @@ def _write_event_text(dir_tag, file_tag, n_ev, s, w, x, k, tree, fin, ev, wgt, i
         for q in range(len(fin)):
             t = "0" if is_root[q] else jl(fin["t0"][q])
             vals = [θf[q], ϕf[q], absf[q], θfX[q], ϕfX[q], absfX[q]]
-            ff.write(f"{int(ev[q]) + 1} {jl(wgt[q])} {int(ident[q])} " + " ".join(jl(a) for a in vals) + f" {t}\n")
+            ff.write(f"{ev_offset + int(ev[q]) + 1} {jl(wgt[q])} {int(ident[q])} " + " ".join(jl(a) for a in vals) + f" {t}\n")
 
 
 SPECIES_NAME = {AXION: "axion", PHOTON: "photon"}
@@ -158,23 +161,42 @@ def save_node(fh, node, tr, q):
 
 def main_runner_tree(params: Params, Ntajs: int, *, seed=1769, ntimes=1000, rho_DM=0.45, n_maxSample=6,
                      num_cutoff=5, MC_nodes=5, max_nodes=50, prob_cutoff=1e-10, saveMode=0, dir_tag=None,
-                     file_tag="", backtrace_cap=256):
+                     file_tag="", backtrace_cap=256, rank=0, world=1, nbins=50, run_info=None):
     """main_runner_tree (MainRunner.jl:354-763) for Ntajs - 1 events (the reference's
     `while photon_trajs < desired_trajs` loop), all events batched on the GPU. Returns the
     row matrix (13 columns, 29 with saveMode > 0) after the final division of column 8 by
     f_inx, and writes it to the reference's npy path when dir_tag is given; saveMode > 1
     also writes the event_/final_ text files and saveMode > 2 one tree_<file_tag><event>
     file per event with saveNode of the backtrace node and of every forward-tree node
-    (MainRunner.jl:573-577, :612, :671), each segment saved at ntimes points."""
+    (MainRunner.jl:573-577, :612, :671), each segment saved at ntimes points.
+
+    Sharding, world > 1 with torch.distributed initialised (one process per
+    GPU): the Ntajs - 1 events of ONE logical run are split by global event id
+    (shard.shard_range). Rank r samples its block (Philox keyed by the global event id),
+    backtraces it and grows its trees (Monte-Carlo draws keyed by the global tree id), and
+    numbers its rows by global event id, so the ranks' rows in rank order are the
+    single-process rows. f_inx (MainRunner.jl:469,477,711-713) is all-reduced and column 8
+    is divided by the GLOBAL f_inx (:747): the normalisation of one large run, not the
+    per-file /Nruns of Gen_Samples.jl:220. Rank r writes file_tag + str(r) (:750-761).
+
+    run_info (a dict, optional) receives the run's reduced totals: f_inx (global), the
+    binned radiated flux of plot/flux.py:38-48 -- np.histogram(φf, nbins, range=(-π, π),
+    weights = weight * sln_prob) of the rows, axions in flux[0], photons in flux[1], after
+    the f_inx division, binned on the GPU and summed over ranks in the same all-reduce --
+    Σ weight * sln_prob per species and the global row count."""
     if saveMode < 3:
         ntimes = 3  # "Times to store in ODE" (MainRunner.jl:379-381): also names the npy file
     import time
+    from .shard import allreduce_sum, shard_range
     t_start = time.perf_counter()
-    n_ev = max(0, int(Ntajs) - 1)
+    n_glob = max(0, int(Ntajs) - 1)
+    lo, hi = shard_range(n_glob, rank, world)
+    n_ev = hi - lo
+    tag = f"{file_tag}{rank}" if world > 1 else file_tag
     max_r = params.max_r()
     if max_r < params.rNS:
         raise ValueError("maxR < rNS: this neutron star has no conversion surface (MainRunner.jl:387-396)")
-    s = sample_conversion_points(params, n_ev, seed=seed, max_r=max_r)
+    s = sample_conversion_points(params, n_ev, seed=seed, ray_offset=lo, max_r=max_r)
     w = event_weight(params, s["x"], s["k_init"], s["vifty"], max_r=max_r, rho_DM=rho_DM, n_maxSample=n_maxSample)
     x = s["x"].reshape(3, n_ev).T
     k = s["k_init"].reshape(3, n_ev).T
@@ -184,19 +206,20 @@ def main_runner_tree(params: Params, Ntajs: int, *, seed=1769, ntimes=1000, rho_
     # backtrace: axion, -k, -B0, every crossing, only the root is processed (:578-590)
     dumps = saveMode > 2 and dir_tag is not None
     got = grow_trees(replace(params, B0=-params.B0), x, -k, erg, AXION, num_cutoff=0, splittings_cutoff=100000,
-                     crossing_cap=backtrace_cap, prob_cutoff=prob_cutoff, seed=seed, ntimes=ntimes if dumps else None)
+                     crossing_cap=backtrace_cap, prob_cutoff=prob_cutoff, seed=seed, ntimes=ntimes if dumps else None,
+                     tree_offset=lo)
     nb, c_bck = got[0], got[1]
     samp_back_weight = nb["prob"] * nb["weight"]  # (:635)
     prob0 = nb["prob"]
     # forward photon tree from the sample (:653-667)
     fwd = grow_trees(params, x, k, erg, PHOTON, num_cutoff=num_cutoff, mc_nodes=MC_nodes, max_nodes=max_nodes,
-                     prob_cutoff=prob_cutoff, seed=seed, ntimes=ntimes if dumps else None)
+                     prob_cutoff=prob_cutoff, seed=seed, ntimes=ntimes if dumps else None, tree_offset=lo)
     tree, counts, infos = fwd[:3]
     if dumps:  # saveMode > 2: one file per event, the backtrace node then the forward tree
         d = os.path.join(dir_tag, "tree")
         os.makedirs(d, exist_ok=True)
         for e in range(n_ev):
-            with open(os.path.join(d, f"tree_{file_tag}{e + 1}"), "w") as fh:
+            with open(os.path.join(d, f"tree_{file_tag}{lo + e + 1}"), "w") as fh:
                 save_node(fh, nb[e], got[3], e)
                 for q in np.flatnonzero(tree["tree"] == e):
                     save_node(fh, tree[q], fwd[3], q)
@@ -208,7 +231,7 @@ def main_runner_tree(params: Params, Ntajs: int, *, seed=1769, ntimes=1000, rho_
     ident = np.where(fin["species"] == AXION, 0.0, 1.0)
     f_inx += int(np.sum(ident == 1.0))
     dω = fin["u7_end"] / params.mass_a + w["vel_eng"][ev]  # (:713)
-    photon_trajs = ev + 1.0
+    photon_trajs = lo + ev + 1.0  # global event number
     cols = [photon_trajs, ident, θf, ϕf, θfX, ϕfX, absfX, w["sln_prob"][ev], wgt, x[ev, 0], x[ev, 1], x[ev, 2], dω]
     if saveMode > 0:
         zero = np.zeros_like(wgt)
@@ -217,16 +240,57 @@ def main_runner_tree(params: Params, Ntajs: int, *, seed=1769, ntimes=1000, rho_
                  absfX, c_bck[ev].astype(float), prob0[ev]]
     rows = np.stack(cols, axis=1) if len(fin) else np.zeros((0, len(cols)))
     if saveMode > 1 and dir_tag is not None:
-        _write_event_text(dir_tag, file_tag, n_ev, s, w, x, k, tree, fin, ev, wgt, ident, counts,
-                          elapsed=time.perf_counter() - t_start)
+        _write_event_text(dir_tag, tag, n_ev, s, w, x, k, tree, fin, ev, wgt, ident, counts,
+                          elapsed=time.perf_counter() - t_start, ev_offset=lo)
+    # the run's totals: [flux (2 nbins, weight * sln_prob before the f_inx division) | f_inx |
+    # Σ weight * sln_prob (axions, photons) | rows], ONE sum over the ranks
+    flux = radiated_flux(rows[:, 3], rows[:, 1], rows[:, 8] * rows[:, 7], nbins) if len(rows) else np.zeros(2 * nbins)
+    pps = rows[:, 8] * rows[:, 7] if len(rows) else np.zeros(0)
+    tot = np.concatenate([flux, [float(f_inx), float(pps[rows[:, 1] == 0].sum()) if len(rows) else 0.0,
+                                 float(pps[rows[:, 1] == 1].sum()) if len(rows) else 0.0, float(len(rows))]])
+    if world > 1:
+        tot = allreduce_sum(tot)
+    f_glob = tot[2 * nbins]
     if len(rows):
-        rows[:, 7] /= float(f_inx)  # saveAll[:, 8] ./= f_inx (:747)
+        rows[:, 7] /= f_glob  # saveAll[:, 8] ./= f_inx (:747), the whole run's f_inx
+    if run_info is not None:
+        run_info.update(f_inx=int(round(f_glob)), flux=(tot[:2 * nbins] / f_glob).reshape(2, nbins),
+                        sum_weight_sln_prob=(tot[2 * nbins + 1] / f_glob, tot[2 * nbins + 2] / f_glob),
+                        rows=int(round(tot[2 * nbins + 3])), events=(lo, hi), n_events=n_glob)
     if dir_tag is not None:
         path = tree_file_name(dir_tag, params.mass_a, params.g_agg, params.theta_m, params.omega_pul, params.B0, Ntajs,
-                              ntimes, num_cutoff, MC_nodes, max_nodes, file_tag)
+                              ntimes, num_cutoff, MC_nodes, max_nodes, tag)
         os.makedirs(os.path.dirname(path), exist_ok=True)
         np.save(path, rows)
     return rows
+
+
+def radiated_flux(phif, ident, weights, nbins=50) -> np.ndarray:
+    """The binned flux of plot/flux.py:38-48 on the GPU: np.histogram(phif, nbins,
+    range=(-π, π), weights=weights) for axion rows (ident 0) and photon rows (ident 1),
+    as a (2 * nbins,) array [axions | photons]. The reference's radiated flux is the photon
+    half with weights = weight * sln_prob (npy columns 9 and 8)."""
+    import torch
+    lib = _lib.load()
+    n = len(phif)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    f = lambda a, dt=torch.float64: torch.as_tensor(np.ascontiguousarray(a), dtype=dt).to(dev)  # noqa: E731
+    ph, sp, ww = f(phif), f(np.asarray(ident) != 0, torch.int8), f(weights)
+    hist = torch.zeros(2 * nbins, dtype=torch.float64, device=dev)
+    stream = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    check(lib.art_flux_histogram_phi_device(n, C.c_void_p(ph.data_ptr()), C.c_void_p(sp.data_ptr()),
+                                            C.c_void_p(ww.data_ptr()), int(nbins), C.c_void_p(hist.data_ptr()),
+                                            stream))
+    return hist.cpu().numpy()
+
+
+def gather_rank_rows(dir_tag, params: Params, Ntajs, world, file_tag="", ntimes=3, num_cutoff=5, MC_nodes=5,
+                     max_nodes=50) -> np.ndarray:
+    """The rows of a sharded run: its per-rank files (file_tag + str(rank)) concatenated in rank
+    order -- the rows the single-process run writes."""
+    return np.concatenate([np.load(tree_file_name(dir_tag, params.mass_a, params.g_agg, params.theta_m,
+                                                  params.omega_pul, params.B0, Ntajs, ntimes, num_cutoff, MC_nodes,
+                                                  max_nodes, f"{file_tag}{r}")) for r in range(int(world))], axis=0)
 
 
 def combine_files(Mass_a, Ax_g, θm, ωPul, B0, Ntajs, Nruns, file_tag, ntimes=3, dir_tag="results", num_cutoff=5,

@@ -16,7 +16,11 @@
  *   art_sample_conversion_points_* RT.find_samples_new + k_norm_Cart
  *                                  RayTracer.jl:1480-1653, MainRunner.jl:463-529
  *   art_find_conversion_surface    RT.Find_Conversion_Surface RayTracer.jl:1250-1263
- *   art_flux_histogram_device      plot/flux.py:38-48 (binned flux, reduced over ranks)
+ *   art_flux_histogram_device      plot/flux.py:38-48 (binned flux of segment end states)
+ *   art_flux_histogram_phi_device  plot/flux.py:38-48 (binned flux of the npy rows' φf)
+ *   art_comm_* / art_flux_allreduce  the reduction of the flux and counters over the GPUs of
+ *                                  a node (the reference merges files instead,
+ *                                  Combine_Files.py, Gen_Samples.jl:195-239)
  *   art_grow_trees[_traj]          get_tree (MainRunner.jl:126-352) for n trees, batched
  *                                  (_traj: + saveNode data, MainRunner.jl:17-65)
  *   art_event_weight_*             sln_prob of a sampled point: dwp_ds cos_w + g_det
@@ -34,8 +38,12 @@
  *     void*, used exactly as given (NULL = the HIP null stream, which is also
  *     PyTorch's default stream); they are asynchronous on that stream.
  *   - Return 0 on success or a negative ART_E* code; art_last_error() describes it.
- *   - Thread safety: calls are serialized by an internal mutex; one device per call
- *     (art_set_device).
+ *   - Thread safety: calls are issued under an internal mutex; one device per call
+ *     (art_set_device). *_host calls are synchronous. *_device calls only enqueue work:
+ *     every propagate / sampler launch allocates its own scratch (work-queue word,
+ *     statistics, fresh-state and end-record buffers) from the stream-ordered allocator
+ *     and frees it in stream order, so launches on different streams may run
+ *     concurrently and never share device state.
  */
 #ifndef ART_H
 #define ART_H
@@ -65,6 +73,9 @@ extern "C" {
 #define ART_STATUS_HIT_NS 2     /* photon r < 1.01 rNS (cb_r, :352-368)   (:Terminated) */
 #define ART_STATUS_MAXITERS 3   /* maxiters step attempts                 (:MaxIters)   */
 #define ART_STATUS_NONFINITE 4  /* NaN/Inf in state or error estimate     (:Unstable)   */
+
+/* max_crossings of art_propagate_*: no callbacks (RT.propagate with make_tree = false) */
+#define ART_NO_CALLBACKS (-2147483647 - 1)
 
 /* species (RT.node.species; MainRunner.jl:175-191) */
 #define ART_AXION 0
@@ -133,6 +144,10 @@ double art_last_kernel_ms(void);
  * scan condition evals, interpolant-root condition evals, rays, init RHS evals, 0] and the
  * persistent grid size; they feed the roofline accounting of bench.py. */
 int art_last_stats(uint64_t* stats, int32_t* grid);
+/* Integrator-kernel durations [ms] of the last min(n, 64) propagate launches on the current
+ * device, oldest first, each from the HIP events around that launch on its own stream (waits
+ * for them). Returns the number written (>= 0) or a negative ART_E* code. */
+int art_recent_kernel_ms(int32_t n, double* ms);
 /* The Vern6 tableau the kernel uses: c[9], A[81] row-major, b[9], bhat[9]. */
 int art_vern6_tableau(double* c, double* A, double* b, double* bhat);
 
@@ -148,7 +163,10 @@ double art_find_conversion_surface(const art_params* p);
  * species  : n  ART_PHOTON (func!) or ART_AXION (func_axion!)
  * max_crossings : terminate! once this many crossings are recorded (RayTracer.jl:346);
  *            <= 0 means "stop at the first new crossing" exactly like the reference's
- *            splittings_cutoff = -1 (MainRunner.jl:128).
+ *            splittings_cutoff = -1 (MainRunner.jl:128). ART_NO_CALLBACKS integrates the
+ *            plain ODE with no callbacks, as the reference does for make_tree = false
+ *            (RayTracer.jl:361-377): no crossing is recorded and photons are not stopped
+ *            at 1.01 rNS.
  * xc may be NULL when crossings are not wanted (the segment still stops on them). */
 int art_propagate_host(const art_params* p, int64_t n, const double* x0, const double* k0,
                        const double* erg, const double* dw, const double* ln_t0,
@@ -225,7 +243,9 @@ typedef struct art_tree_opts {
   int32_t max_nodes;         /* 50                                                 */
   int32_t splittings_cutoff; /* -1: forward trees; 100000: backtrace (:588)        */
   int32_t crossing_cap;      /* crossings stored per segment when splittings > 0   */
-  int32_t pad;
+  int32_t tree_offset;       /* global id of tree 0: the Monte-Carlo draws are keyed */
+                             /* by (seed, tree_offset + i, count), so a run sharded */
+                             /* over ranks by event id draws what one process would */
   double prob_cutoff;        /* 1e-10                                              */
   uint64_t seed;             /* key of the Monte-Carlo draws                        */
 } art_tree_opts;
@@ -293,6 +313,31 @@ int art_flux_histogram_device(const art_params* p, int64_t n, const double* x_en
                               const double* k_end, const int32_t* status,
                               const int8_t* species, const double* w, int32_t nbins,
                               double* hist, void* stream);
+
+/* ---- binned flux of the npy rows (plot/flux.py:38-48): np.histogram(phif, nbins,
+ * range = (-π, π), weights = w) of the given azimuths φf (npy column 4, MainRunner.jl:715),
+ * axions (species 0) into row 0 and photons into row 1 of hist (2*nbins, device, float64),
+ * with numpy's bin assignment (edges linspace(-π, π, nbins + 1), the right edge in the last
+ * bin, values outside [-π, π] dropped). hist is ACCUMULATED into. The reference's radiated
+ * flux is row 1 with w = weight * sln_prob (columns 9 and 8). */
+int art_flux_histogram_phi_device(int64_t n, const double* phi, const int8_t* species, const double* w,
+                                  int32_t nbins, double* hist, void* stream);
+
+/* ---- reduction over the GPUs of a node (RCCL over xGMI) ----
+ * One process per GPU. Rank 0 calls art_comm_unique_id and shares the 128 bytes with the
+ * other ranks (a file, MPI, the launcher); every rank then calls art_comm_init on its device.
+ * art_flux_allreduce sums count float64 values of a device buffer in place over all ranks,
+ * asynchronously on `stream` (the binned flux and the run's counters f_inx, Σ weight, ...).
+ * RCCL is opened on first use; without it these return ART_E_UNSUPPORTED. */
+typedef struct art_rccl_id {
+  char internal[128]; /* ncclUniqueId */
+} art_rccl_id;
+int art_comm_unique_id(art_rccl_id* id);
+int art_comm_init(int32_t rank, int32_t world, const art_rccl_id* id);
+int art_flux_allreduce(double* buf, int64_t count, void* stream);
+/* the same for a host buffer (staged through HBM; synchronous) */
+int art_flux_allreduce_host(double* buf, int64_t count);
+int art_comm_destroy(void);
 
 /* ---- pointwise physics on device, for parity tests (u: 7n SoA r,θ,φ,w_r,w_θ,w_φ,u7) */
 /* func!/func_axion! (RayTracer.jl:71-123): du (7n) */

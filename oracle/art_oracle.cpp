@@ -689,7 +689,9 @@ class Segment {
       double last_c = cprev, last_th = 0.0;
       int last_s = sprev;
       bool evented = false;
-      for (int ip = 1; ip < npts && !evented; ++ip) {
+      // make_tree = false installs no callbacks at all (RayTracer.jl:361-377): no scan, no cb_r
+      const bool cbs = max_crossings != INT32_MIN;
+      for (int ip = 1; cbs && ip < npts && !evented; ++ip) {
         double th = double(ip) / double(npts - 1);
         double ui[7];
         hermite(u, fcur, unew, fnew, h, th, ui);
@@ -743,7 +745,7 @@ class Segment {
       cprev = last_c;
       sprev = last_s;
       just_evented = false;
-      if (photon && u[0] < P.rNS * 1.01) return ART_STATUS_HIT_NS;  // cb_r (:352-359)
+      if (cbs && photon && u[0] < P.rNS * 1.01) return ART_STATUS_HIT_NS;  // cb_r (:352-359)
       if (last) return ART_STATUS_SUCCESS;
       if (!rk4) dt = std::min(dtnext, dtmax);
     }

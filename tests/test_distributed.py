@@ -24,13 +24,12 @@ def _free_port():
 
 def _flux_hist(o, n, nbins=NBINS, rns=10.0):
     """Host restatement of flux_kernel: photons that ended without a crossing beyond 1.1 rNS,
-    binned by atan2(k_y, k_x) over [-pi, pi)."""
+    binned by atan2(k_y, k_x) as np.histogram(range=(-pi, pi))."""
     x, k = o["x_end"].reshape(3, n), o["k_end"].reshape(3, n)
     keep = (o["status"] != 1) & (np.linalg.norm(x, axis=0) > 1.1 * rns)
     phi = np.arctan2(k[1], k[0])
-    b = np.clip(np.floor((phi + np.pi) / (2 * np.pi) * nbins).astype(int), 0, nbins - 1)
     h = np.zeros(2 * nbins)
-    np.add.at(h, nbins + b[keep], 1.0)
+    h[nbins:] = np.histogram(phi[keep], nbins, range=(-np.pi, np.pi))[0]
     return h
 
 

@@ -81,3 +81,31 @@ def test_hamiltonian_matches_oracle(cfg, torch_mod, oracle_lib):
         for a, b in ((gx[:, i], rx), (gk[:, i], rk)):
             assert np.all(np.abs(a - b) <= 1e-9 * (np.abs(b).max() + 1e-300)), (cfg, i, a, b)
         assert abs(gT[i] - rT) <= 1e-9 * (abs(rT) + np.abs(rx).max() * 1e-3 + 1e-300), (cfg, i, gT[i], rT)
+
+
+# The non-default physics branches on the device: the boundary layer of plasma
+# (RayTracer.jl:1155-1162; func! applies it to the ∂t pass only, :84-88) and isotropic
+# plasma (k∥ -> 0, :542-543 and the condition's :1573-1575 analogue).
+BRANCHES = {"bndry_lyr": dict(bndry_lyr=3.0), "isotropic": dict(isotropic=True)}
+
+
+@pytest.mark.parametrize("cfg", ["flat", "gr"])
+@pytest.mark.parametrize("branch", sorted(BRANCHES))
+def test_branch_rhs_and_condition_match_oracle(cfg, branch, torch_mod, oracle_lib):
+    torch = torch_mod
+    kw = dict(CONFIGS[cfg], **BRANCHES[branch])
+    eng = _engine(kw)
+    p = oracle_lib.make_params(**kw)
+    U, tau = random_states(N, seed=21, rmin=9.5)
+    erg = np.full(N, 1.0000002692622573e-05)
+    dev = lambda a, dt=torch.float64: torch.tensor(np.ascontiguousarray(a), dtype=dt, device="cuda")  # noqa: E731
+    du = eng.eval_rhs(dev(U.reshape(-1)), dev(tau), dev(erg), dev(np.full(N, 1), torch.int8)).cpu().numpy()
+    du = du.reshape(7, N)
+    ref = np.stack([oracle_lib.rhs(p, 1, U[:, i], tau[i], erg[i]) for i in range(N)], axis=1)
+    scale = np.abs(ref).max(axis=1, keepdims=True) + 1e-300
+    assert np.nanmax(np.abs(du - ref) / scale) < 1e-10, (cfg, branch, np.nanmax(np.abs(du - ref) / scale, axis=1))
+    c = eng.eval_condition(dev(U.reshape(-1)), dev(tau)).cpu().numpy()
+    cr = np.array([oracle_lib.condition(p, U[:, i], tau[i]) for i in range(N)])
+    assert np.array_equal(np.isnan(c), np.isnan(cr))
+    ok = ~np.isnan(cr)
+    assert np.max(np.abs(c[ok] - cr[ok]) / (np.abs(cr[ok]) + 1e-3)) < 1e-9

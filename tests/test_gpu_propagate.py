@@ -7,10 +7,12 @@ same adaptive Vern6 + event algorithm and differ only by rounding (fused vs unfu
 operations, analytic vs dual-number gradients). An adaptive solver at reltol 1e-7 turns a
 last-bit difference into a different accept/reject sequence for some rays, after which
 the trajectories differ at the solver's own error level. So every test also runs the
-ORACLE a second time with its initial positions perturbed by one ulp, and requires the
-GPU-vs-oracle discrepancy to be no larger than that oracle-vs-oracle discrepancy:
+ORACLE three more times with its initial positions perturbed by one ulp (independent
+draws), and requires the GPU-vs-oracle discrepancy to be no larger than the envelope (the
+per-ray maximum) of those oracle-vs-oracle discrepancies:
   * segment status agreement >= min(0.99, perturbed agreement - 0.02);
-  * final position / crossing position / conversion probability: the 50th, 90th and 99th
+  * final position and momentum, u7, ln t, the crossing's position, momentum, t, Δω and
+    conversion probability: the 50th, 90th and 99th
     percentiles of the relative error are <= 10x the perturbed run's percentiles
     (+1e-12), and the fraction of rays off by more than 1e-3 exceeds the perturbed
     run's by at most 0.01 (chaotic rays, e.g. grazing a kink of |B_z|, exist in both);
@@ -24,26 +26,35 @@ from conftest import CONFIGS
 
 pytestmark = pytest.mark.gpu
 
+N_PERTURB = 3  # independent 1-ulp perturbations of the oracle's start positions
 
-def _run(kw, n, integrator="vern6", species=1, max_crossings=-1, cap=1, oracle_lib=None, seed=1769):
+
+def _run(kw, n, integrator="vern6", species=1, max_crossings=-1, cap=1, oracle_lib=None, seed=1769, sample_kw=None):
     import adiabatic_raytracer_amd as A
     p = A.Params(integrator=integrator, **kw)
     po = oracle_lib.make_params(integrator=oracle_lib.ART_RK4 if integrator == "rk4" else 0, **kw)
-    s = oracle_lib.sample(po, oracle_lib.find_conversion_surface(po), seed, 0, n)
+    ps = po if sample_kw is None else oracle_lib.make_params(**sample_kw)
+    s = oracle_lib.sample(ps, oracle_lib.find_conversion_surface(ps), seed, 0, n)
     k0 = s["k_init"] if species == 1 else -s["k_init"]  # backtrace: k -> -k (MainRunner.jl:581-585)
     sp = np.full(n, species, np.int8)
     g = A.propagate_batch(p, s["x"], k0, s["erg"], -np.ones(n), np.full(n, -30.0), sp,
                           max_crossings=max_crossings, capacity=cap)
     o = oracle_lib.propagate(po, s["x"], k0, s["erg"], -1.0, -30.0, sp, max_crossings=max_crossings, cap=cap)
-    ulp = np.random.default_rng(seed).choice([-1.0, 1.0], s["x"].shape) * 2.2e-16
-    o2 = oracle_lib.propagate(po, s["x"] * (1.0 + ulp), k0, s["erg"], -1.0, -30.0, sp,
-                              max_crossings=max_crossings, cap=cap)
+    o2 = []
+    for k in range(N_PERTURB):
+        ulp = np.random.default_rng(seed + k).choice([-1.0, 1.0], s["x"].shape) * 2.2e-16
+        o2.append(oracle_lib.propagate(po, s["x"] * (1.0 + ulp), k0, s["erg"], -1.0, -30.0, sp,
+                                       max_crossings=max_crossings, cap=cap))
     return g, o, o2
 
 
-def _rel_end(a, b, n):
-    xa, xb = a["x_end"].reshape(3, n), b["x_end"].reshape(3, n)
+def _rel_end(a, b, n, key="x_end"):
+    xa, xb = a[key].reshape(3, n), b[key].reshape(3, n)
     return np.abs(xa - xb).max(0) / np.linalg.norm(xb, axis=0)
+
+
+def _rel1(a, b, key):
+    return np.abs(a[key] - b[key]) / np.maximum(np.abs(b[key]), 1e-300)
 
 
 def _within(err, ref_err, what):
@@ -56,32 +67,83 @@ def _within(err, ref_err, what):
 
 
 def _crossings(a, b, n, mask):
-    pa, pb = a["xc_pos"].reshape(3, -1)[:, :n][:, mask], b["xc_pos"].reshape(3, -1)[:, :n][:, mask]
-    relc = np.abs(pa - pb).max(0) / np.linalg.norm(pb, axis=0)
-    rp = np.abs(a["xc_p"][:n][mask] - b["xc_p"][:n][mask]) / np.abs(b["xc_p"][:n][mask])
-    return relc, rp
+    """Relative errors of the first recorded crossing of the rays in `mask`: position, momentum,
+    tc = exp(τ), Δωc = u7/erg (affect!, RayTracer.jl:325-342) and P_nonAD."""
+    def vec(key):
+        pa, pb = a[key].reshape(3, -1)[:, :n][:, mask], b[key].reshape(3, -1)[:, :n][:, mask]
+        return np.abs(pa - pb).max(0) / np.linalg.norm(pb, axis=0)
+
+    def sc(key):
+        x, y = a[key][:n][mask], b[key][:n][mask]
+        with np.errstate(divide="ignore", invalid="ignore"):
+            e = np.where(x == y, 0.0, np.abs(x - y) / np.abs(y))
+        # P_nonAD is NaN where the reference's is undefined (e.g. v_loc of a crossing below
+        # the axion shell): NaN on both sides agrees, NaN on one side only is a full miss
+        # (capped at 1, so percentiles stay finite)
+        return np.where(np.isnan(x) & np.isnan(y), 0.0, np.where(np.isnan(x) | np.isnan(y), 1.0, np.minimum(e, 1.0)))
+    return {"crossing position": vec("xc_pos"), "crossing k": vec("xc_k"), "crossing t": sc("xc_t"),
+            "crossing dw": sc("xc_dw"), "P_nonAD": sc("xc_p")}
 
 
 def _compare(g, o, o2, n):
+    """GPU run g against the oracle o, measured against the envelope (per-ray maximum) of the
+    oracle's discrepancies under the N_PERTURB 1-ulp perturbations o2."""
     same = g["status"] == o["status"]
-    same2 = o2["status"] == o["status"]
-    assert same.mean() >= min(0.99, same2.mean() - 0.02), (
-        np.bincount(g["status"], minlength=5), np.bincount(o["status"], minlength=5), same2.mean())
+    same2 = np.all([q["status"] == o["status"] for q in o2], axis=0)
+    agree2 = min(np.mean(q["status"] == o["status"]) for q in o2)
+    assert same.mean() >= min(0.99, agree2 - 0.02), (
+        np.bincount(g["status"], minlength=5), np.bincount(o["status"], minlength=5), agree2)
     both = same & same2
-    _within(_rel_end(g, o, n)[both], _rel_end(o2, o, n)[both], "x_end")
-    c = both & (o["status"] == 1) & (g["n_cross"] == o["n_cross"]) & (o2["n_cross"] == o["n_cross"])
+
+    def env(f):
+        return np.max([f(q) for q in o2], axis=0)
+    # every per-ray output of the 14-tuple (RayTracer.jl:448): final position and momentum,
+    # u7 = erg Δω (feeds Δω, MainRunner.jl:709) and the final ln t
+    for key in ("x_end", "k_end"):
+        _within(_rel_end(g, o, n, key)[both], env(lambda q: _rel_end(q, o, n, key))[both], key)
+    for key in ("u7_end", "tau_end"):
+        _within(_rel1(g, o, key)[both], env(lambda q: _rel1(q, o, key))[both], key)
+    c = both & (o["status"] == 1) & (g["n_cross"] == o["n_cross"])
+    c &= np.all([q["n_cross"] == o["n_cross"] for q in o2], axis=0)
     if c.sum() >= 20:
-        gc, gp = _crossings(g, o, n, c)
-        oc, op = _crossings(o2, o, n, c)
-        _within(gc, oc, "crossing position")
-        _within(gp, op, "P_nonAD")
-    assert np.median(np.abs(g["n_accept"][same] - o["n_accept"][same])) <= 1
+        gx = _crossings(g, o, n, c)
+        ox = [_crossings(q, o, n, c) for q in o2]
+        for what in gx:
+            _within(gx[what], np.max([x[what] for x in ox], axis=0), what)
+    # accepted steps: within one of the oracle's, or (long chaotic segments, e.g. ~5e4 steps
+    # with a boundary layer) no further off than the oracle's own 1-ulp runs
+    d_g = np.median(np.abs(g["n_accept"][same] - o["n_accept"][same]))
+    d_o = max(np.median(np.abs(q["n_accept"][same] - o["n_accept"][same])) for q in o2)
+    assert d_g <= max(1.0, 3.0 * d_o), (d_g, d_o)
 
 
 @pytest.mark.parametrize("cfg", sorted(CONFIGS))
 def test_vern6_photon_forward_roots(cfg, oracle_lib):
     n = 512
     g, o, o2 = _run(CONFIGS[cfg], n, oracle_lib=oracle_lib)
+    _compare(g, o, o2, n)
+
+
+# BASELINE.json configs[4]: two grid points of the 32-point (m_a, B0, P) scan, neither at the
+# headline's (m_a = 1e-5, B0 = 1e14, P = 2π)
+@pytest.mark.parametrize("m_a,B0,period", [(1e-6, 2.5e13, 0.5), (1e-5, 2e14, 1.0)])
+def test_vern6_scan_points(m_a, B0, period, oracle_lib):
+    from adiabatic_raytracer_amd.scan import scan_grid
+    kw = [g for g in scan_grid() if g["mass_a"] == m_a and g["B0"] == B0 and abs(g["omega_pul"] * period - 2 * np.pi) < 1e-12]
+    assert len(kw) == 1
+    n = 384
+    g, o, o2 = _run(kw[0], n, oracle_lib=oracle_lib)
+    _compare(g, o, o2, n)
+
+
+# The non-default physics branches on the kernel (GEOM_ANY): the boundary layer of plasma
+# (RayTracer.jl:1155-1162, --bndry_lyr) and the isotropic plasma (k∥ -> 0, :542-543, 1573-1575).
+# Initial conditions are the default geometry's forward roots.
+@pytest.mark.parametrize("cfg", ["flat", "gr"])
+@pytest.mark.parametrize("branch", [dict(bndry_lyr=3.0), dict(isotropic=True)], ids=["bndry_lyr", "isotropic"])
+def test_vern6_physics_branches(cfg, branch, oracle_lib):
+    n = 256
+    g, o, o2 = _run(dict(CONFIGS[cfg], **branch), n, oracle_lib=oracle_lib, sample_kw=CONFIGS[cfg])
     _compare(g, o, o2, n)
 
 
@@ -97,12 +159,14 @@ def test_axion_backtrace_all_crossings(oracle_lib):
     # backtrace semantics: axion, -k, records every crossing (splittings_cutoff = 100000)
     n = 256
     g, o, o2 = _run(CONFIGS["gr"], n, species=0, max_crossings=100000, cap=8, oracle_lib=oracle_lib)
-    same, same2 = g["status"] == o["status"], o2["status"] == o["status"]
-    assert same.mean() >= min(0.99, same2.mean() - 0.03), (same.mean(), same2.mean())
-    nc, nc2 = np.mean(g["n_cross"] == o["n_cross"]), np.mean(o2["n_cross"] == o["n_cross"])
+    same = g["status"] == o["status"]
+    same2 = np.all([q["status"] == o["status"] for q in o2], axis=0)
+    agree2 = min(np.mean(q["status"] == o["status"]) for q in o2)
+    assert same.mean() >= min(0.99, agree2 - 0.03), (same.mean(), agree2)
+    nc, nc2 = np.mean(g["n_cross"] == o["n_cross"]), min(np.mean(q["n_cross"] == o["n_cross"]) for q in o2)
     assert nc >= min(0.98, nc2 - 0.03), (nc, nc2)
     both = same & same2
-    _within(_rel_end(g, o, n)[both], _rel_end(o2, o, n)[both], "x_end")
+    _within(_rel_end(g, o, n)[both], np.max([_rel_end(q, o, n) for q in o2], axis=0)[both], "x_end")
     assert np.all(g["status"] != 2)  # axions never stop at the star (cb_r is photon-only, :361-368)
 
 
@@ -118,10 +182,18 @@ def test_golden_fixture_roundtrip(oracle_lib):
     g = A.propagate_batch(p, z["x0"], z["k0"], z["erg"], z["dw"], z["ln_t0"], z["species"], max_crossings=-1)
     same = g["status"] == z["status"]
     assert same.mean() >= 0.98
-    rel = np.abs(g["x_end"].reshape(3, n) - z["x_end"].reshape(3, n)).max(0) / np.linalg.norm(
-        z["x_end"].reshape(3, n), axis=0)
     # the bulk is reproduced to rounding; the tail at the oracle's own 1-ulp sensitivity (module doc)
-    assert np.median(rel[same]) <= 1e-9 and np.percentile(rel[same], 99) <= 3e-4, np.percentile(rel[same], [50, 99])
+    for key in ("x_end", "k_end"):
+        rel = _rel_end(g, z, n, key)[same]
+        assert np.median(rel) <= 1e-9 and np.percentile(rel, 99) <= 3e-4, (key, np.percentile(rel, [50, 99]))
+    for key in ("u7_end", "tau_end"):
+        rel = _rel1(g, z, key)[same]
+        assert np.median(rel) <= 1e-9 and np.percentile(rel, 99) <= 3e-4, (key, np.percentile(rel, [50, 99]))
+    c = same & (z["status"] == 1) & (g["n_cross"] == z["n_cross"])
+    assert c.sum() >= 20
+    for what, rel in _crossings(g, z, n, c).items():
+        assert np.median(rel) <= 1e-9 and np.percentile(rel, 99) <= 3e-4, (what, np.percentile(rel, [50, 99]))
+    assert np.array_equal(g["n_cross"][same], z["n_cross"][same])
 
 
 def test_invariants_full_size():
@@ -144,3 +216,47 @@ def test_invariants_full_size():
     assert np.allclose(u7, -erg, rtol=1e-12, atol=0)  # du7 = ∂H/∂t ... = 0 for θm = 0
     tau = out["tau_end"].cpu().numpy()
     assert np.all(tau[st == 0] == p.to_c().ln_t_end)
+
+
+def test_rt_propagate_mirror_make_tree(oracle_lib):
+    """The host mirror raytracer.propagate called exactly as MainRunner.jl:179-182 calls
+    RT.propagate (Mvars in the photon order, NumerP, func!, make_tree = true, splittings
+    cutoff -1) returns the 14-tuple of the batched kernel; with make_tree = false (the
+    reference's default) no callback is installed (RayTracer.jl:361-377): no crossing stops
+    the segment, photons are not cut at 1.01 rNS, and the 4-tuple is returned. Both against
+    the oracle run in the same mode."""
+    import adiabatic_raytracer_amd as A
+    from adiabatic_raytracer_amd.raytracer import ART_NO_CALLBACKS, func_photon
+    kw = CONFIGS["flat"]
+    po = oracle_lib.make_params(**kw)
+    n = 128
+    s = oracle_lib.sample(po, oracle_lib.find_conversion_surface(po), 1769, 0, n)
+    x, k = s["x"].reshape(3, n).T, s["k_init"].reshape(3, n).T
+    erg = s["erg"][0]
+    p = A.Params(**kw)
+    # MainRunner.jl:177-178 photon order: θm, ωPul, B0, rNS, gammaF, time0, Mass_NS, Mass_a, [erg], flat, isotropic,
+    # melrose, bndry_lyr
+    Mvars = [p.theta_m, p.omega_pul, p.B0, p.rNS, 1.0, 0.0, 1.0, p.mass_a, [erg], 1, 0, 1, -1.0]
+    NumerP = [-30.0, float(np.log(1.0 / p.omega_pul)), 1e-6]
+    t = A.raytracer.propagate(x, k, 3, Mvars, NumerP, func_photon, True, False, p.mass_a, -1, -1.0)
+    assert len(t) == 18 and t.status.shape == (n,)
+    o = oracle_lib.propagate(po, x, k, np.full(n, erg), -1.0, -30.0, 1, max_crossings=-1)
+    assert np.mean(t.status == o["status"]) >= 0.97
+    plain = A.raytracer.propagate(x, k, 3, Mvars, NumerP, func_photon, False, False, p.mass_a, -1, -1.0)
+    assert len(plain) == 4 and plain.x.shape == (n, 3, 1)
+    o2 = oracle_lib.propagate(po, x, k, np.full(n, erg), -1.0, -30.0, 1, max_crossings=ART_NO_CALLBACKS)
+    assert np.all(o2["n_cross"] == 0) and np.all(o2["status"] != 1) and np.all(o2["status"] != 2)
+    # without callbacks every photon escapes to ~3e5 km, where the end point carries the
+    # solver's own ~1e-6 sensitivity: compared against the oracle's 1-ulp envelope
+    xg = {"x_end": plain.x[:, :, 0].T.reshape(-1)}
+    ref = []
+    for sd in range(N_PERTURB):
+        ulp = np.random.default_rng(1769 + sd).choice([-1.0, 1.0], x.shape) * 2.2e-16
+        ref.append(_rel_end(oracle_lib.propagate(po, x * (1.0 + ulp), k, np.full(n, erg), -1.0, -30.0, 1,
+                                                 max_crossings=ART_NO_CALLBACKS), o2, n))
+    _within(_rel_end(xg, o2, n), np.max(ref, axis=0), "x_end (no callbacks)")
+    # without callbacks every segment runs to ln t_end (none is terminated by a crossing)
+    g = A.propagate_batch(p, s["x"], s["k_init"], np.full(n, erg), -np.ones(n), np.full(n, -30.0), np.ones(n, np.int8),
+                          max_crossings=ART_NO_CALLBACKS)
+    assert np.all(g["n_cross"] == 0) and np.all((g["status"] == 0) | (g["status"] >= 3))
+    assert np.array_equal(g["x_end"], plain.x[:, :, 0].T.reshape(-1))

@@ -40,3 +40,21 @@ def test_certificate_is_bit_exact(cfg, species, monkeypatch):
     assert sb["cert_steps"] == 0 and sa["cert_steps"] > 0, (sa, sb)
     assert sa["accepted"] == sb["accepted"] and sa["scan_evals"] < sb["scan_evals"], (sa, sb)
     print(cfg, species, "certified", sa["cert_steps"] / sa["accepted"], "scan evals", sa["scan_evals"] / sb["scan_evals"])
+
+
+@pytest.mark.parametrize("cfg", ["flat", "gr", "scan7"])
+def test_sampler_certificate_is_bit_exact(cfg, monkeypatch):
+    """The sampler's certified-negative steps (sample_kernel; a step whose every point is
+    provably below the resonance evaluates only its last point) change no sample: positions,
+    momenta, energies, weights and attempt counts with and without them (ART_SCAN_CERT=0)
+    are bit-identical, for the flat and GR geometries and the heaviest scan point."""
+    import adiabatic_raytracer_amd as A
+    from adiabatic_raytracer_amd.scan import scan_grid
+    kw = scan_grid()[7] if cfg == "scan7" else CONFIGS[cfg]
+    p = A.Params(**kw)
+    n = 20000 if cfg != "scan7" else 4000
+    a = A.sample_conversion_points(p, n, seed=1769)
+    monkeypatch.setenv("ART_SCAN_CERT", "0")
+    b = A.sample_conversion_points(p, n, seed=1769)
+    for k in ("x", "k_init", "erg", "vifty", "weights", "attempts"):
+        assert np.array_equal(a[k], b[k], equal_nan=True), (cfg, k)
