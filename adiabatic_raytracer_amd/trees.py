@@ -311,3 +311,28 @@ def combine_files(Mass_a, Ax_g, θm, ωPul, B0, Ntajs, Nruns, file_tag, ntimes=3
         for f in files:
             os.remove(f)
     return out
+
+
+def combine_files_py(out_path, files) -> np.ndarray:
+    """Combine_Files.py OUT IN... (the reference's Python combine, Combine_Files.py:1-31):
+    the row files in the given order, each file's event numbers (column 1) offset by the last
+    event number combined so far (:22), and -- its quirk -- column 10 (0-based 9, the sampled
+    x position) divided by the number of files (:28). Writes out_path and returns the rows.
+    (Gen_Samples.jl --run_Combine divides the sln_prob column instead: combine_files.)"""
+    data = None
+    for f in files:
+        name = os.path.basename(f)
+        if not (name[:5] == "tree_" and name[-4:] == ".npy"):
+            raise ValueError(f"{f} is not a tree_*.npy row file")
+        tmp = np.load(f).T.copy()
+        if data is None:
+            data = tmp
+        else:
+            tmp[0, :] += data[0, -1]
+            data = np.append(data, tmp, axis=1)
+    if data is None:
+        raise ValueError("no input files")
+    data[9, :] /= len(files)
+    np.save(out_path, data.T)
+    return data.T
+

@@ -73,7 +73,54 @@ def cpu_baseline(params, x0, k0, erg, seed, threads):
     steps = int(r["n_accept"].sum())
     return {"value": steps / dt, "unit": "ray-steps/s", "cores": threads, "kind": "port",
             "sample": f"first {n} forward-root photon segments of the seed-{seed} batch, {steps} accepted Vern6 "
-                      f"steps in {dt:.1f} s; oracle restatement (C++/OpenMP, dual-number gradients like ForwardDiff)"}
+                      f"steps in {dt:.1f} s on {threads} thread(s); oracle restatement (C++/OpenMP, dual-number "
+                      f"gradients like ForwardDiff)"}
+
+
+def host_cores():
+    """CPUs this job may use: the cgroup CPU quota (cpu.max) when one is set, else the
+    affinity mask. (The GPU box: 16 of a 2 x 64-core EPYC 9575F.)"""
+    n = len(os.sched_getaffinity(0))
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            n = min(n, max(1, int(int(q) // int(per))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+def pcie_inclusive(eng, inp, n, accepted_per_launch, reps=2):
+    """The host-buffer rate: art_propagate_host on pageable host
+    arrays -- H2D of the inputs, the kernels, D2H of every output -- as a Julia ccall would
+    run it. Outputs are allocated and faulted in once, outside the timing."""
+    import ctypes as C
+    from adiabatic_raytracer_amd._lib import CrossingBuf, SegmentOut, check, load
+    lib = load()
+    h = {k: inp[k].cpu().numpy() for k in ("x0", "k0", "erg", "dw", "ln_t0", "species")}
+    out = {"x_end": np.ones(3 * n), "k_end": np.ones(3 * n), "u7_end": np.ones(n), "tau_end": np.ones(n),
+           "status": np.ones(n, np.int32), "n_accept": np.ones(n, np.int32), "n_reject": np.ones(n, np.int32),
+           "n_cross": np.ones(n, np.int32), "xc_pos": np.ones(3 * n), "xc_k": np.ones(3 * n), "xc_t": np.ones(n),
+           "xc_dw": np.ones(n), "xc_p": np.ones(n)}
+    P = lambda a: a.ctypes.data_as(C.c_void_p)  # noqa: E731
+    so = SegmentOut(*[P(out[k]) for k in ("x_end", "k_end", "u7_end", "tau_end", "status", "n_accept", "n_reject")])
+    xb = CrossingBuf(1, *[P(out[k]) for k in ("n_cross", "xc_pos", "xc_k", "xc_t", "xc_dw", "xc_p")])
+    cp = eng.cp
+
+    def run():
+        check(lib.art_propagate_host(C.byref(cp), n, *[P(h[k]) for k in ("x0", "k0", "erg", "dw", "ln_t0", "species")],
+                                     -1, C.byref(so), C.byref(xb)))
+    run()  # staging buffers
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        run()
+    dt = (time.perf_counter() - t0) / reps
+    in_b = sum(a.nbytes for a in h.values())
+    out_b = sum(a.nbytes for a in out.values())
+    return {"value": accepted_per_launch / dt, "unit": "ray-steps/s", "ms_per_step": dt * 1e3,
+            "h2d_bytes": in_b, "d2h_bytes": out_b,
+            "note": "art_propagate_host on pageable host buffers (H2D + init/integrator/finalize kernels + "
+                    "D2H), rank 0, same batch; value above is device-resident"}
 
 
 def main():
@@ -87,7 +134,9 @@ def main():
     ap.add_argument("--seed", type=int, default=1769)
     ap.add_argument("--nbins", type=int, default=50)
     ap.add_argument("--cpu-rays", type=int, default=int(os.environ.get("ART_CPU_RAYS", "500000")))
+    ap.add_argument("--cpu-rays-1t", type=int, default=int(os.environ.get("ART_CPU_RAYS_1T", "24000")))
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-pcie", action="store_true")
     args = ap.parse_args()
 
     import torch
@@ -208,13 +257,21 @@ def main():
             "attempts_per_ray": attempt_dist,
             "ic_sampling_s": sample_s,
         }
+        if not args.no_pcie:
+            line["pcie_inclusive"] = pcie_inclusive(eng, inp, n, stats_last["accepted"])
         if world == 1 and not args.no_cpu_baseline:
-            threads = int(os.environ.get("ART_CPU_THREADS", str(min(16, os.cpu_count() or 1))))
+            threads = int(os.environ.get("ART_CPU_THREADS", str(host_cores())))
+
+            def sample(m):
+                xs = inp["x0"].view(3, n)[:, :m].cpu().numpy().reshape(-1)
+                ks = inp["k0"].view(3, n)[:, :m].cpu().numpy().reshape(-1)
+                return xs, ks, inp["erg"][:m].cpu().numpy()
+            cfg = CONFIGS[args.config] | {"integrator": 0}
             m = min(args.cpu_rays, n)
-            xs = inp["x0"].view(3, n)[:, :m].cpu().numpy().reshape(-1)
-            ks = inp["k0"].view(3, n)[:, :m].cpu().numpy().reshape(-1)
-            line["cpu_baseline"] = cpu_baseline(CONFIGS[args.config] | {"integrator": 0}, xs, ks,
-                                                inp["erg"][:m].cpu().numpy(), args.seed, threads)
+            line["cpu_baseline"] = cpu_baseline(cfg, *sample(m), args.seed, threads)
+            # and one core: the reference's own model is one single-threaded process per ray batch
+            m1 = min(args.cpu_rays_1t, n)
+            line["cpu_baseline"]["one_thread"] = cpu_baseline(cfg, *sample(m1), args.seed, 1)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

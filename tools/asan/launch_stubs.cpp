@@ -1,0 +1,28 @@
+// launch_stubs.cpp -- TEST INFRASTRUCTURE ONLY: the kernel launch wrappers of
+// art_internal.h for the host-only sanitizer build of art_capi.cpp (capi_main.cpp). No GPU
+// exists there, so every launch reports hipErrorNoDevice.
+#include "../../adiabatic_raytracer_amd/csrc/art_internal.h"
+
+namespace art {
+int persistent_blocks(const void*, int64_t) { return 1; }
+hipError_t launch_propagate(const KParams&, int64_t, const SegIn&, const SegOut&, int32_t, unsigned long long*,
+                            unsigned long long*, hipStream_t, int*, hipEvent_t, hipEvent_t) { return hipErrorNoDevice; }
+hipError_t launch_sample(const KParams&, double, uint64_t, int64_t, int64_t, double*, double*, double*, double*, int32_t*,
+                         int32_t*, unsigned long long*, hipStream_t) { return hipErrorNoDevice; }
+hipError_t launch_prob(const KParams&, int64_t, const double*, const double*, const double*, int64_t, const int64_t*,
+                       double*, hipStream_t) { return hipErrorNoDevice; }
+hipError_t launch_flux(const KParams&, int64_t, const double*, const double*, const int32_t*, const int8_t*,
+                       const double*, int32_t, double*, hipStream_t) { return hipErrorNoDevice; }
+hipError_t launch_flux_phi(int64_t, const double*, const int8_t*, const double*, int32_t, double*, hipStream_t) {
+  return hipErrorNoDevice;
+}
+hipError_t launch_eval_rhs(const KParams&, int64_t, const double*, const double*, const double*, const int8_t*, double*,
+                           hipStream_t) { return hipErrorNoDevice; }
+hipError_t launch_eval_hamiltonian(const KParams&, int64_t, const double*, const double*, const double*, const double*,
+                                   double*, double*, double*, double*, hipStream_t) { return hipErrorNoDevice; }
+hipError_t launch_event_weight(const KParams&, int64_t, const double*, const double*, const double*, double, double,
+                               double, double*, hipStream_t) { return hipErrorNoDevice; }
+hipError_t launch_eval_condition(const KParams&, int64_t, const double*, const double*, double*, hipStream_t) {
+  return hipErrorNoDevice;
+}
+}  // namespace art
