@@ -44,5 +44,20 @@ def build(force=False, verbose=False):
     return LIB
 
 
+def build_variant(out, defines=(), extra=()):
+    """Dev A/B builds (tools/ab_multi.sh): the same sources with extra -D defines / flags into
+    `out` (e.g. tools/build/libart_x.so, loaded with ART_LIB)."""
+    os.makedirs(os.path.dirname(os.path.abspath(out)), exist_ok=True)
+    cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+           "-mllvm", "-amdgpu-use-amdgpu-trackers=1", *[f"-D{d}" for d in defines], *extra,
+           *[os.path.join(CSRC, s) for s in SOURCES], "-o", out]
+    subprocess.run(cmd, check=True)
+    return out
+
+
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv, verbose=True))
+    if len(sys.argv) > 2 and sys.argv[1] == "--variant":  # --variant OUT [-DNAME ...]
+        print(build_variant(sys.argv[2], [a[2:] for a in sys.argv[3:] if a.startswith("-D")],
+                            [a for a in sys.argv[3:] if not a.startswith("-D")]))
+    else:
+        print(build(force="--force" in sys.argv, verbose=True))

@@ -1013,7 +1013,17 @@ __host__ __device__ inline T prob_nonad_single(const KParams& P, const T* pos, c
 // rounding); the metric always uses the GR mass (the sampler gets no `flat`). Divisions are
 // hardware reciprocals with two Newton steps (trcp) on the device.
 template <class T>
+__host__ __device__ inline T sampler_condition_e(const KParams& P, const T* x, const T* vl, double E, double iE2);
+
+template <class T>
 __host__ __device__ inline T sampler_condition(const KParams& P, const T* x, const T* vl, double E) {
+  const double iE2 = 1.0 / (E * E);  // per attempt: hoisted out of a scan by the compiler
+  return sampler_condition_e(P, x, vl, E, iE2);
+}
+
+// The same with 1/E² given (the cooperative scan of sample_kernel evaluates other lanes' lines).
+template <class T>
+__host__ __device__ inline T sampler_condition_e(const KParams& P, const T* x, const T* vl, double E, double iE2) {
   const T rho2 = x[0] * x[0] + x[1] * x[1];
   const T r = msqrt(rho2 + x[2] * x[2]);
   const T ir = trcp(r);
@@ -1048,7 +1058,6 @@ __host__ __device__ inline T sampler_condition(const KParams& P, const T* x, con
     kpar2 = p * p * trcp(4.0 * d.a1 * d.a1 + d.a2 * d.a2 + d.a3 * d.a3);
   }
   const T ksqr = gtt * E2 + grr * w0 * w0 + ir2 * w1 * w1 + gpp * w2 * w2;
-  const double iE2 = 1.0 / E2;  // per attempt: hoisted out of the scan by the compiler
   return 0.5 * (ksqr + wp2 * (1.0 - grr * kpar2 * iE2)) * iE2;
 }
 

@@ -39,7 +39,7 @@ constexpr int END_REC = 16;
 constexpr int X_REC = 8;
 constexpr int N_STATS = 8;  // propagate statistics: attempts, accepted, root re-steps, scan evals,
                             // interpolant-root evals, rays, init RHS, (reserved)
-int persistent_blocks(const void* func, int64_t work);
+int persistent_blocks(const void* func, int64_t work, int block);
 // propagate = init (u0 of every ray) -> the persistent integrator -> finalize (Cartesian
 // end state, conversion probability at the crossings); ev0/ev1 (may be null) bracket the
 // integrator kernel alone.

@@ -332,7 +332,13 @@ __constant__ StageTable c_rk4 = {
 
 enum LaneMode { M_IDLE = 0, M_STEP = 2, M_ROOT = 3 };
 
-constexpr int BLOCK = 256;
+// Lanes per block of the persistent integrator. A block retires only when all its waves are
+// done, so smaller blocks free their CU slots sooner while a launch drains (the next launch,
+// on another stream, fills them).
+#ifndef ART_BLOCK
+#define ART_BLOCK 256
+#endif
+constexpr int BLOCK = ART_BLOCK;
 constexpr int SCAN_WORDS = 4;  // 2-bit codes for up to 64 grid points (interp_points <= 65)
 // Waves per SIMD the integrator is register-budgeted for (1: 512 VGPR+AGPR, 2: 256).
 #ifndef ART_WAVES_PER_SIMD
@@ -385,7 +391,7 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
   __shared__ unsigned codes[SCAN_WORDS * BLOCK];  // [word][lane]: 2-bit sign codes of the grid scan
   __shared__ double lastv[BLOCK];                 // value at the last grid point (before: b at the step's end)
   __shared__ double lastt[BLOCK];                 // t at the step's end (the scan certificate)
-  __shared__ int srcl[BLOCK];                     // compact list of the wave's scanning lanes
+  __shared__ unsigned char srcl[BLOCK];           // compact list of the wave's scanning lanes
   __shared__ double thgrid[SCAN_WORDS * 16 + 1];  // Θs = j/(npts-1): range(0, 1, length = npts)
   double* const L = lds + threadIdx.x;
   const int wbase = threadIdx.x & ~63;
@@ -646,35 +652,41 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
     L[(4 * 7 + 1) * BLOCK] = tau;
     const bool grid = scan && !cert;
     const unsigned long long smask = __ballot(grid);
+    // lanes polishing a crossing need the condition at the end of their re-step (th = 1 of the
+    // parked step): those items ride in the same pass, after the grid items
+    const unsigned long long rmask = __ballot(mode == M_ROOT);
     ART_TMARK(2)  // error norm, controller, certificate and parking
-    if (smask != 0ull) {
-      const int ns = __popcll(smask);
+    if ((smask | rmask) != 0ull) {
+      const int ns = __popcll(smask), nr = __popcll(rmask);
       if (grid) {
         srcl[wbase + __popcll(smask & ((1ull << lane) - 1ull))] = lane;
 #pragma unroll
         for (int w = 0; w < SCAN_WORDS; ++w) codes[w * BLOCK + threadIdx.x] = 0u;
       }
+      if (mode == M_ROOT) srcl[wbase + ns + __popcll(rmask & ((1ull << lane) - 1ull))] = lane;
       wave_lds_sync();
-      // item w = (j - 1) ns + c: point-major, advanced by 64 items per pass
-      const int total = ns * nper;
-      const int dj = 64 / ns, dc = 64 % ns;
-      int c = lane % ns, j = lane / ns + 1;
+      // grid item w = (j - 1) ns + c: point-major, advanced by 64 items per pass; then the
+      // root items
+      const int tg = ns * nper, total = tg + nr;
+      const int dj = ns ? 64 / ns : 0, dc = ns ? 64 % ns : 0;
+      int c = ns ? lane % ns : 0, j = ns ? lane / ns + 1 : 0;
 #pragma unroll 1
       for (int w0 = 0; w0 < total; w0 += 64) {
-        if (w0 + lane < total) {
-          const int src = srcl[wbase + c];
+        const int t = w0 + lane;
+        if (t < total) {  // one evaluation site for both kinds of item (no divergent second copy)
+          const bool gi = t < tg;
+          const int src = srcl[wbase + (gi ? c : ns + (t - tg))];
           double N, D;
-          scan_nd_lds(P, lds + wbase + src, BLOCK, thgrid[j], N, D);
-          unsigned code;
-          if (j == nper) {  // the end value opens the next step's brackets
-            const double cv = 0.5 * N / D;
+          scan_nd_lds(P, lds + wbase + src, BLOCK, gi ? thgrid[j] : 1.0, N, D);
+          if (!gi || j == nper) {  // a root item's value; the end value opens the next step's brackets
+            const double cv = 0.5 * N / D;  // = scan_point_lds, bit for bit
             lastv[wbase + src] = cv;
-            code = sign_code(cv);
-          } else {
-            code = sign_code_nd(N, D);
           }
-          atomicOr(&codes[((j - 1) >> 4) * BLOCK + wbase + src], code << (2 * ((j - 1) & 15)));
-          s_scan += 1;
+          if (gi) {
+            const unsigned code = (j == nper) ? sign_code(lastv[wbase + src]) : sign_code_nd(N, D);
+            atomicOr(&codes[((j - 1) >> 4) * BLOCK + wbase + src], code << (2 * ((j - 1) & 15)));
+            s_scan += 1;
+          }
         }
         c += dc;
         j += dj;
@@ -694,7 +706,7 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
     //     here only happen at brackets, Illinois points and root polish steps.
     //     ph: 0 done, 1 single point (INIT / ROOT), 2 walk codes, 3 Illinois, 5 value at the
     //     change point, 6 value at the bracket start, 7 value at the step's last nonzero point.
-    int ph = (mode == M_ROOT) ? 1 : (scan ? 2 : 0);
+    int ph = scan ? 2 : 0;  // (polishing lanes: their value came with the grid pass, below)
     int ip = 1, last_j = 0;
     int last_s = sprev;
     double last_c = cprev;
@@ -822,6 +834,10 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
       root_done = done;
       ph = 0;
     };
+    if (mode == M_ROOT) {  // the re-stepped end's value, from the grid pass
+      s_root += 1;
+      polish(lastv[threadIdx.x]);
+    }
     ART_TMARK(4)  // sign-code fast paths
     if (ph == 2) walk();
     ART_TMARK(5)  // code walk
@@ -1146,13 +1162,50 @@ __global__ __launch_bounds__(256) void finalize_kernel(const KParams P, const in
 
 // ---------------------------------------------------------------------------
 // find_samples_new (RayTracer.jl:1480-1653) + main_runner's erg and k_init
-// (MainRunner.jl:511-529): persistent lanes, one (ray, attempt) per lane per iteration.
+// (MainRunner.jl:511-529): persistent lanes, one ray per lane, one attempt per lane per outer
+// iteration; all lanes of a wave walk their lines' 0.5 km Euler steps in lockstep.
+//
+// Per step, the ContinuousCallback(interp_points = 20) scan (:1603-1613) is WAVE-COOPERATIVE:
+//   * a step whose every point is provably below the resonance (certified negative, below)
+//     needs only its last point -- the value the next step's first bracket starts from;
+//   * every other step needs its 19 points.
+// Those items (source lane, point) of the whole wave are evaluated 64 at a time by all lanes
+// on the source lines (kept in LDS), so one lane's uncertified step no longer makes the whole
+// wave evaluate 19 points. Each item leaves the signbit and nonzero-ness of its value in its
+// source lane's bit masks; a lane then finds its sign changes (the reference's brackets:
+// signbit differs, both values nonzero) with bit operations. Brackets are queued (in each
+// lane's order of discovery) and resolved 64 at a time -- Illinois on the exact line and the
+// affect! test (rr > rNS, E_loc > ωp, :1585-1597) -- and each lane then counts its valid
+// crossings in order and keeps the randInx-th (:1623-1636). Every value is computed by the same
+// expression on the same operands as a per-lane scan would, so the samples do not change.
+constexpr int SQCAP = 128;  // bracket queue entries per wave
+
+// closest approach of the line x0 + va s to the centre within [s0, s1], squared
+__device__ inline double line_rmin2(const double* x0, const double* va, double s0, double s1) {
+  const double sd = -(x0[0] * va[0] + x0[1] * va[1] + x0[2] * va[2]);
+  const double sm = fmin(fmax(sd, s0), s1);
+  double xm[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) xm[i] = x0[i] + va[i] * sm;
+  return xm[0] * xm[0] + xm[1] * xm[1] + xm[2] * xm[2];
+}
+
 __global__ __launch_bounds__(256) void sample_kernel(const KParams P, const double maxR, const uint64_t seed,
                                                      const int64_t ray_offset, const int64_t n, double* __restrict__ xo,
                                                      double* __restrict__ ko, double* __restrict__ ergo,
                                                      double* __restrict__ vifo, int32_t* __restrict__ wo,
                                                      int32_t* __restrict__ ao, unsigned long long* __restrict__ queue) {
+  // line data of every lane [component][lane]: x0 (3), va (3), vl (3), E, 1/E²
+  __shared__ double sline[11 * 256];
+  __shared__ double slast[256];           // value at the step's last point
+  __shared__ unsigned ssb[256], snz[256];  // bit j: signbit / nonzero of point j (bit 0: the step start)
+  __shared__ unsigned char ssrc[2 * 256];  // compact lists: uncertified lanes, certified lanes
+  __shared__ double sqa[4 * SQCAP], sqb[4 * SQCAP];  // bracket queue: ends -> root
+  __shared__ unsigned char sqsrc[4 * SQCAP], sqok[4 * SQCAP];
   const int lane = threadIdx.x & 63;
+  const int wb = threadIdx.x & ~63;
+  const int wq = (threadIdx.x >> 6) * SQCAP;
+  double* const Lx = sline + threadIdx.x;
   int64_t ray = -1;
   uint32_t attempt = 0;
   int64_t wnext = 0, wend = 0;
@@ -1160,9 +1213,11 @@ __global__ __launch_bounds__(256) void sample_kernel(const KParams P, const doub
   const double send = 2.2 * maxR;
   const int nsteps = (int)ceil(send / 0.5);
   const int np = 20;  // ContinuousCallback(interp_points=20) (:1603)
-  // certified-negative scan steps (below): GJ plasma without a boundary layer only
-  const bool cert_ok = !(P.bndry_lyr > 0.0) && P.mass_a > 0.0 && P.cert_fac < 1e300;  // ART_SCAN_CERT=0: off
+  const int nper = np - 1;
+  // certified-negative scan steps: GJ plasma without a boundary layer only (ART_SCAN_CERT=0: off)
+  const bool cert_ok = !(P.bndry_lyr > 0.0) && P.mass_a > 0.0 && P.cert_fac < 1e300;
   const double cert_lhs = 2.0 * P.wp2n, cert_rhs = P.mass_a2 * (1.0 - 1e-6);
+  const unsigned long long lt = (1ull << lane) - 1ull;
   while (true) {
     if (!exhausted) {
       unsigned long long need = __ballot(ray < 0);
@@ -1176,7 +1231,7 @@ __global__ __launch_bounds__(256) void sample_kernel(const KParams P, const doub
           wnext = (int64_t)base;
           wend = (wnext + CHUNK < n) ? wnext + CHUNK : n;
         }
-        const int rank = __popcll(need & ((1ull << lane) - 1ull));
+        const int rank = __popcll(need & lt);
         const int64_t avail = wend - wnext;
         const int take = (int)(avail < (int64_t)__popcll(need) ? avail : (int64_t)__popcll(need));
         if (ray < 0 && rank < take) { ray = wnext + rank; attempt = 0; }
@@ -1185,10 +1240,11 @@ __global__ __launch_bounds__(256) void sample_kernel(const KParams P, const doub
       }
     }
     if (__ballot(ray >= 0) == 0ull) break;
-    if (ray < 0) continue;
+    const bool active = ray >= 0;
 
+    // ---- one attempt of every active lane: its line (:1486-1531) ----
     double U[10];
-    attempt_uniforms(seed, uint64_t(ray_offset + ray), attempt, U);
+    attempt_uniforms(seed, uint64_t(ray_offset + (active ? ray : 0)), attempt, U);
     double sti, cti, spi, cpi, stl, ctl, spl, cpl, sR, cR;
     cti = 1.0 - 2.0 * U[0];
     sti = sin(acos(cti));
@@ -1209,17 +1265,77 @@ __global__ __launch_bounds__(256) void sample_kernel(const KParams P, const doub
     const double vmag = sqrt(vI[0] * vI[0] + vI[1] * vI[1] + vI[2] * vI[2]);
     const double gammaA = 1.0 / sqrt(1.0 - (vmag / C_KM) * (vmag / C_KM));
     const double E = P.mass_a * sqrt(1.0 + (vmag / C_KM * gammaA) * (vmag / C_KM * gammaA));
+    const double iE2 = 1.0 / (E * E);
 #pragma unroll
     for (int i = 0; i < 3; ++i) x0[i] += va[i] * (-maxR * 1.1);
     int randInx = 1 + (int)(U[9] * 6.0);
     if (randInx > 6) randInx = 6;
     int count = 0;
     double xsel[3] = {0.0, 0.0, 0.0};
-    double xl[3];
-    double s_prev = 0.0;
 #pragma unroll
-    for (int i = 0; i < 3; ++i) xl[i] = x0[i];
-    double c_prev = sampler_condition(P, xl, vl, E);
+    for (int i = 0; i < 3; ++i) {
+      Lx[i * 256] = x0[i];
+      Lx[(3 + i) * 256] = va[i];
+      Lx[(6 + i) * 256] = vl[i];
+    }
+    Lx[9 * 256] = E;
+    Lx[10 * 256] = iE2;
+    double s_prev = 0.0;
+    double c_prev = sampler_condition_e(P, x0, vl, E, iE2);
+    int qn = 0;  // queued brackets (wave-uniform)
+
+    // resolve the queued brackets: Illinois on the exact line (the lane that found one owns
+    // it), then each owner counts its valid crossings in queue order and keeps the randInx-th
+    auto flush = [&]() {
+      wave_lds_sync();
+      for (int t = lane; t < qn; t += 64) {
+        const int src = sqsrc[wq + t];
+        const double* S = sline + wb + src;
+        const double X0[3] = {S[0], S[256], S[2 * 256]}, VA[3] = {S[3 * 256], S[4 * 256], S[5 * 256]};
+        const double VL[3] = {S[6 * 256], S[7 * 256], S[8 * 256]};
+        const double Es = S[9 * 256], iEs = S[10 * 256];
+        double a = sqa[wq + t], b = sqb[wq + t], root = b;
+        double xr[3];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) xr[i] = X0[i] + VA[i] * a;
+        double fa = sampler_condition_e(P, xr, VL, Es, iEs);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) xr[i] = X0[i] + VA[i] * b;
+        double fb = sampler_condition_e(P, xr, VL, Es, iEs);
+        int side = 0;
+        for (int it = 0; it < 100; ++it) {  // Illinois on the exact line
+          root = a - fa * (b - a) / (fb - fa);
+#pragma unroll
+          for (int i = 0; i < 3; ++i) xr[i] = X0[i] + VA[i] * root;
+          const double fr = sampler_condition_e(P, xr, VL, Es, iEs);
+          if (fr == 0.0 || (b - a) < 1e-13 * fmax(1.0, fabs(root))) break;
+          if (signbit(fr) == signbit(fa)) { a = root; fa = fr; if (side == -1) fb *= 0.5; side = -1; }
+          else { b = root; fb = fr; if (side == 1) fa *= 0.5; side = 1; }
+        }
+#pragma unroll
+        for (int i = 0; i < 3; ++i) xr[i] = X0[i] + VA[i] * root;
+        // affect! (:1585-1597): keep crossings outside the star with E_loc > ωp
+        const double rr = sqrt(xr[0] * xr[0] + xr[1] * xr[1] + xr[2] * xr[2]);
+        double gtt, grr;
+        metric_tr(rr, P.rs_gr, gtt, grr);
+        sqa[wq + t] = root;
+        sqok[wq + t] = (rr > P.rNS && Es / sqrt(grr) > wp_cart(P, xr)) ? 1 : 0;
+      }
+      wave_lds_sync();
+      for (int t = 0; t < qn; ++t) {
+        if (sqsrc[wq + t] == lane && sqok[wq + t] && active) {
+          ++count;
+          if (count == randInx) {
+            const double r = sqa[wq + t];
+#pragma unroll
+            for (int i = 0; i < 3; ++i) xsel[i] = x0[i] + va[i] * r;
+          }
+        }
+      }
+      qn = 0;
+      wave_lds_sync();
+    };
+
     for (int st = 0; st < nsteps; ++st) {
       const double s0 = st * 0.5;
       const double s1 = fmin(s0 + 0.5, send);
@@ -1230,82 +1346,102 @@ __global__ __launch_bounds__(256) void sample_kernel(const KParams P, const doub
       // closest approach to the centre within [s0, s1]), all its points are negative. If the
       // point before is negative too, no sign change can occur: only the last point is
       // evaluated, for the value a bracket opening at the next step's first point starts from.
-      if (cert_ok && c_prev < 0.0) {
-        const double sd = -(x0[0] * va[0] + x0[1] * va[1] + x0[2] * va[2]);
-        const double sm = fmin(fmax(sd, s0), s1);
-        double xm[3];
+      bool cert = false;
+      if (active && cert_ok && c_prev < 0.0) {
+        const double rm2 = line_rmin2(x0, va, s0, s1);
+        cert = cert_lhs < cert_rhs * (rm2 * sqrt(rm2));
+      }
+      const bool unc = active && !cert;
+      const unsigned long long mU = __ballot(unc), mC = __ballot(active && cert);
+      const int nU = __popcll(mU), nC = __popcll(mC);
+      if (unc) ssrc[wb + __popcll(mU & lt)] = (unsigned char)lane;
+      if (active && cert) ssrc[256 + wb + __popcll(mC & lt)] = (unsigned char)lane;
+      ssb[threadIdx.x] = signbit(c_prev) ? 1u : 0u;
+      snz[threadIdx.x] = (c_prev != 0.0) ? 1u : 0u;
+      wave_lds_sync();
+      // items: (uncertified lane, point 1..nper) point-major, then (certified lane, point nper)
+      const int totU = nU * nper, tot = totU + nC;
+      for (int w0 = 0; w0 < tot; w0 += 64) {
+        const int t = w0 + lane;
+        if (t < tot) {
+          int src, j;
+          if (t < totU) {
+            j = t / nU + 1;
+            src = ssrc[wb + t % nU];
+          } else {
+            j = nper;
+            src = ssrc[256 + wb + (t - totU)];
+          }
+          const double* S = sline + wb + src;
+          const double sc = s0 + (s1 - s0) * double(j) / double(np - 1);
+          double xl[3];
 #pragma unroll
-        for (int i = 0; i < 3; ++i) xm[i] = x0[i] + va[i] * sm;
-        const double rm2 = xm[0] * xm[0] + xm[1] * xm[1] + xm[2] * xm[2];
-        if (cert_lhs < cert_rhs * (rm2 * sqrt(rm2))) {
-          const double sc = s0 + (s1 - s0) * double(np - 1) / double(np - 1);
-#pragma unroll
-          for (int i = 0; i < 3; ++i) xl[i] = x0[i] + va[i] * sc;
-          s_prev = sc;
-          c_prev = sampler_condition(P, xl, vl, E);
-          continue;
+          for (int i = 0; i < 3; ++i) xl[i] = S[i * 256] + S[(3 + i) * 256] * sc;
+          const double VL[3] = {S[6 * 256], S[7 * 256], S[8 * 256]};
+          const double v = sampler_condition_e(P, xl, VL, S[9 * 256], S[10 * 256]);
+          if (j == nper) slast[wb + src] = v;
+          atomicOr(&ssb[wb + src], (signbit(v) ? 1u : 0u) << j);
+          atomicOr(&snz[wb + src], (v != 0.0 ? 1u : 0u) << j);
         }
       }
-      for (int ip = 1; ip < np; ++ip) {
-        const double sc = s0 + (s1 - s0) * double(ip) / double(np - 1);
-#pragma unroll
-        for (int i = 0; i < 3; ++i) xl[i] = x0[i] + va[i] * sc;
-        const double cc = sampler_condition(P, xl, vl, E);
-        if (signbit(c_prev) != signbit(cc) && c_prev != 0.0 && cc != 0.0) {
-          double a = s_prev, b = sc, fa = c_prev, fb = cc, root = sc;
-          int side = 0;
-          for (int it = 0; it < 100; ++it) {  // Illinois on the exact line
-            root = a - fa * (b - a) / (fb - fa);
-            double xr[3];
-#pragma unroll
-            for (int i = 0; i < 3; ++i) xr[i] = x0[i] + va[i] * root;
-            const double fr = sampler_condition(P, xr, vl, E);
-            if (fr == 0.0 || (b - a) < 1e-13 * fmax(1.0, fabs(root))) break;
-            if (signbit(fr) == signbit(fa)) { a = root; fa = fr; if (side == -1) fb *= 0.5; side = -1; }
-            else { b = root; fb = fr; if (side == 1) fa *= 0.5; side = 1; }
-          }
-          double xr[3];
-#pragma unroll
-          for (int i = 0; i < 3; ++i) xr[i] = x0[i] + va[i] * root;
-          // affect! (:1585-1597): keep crossings outside the star with E_loc > ωp
-          const double rr = sqrt(xr[0] * xr[0] + xr[1] * xr[1] + xr[2] * xr[2]);
-          double gtt, grr;
-          metric_tr(rr, P.rs_gr, gtt, grr);
-          if (rr > P.rNS && E / sqrt(grr) > wp_cart(P, xr)) {
-            ++count;
-            if (count == randInx) { xsel[0] = xr[0]; xsel[1] = xr[1]; xsel[2] = xr[2]; }
-          }
+      wave_lds_sync();
+      // this lane's sign changes in (point j-1, point j]: signbits differ, both values nonzero
+      unsigned br = 0u;
+      const double s_start = s_prev;
+      if (active) {
+        if (unc) {
+          const unsigned sb = ssb[threadIdx.x], nz = snz[threadIdx.x];
+          br = (sb ^ (sb << 1)) & nz & (nz << 1) & (((1u << np) - 1u) & ~1u);
         }
-        s_prev = sc;
-        c_prev = cc;
+        c_prev = slast[threadIdx.x];
+        s_prev = s0 + (s1 - s0) * double(nper) / double(np - 1);
+      }
+      // queue the brackets, each lane's in its order along the line
+      unsigned long long bm = __ballot(br != 0u);
+      while (bm != 0ull) {
+        if (qn + 64 > SQCAP) flush();
+        if (br != 0u) {
+          const int ip = __builtin_ctz(br);
+          const int slot = qn + __popcll(bm & lt);
+          sqa[wq + slot] = (ip == 1) ? s_start : s0 + (s1 - s0) * double(ip - 1) / double(np - 1);
+          sqb[wq + slot] = s0 + (s1 - s0) * double(ip) / double(np - 1);
+          sqsrc[wq + slot] = (unsigned char)lane;
+          br &= br - 1u;
+        }
+        qn += __popcll(bm);
+        bm = __ballot(br != 0u);
       }
     }
-    const bool give_up = attempt + 1 >= 1000000u;  // bounded: no conversion surface reachable
-    if (count >= randInx || give_up) {
-      if (count < randInx) { xsel[0] = xsel[1] = xsel[2] = NAN; count = 0; }
-      const double rmag = sqrt(xsel[0] * xsel[0] + xsel[1] * xsel[1] + xsel[2] * xsel[2]);
-      const double vml = sqrt(vmag * vmag + 2.0 * P.GM_c2 * C_KM * C_KM / rmag) / C_KM;  // :1644
-      double vel[3], vc[3];
+    if (qn > 0) flush();
+
+    if (active) {
+      const bool give_up = attempt + 1 >= 1000000u;  // bounded: no conversion surface reachable
+      if (count >= randInx || give_up) {
+        if (count < randInx) { xsel[0] = xsel[1] = xsel[2] = NAN; count = 0; }
+        const double rmag = sqrt(xsel[0] * xsel[0] + xsel[1] * xsel[1] + xsel[2] * xsel[2]);
+        const double vml = sqrt(vmag * vmag + 2.0 * P.GM_c2 * C_KM * C_KM / rmag) / C_KM;  // :1644
+        double vel[3], vc[3];
 #pragma unroll
-      for (int i = 0; i < 3; ++i) { vel[i] = vl[i] * vml; vc[i] = vI[i] / C_KM; }
-      // MainRunner.jl:514-529: erg_inf_ini from vIfty/c, k_init = k_norm_Cart(ax_fix = true)
-      const double vm = sqrt(vc[0] * vc[0] + vc[1] * vc[1] + vc[2] * vc[2]);
-      const double gA = 1.0 / sqrt(1.0 - vm * vm);
-      const double Ei = P.mass_a * sqrt(1.0 + (vm * gA) * (vm * gA));
-      double kn[3];
-      k_norm_axion_shell(P, xsel, vel, Ei, kn);
+        for (int i = 0; i < 3; ++i) { vel[i] = vl[i] * vml; vc[i] = vI[i] / C_KM; }
+        // MainRunner.jl:514-529: erg_inf_ini from vIfty/c, k_init = k_norm_Cart(ax_fix = true)
+        const double vm = sqrt(vc[0] * vc[0] + vc[1] * vc[1] + vc[2] * vc[2]);
+        const double gA = 1.0 / sqrt(1.0 - vm * vm);
+        const double Ei = P.mass_a * sqrt(1.0 + (vm * gA) * (vm * gA));
+        double kn[3];
+        k_norm_axion_shell(P, xsel, vel, Ei, kn);
 #pragma unroll
-      for (int c = 0; c < 3; ++c) {
-        xo[c * n + ray] = xsel[c];
-        ko[c * n + ray] = kn[c];
-        vifo[c * n + ray] = vc[c];
+        for (int c = 0; c < 3; ++c) {
+          xo[c * n + ray] = xsel[c];
+          ko[c * n + ray] = kn[c];
+          vifo[c * n + ray] = vc[c];
+        }
+        ergo[ray] = Ei;
+        wo[ray] = count;
+        ao[ray] = (int32_t)(attempt + 1);
+        ray = -1;
+      } else {
+        ++attempt;
       }
-      ergo[ray] = Ei;
-      wo[ray] = count;
-      ao[ray] = (int32_t)(attempt + 1);
-      ray = -1;
-    } else {
-      ++attempt;
     }
   }
 }
@@ -1470,12 +1606,12 @@ __global__ __launch_bounds__(256) void event_weight_kernel(const KParams P, cons
 
 // ---------------------------------------------------------------------------
 // host-side launch wrappers (art_internal.h)
-int persistent_blocks(const void* func, int64_t work) {
+int persistent_blocks(const void* func, int64_t work, int block) {
   int dev = 0, ncu = 0, per_cu = 0;
   (void)hipGetDevice(&dev);
   (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, func, 256, 0) != hipSuccess || per_cu < 1) per_cu = 1;
-  const int64_t need = (work + 255) / 256;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, func, block, 0) != hipSuccess || per_cu < 1) per_cu = 1;
+  const int64_t need = (work + block - 1) / block;
   const int64_t full = (int64_t)ncu * per_cu;
   return (int)(need < full ? need : full);
 }
@@ -1502,7 +1638,7 @@ hipError_t launch_propagate(const KParams& P, int64_t n, const SegIn& in, const 
     fn = rk4 ? (flat ? propagate_kernel<ART_RK4, GEOM_FLAT, false> : propagate_kernel<ART_RK4, GEOM_ANY, false>)
              : (flat ? propagate_kernel<ART_VERN6, GEOM_FLAT, false>
                      : (sch ? propagate_kernel<ART_VERN6, GEOM_GR, false> : propagate_kernel<ART_VERN6, GEOM_ANY, false>));
-  const int grid = persistent_blocks((const void*)fn, n);
+  const int grid = persistent_blocks((const void*)fn, n, BLOCK);
   if (grid_out) *grid_out = grid;
   if (ev0 && (e = hipEventRecord(ev0, s)) != hipSuccess) return e;
   hipLaunchKernelGGL(fn, dim3(grid), dim3(BLOCK), 0, s, P, n, in, out, max_crossings, queue, stats);
@@ -1515,7 +1651,7 @@ hipError_t launch_propagate(const KParams& P, int64_t n, const SegIn& in, const 
 hipError_t launch_sample(const KParams& P, double maxR, uint64_t seed, int64_t ray_offset, int64_t n, double* x,
                          double* k, double* erg, double* vifty, int32_t* w, int32_t* att, unsigned long long* queue,
                          hipStream_t s) {
-  const int grid = persistent_blocks((const void*)sample_kernel, n);
+  const int grid = persistent_blocks((const void*)sample_kernel, n, 256);
   hipLaunchKernelGGL(sample_kernel, dim3(grid), dim3(256), 0, s, P, maxR, seed, ray_offset, n, x, k, erg, vifty, w, att,
                      queue);
   return hipGetLastError();

@@ -64,15 +64,88 @@ def run_point(kw: dict, rays: int, seed: int = 1769, nbins: int = 50, device: in
                 attempts=st["attempts"], status_counts=status, flux_photon=hist[nbins:].tolist())
 
 
-def run_scan(rays: int, n_points: int | None = None, seed: int = 1769, run=run_point) -> list[dict]:
-    """This rank's share of the grid; with WORLD_SIZE > 1 the records are gathered on every
-    rank (all_gather_object) and returned in grid order."""
+def run_points(kws: list[dict], rays: int, seed: int = 1769, nbins: int = 50, device: int = 0,
+               streams: int = 4) -> tuple[list[dict], dict]:
+    """Several grid points on one GPU, `streams` of them in flight: every point's forward
+    roots are sampled first, then the points are propagated on `streams` HIP streams round
+    robin -- each launch has its own device scratch (include/art.h), so a point's drain tail
+    (its last long rays on a few CUs; 130-900 ms per 1e6-ray point when run alone) overlaps
+    the other points' bulk -- and each point's flux is binned on its stream. Returns the
+    per-point records and a summary of the propagate phase (wall time, Σ accepted steps)."""
+    import ctypes as C
+
+    import torch
+
+    import adiabatic_raytracer_amd as A
+    from adiabatic_raytracer_amd import Engine
+    t0 = time.perf_counter()
+    engs, inps, recs = [], [], []
+    for kw in kws:
+        p = A.Params(**kw)
+        eng = Engine(p, device=device)
+        max_r = p.max_r()
+        rec = dict(kw, rays=rays, max_r_km=max_r)
+        recs.append(rec)
+        if max_r < p.rNS:  # no conversion surface outside the star (MainRunner.jl:387-396)
+            rec["skipped"] = "maxR < rNS"
+            engs.append(None)
+            inps.append(None)
+            continue
+        engs.append(eng)
+        inps.append(eng.forward_roots(rays, seed=seed))
+    torch.cuda.synchronize()
+    t_sample = time.perf_counter() - t0
+    main = torch.cuda.current_stream()
+    ss = [main] + [torch.cuda.Stream() for _ in range(max(1, streams) - 1)]
+    for s_ in ss[1:]:
+        s_.wait_stream(main)
+    outs, hists = [None] * len(kws), [None] * len(kws)
+    t1 = time.perf_counter()
+    k = 0
+    for i, eng in enumerate(engs):
+        if eng is None:
+            continue
+        with torch.cuda.stream(ss[k % len(ss)]):
+            outs[i] = eng.propagate(inps[i], max_crossings=-1)
+            hists[i] = eng.flux_histogram(outs[i], inps[i]["species"], None, nbins)
+        k += 1
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t1
+    ms = (C.c_double * max(1, k))()
+    got = A._lib.load().art_recent_kernel_ms(k, ms)
+    kms = list(ms)[:max(0, got)]
+    acc_total, j = 0, 0
+    for i, eng in enumerate(engs):
+        if eng is None:
+            continue
+        o = outs[i]
+        acc = int(o["n_accept"].sum().item())
+        att = acc + int(o["n_reject"].sum().item())
+        acc_total += acc
+        recs[i].update(kernel_ms=kms[j] if j < len(kms) else None, accepted=acc, attempts=att,
+                       status_counts=torch.bincount(o["status"].long(), minlength=5).tolist(),
+                       flux_photon=hists[i][nbins:].tolist())
+        j += 1
+    summary = {"points": k, "streams": len(ss), "sample_s": t_sample, "propagate_wall_s": wall,
+               "accepted": acc_total, "kernel_ray_steps_per_s": acc_total / wall if wall > 0 else None}
+    return recs, summary
+
+
+def run_scan(rays: int, n_points: int | None = None, seed: int = 1769, run=None, streams: int = 4):
+    """This rank's share of the grid (run_points, or `run` point by point); with
+    WORLD_SIZE > 1 the records are gathered on every rank (all_gather_object) and returned in
+    grid order."""
     import torch.distributed as dist
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     grid = scan_grid()[:n_points]
-    mine = [dict(run(grid[i], rays, seed, device=local), point=i) for i in points_of_rank(len(grid), rank, world)]
+    idx = points_of_rank(len(grid), rank, world)
+    if run is None:
+        recs, _ = run_points([grid[i] for i in idx], rays, seed, device=local, streams=streams)
+        mine = [dict(r, point=i) for r, i in zip(recs, idx)]
+    else:
+        mine = [dict(run(grid[i], rays, seed, device=local), point=i) for i in idx]
     if world == 1:
         return mine
     parts = [None] * world
@@ -86,6 +159,7 @@ def main():
     ap.add_argument("--points", type=int, default=None)
     ap.add_argument("--seed", type=int, default=1769)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--streams", type=int, default=4)
     args = ap.parse_args()
     import torch
     import torch.distributed as dist
@@ -94,7 +168,7 @@ def main():
         local = int(os.environ.get("LOCAL_RANK", "0"))
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    recs = run_scan(args.rays, args.points, args.seed)
+    recs = run_scan(args.rays, args.points, args.seed, streams=args.streams)
     if int(os.environ.get("RANK", "0")) == 0:
         lines = "\n".join(json.dumps(r) for r in recs)
         if args.out:

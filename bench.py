@@ -15,6 +15,7 @@ contiguous blocks (strong scaling of the fixed 1e7-ray batch named by BASELINE.j
 Rank 0 prints ONE JSON line.
 """
 import argparse
+import ctypes as C
 import json
 import os
 import sys
@@ -133,6 +134,7 @@ def main():
     ap.add_argument("--integrator", default="vern6", choices=["vern6", "rk4"])
     ap.add_argument("--seed", type=int, default=1769)
     ap.add_argument("--nbins", type=int, default=50)
+    ap.add_argument("--streams", type=int, default=2, help="batches in flight (HIP streams)")
     ap.add_argument("--cpu-rays", type=int, default=int(os.environ.get("ART_CPU_RAYS", "500000")))
     ap.add_argument("--cpu-rays-1t", type=int, default=int(os.environ.get("ART_CPU_RAYS_1T", "24000")))
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -170,34 +172,50 @@ def main():
     inp = eng.forward_roots(n, seed=args.seed, ray_offset=lo)
     torch.cuda.synchronize()
     sample_s = time.perf_counter() - t_s
-    out = eng.alloc_out(n, capacity=1)
-    hist = torch.zeros(2 * args.nbins, dtype=torch.float64, device=eng.device)
+    # `streams` batches in flight: step i runs on stream i % streams with its own outputs, so
+    # the drain tail of one pass (its last long rays on a few CUs) overlaps the next pass's
+    # bulk instead of idling the GPU. Each launch has its own scratch (include/art.h).
+    streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(args.streams - 1)]
+    for st_ in streams[1:]:
+        st_.wait_stream(streams[0])  # the sampled inputs
+    outs = [eng.alloc_out(n, capacity=1) for _ in streams]
+    hists = [torch.zeros(2 * args.nbins, dtype=torch.float64, device=eng.device) for _ in streams]
+    out, hist = outs[0], hists[0]
 
-    def one_step():
-        eng.propagate(inp, out, max_crossings=-1)
-        hist.zero_()
-        eng.flux_histogram(out, inp["species"], None, args.nbins, hist)
-        allreduce_flux(hist, world)  # the only data-path collective: the binned flux (RCCL over xGMI)
+    def one_step(i):
+        k = i % len(streams)
+        with torch.cuda.stream(streams[k]):
+            eng.propagate(inp, outs[k], max_crossings=-1)
+            hists[k].zero_()
+            eng.flux_histogram(outs[k], inp["species"], None, args.nbins, hists[k])
+            allreduce_flux(hists[k], world)  # the only data-path collective: the binned flux (RCCL over xGMI)
 
-    for _ in range(args.warmup):
-        one_step()
+    for i in range(args.warmup):
+        one_step(i)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    kernel_ms, accepted, stats_last = [], 0, None
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        one_step()
-        kernel_ms.append(eng.kernel_ms())  # HIP events on the propagate kernel's stream
-        st = A.raytracer.last_stats()
-        accepted += st["accepted"]
-        stats_last = st
+    for i in range(args.steps):
+        one_step(args.warmup + i)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    # per-launch integrator durations (HIP events on each launch's own stream) and the
+    # launch's counters; every step integrates the same batch, so its accepted steps are
+    # the same each time (checked against the outputs)
+    kms_buf = (C.c_double * args.steps)()
+    got = A._lib.load().art_recent_kernel_ms(args.steps, kms_buf)
+    kernel_ms = list(kms_buf)[:max(0, got)]
+    eng.kernel_ms()  # latches the last launch's counters
+    stats_last = A.raytracer.last_stats()
+    k_last = (args.warmup + args.steps - 1) % len(streams)
+    out, hist = outs[k_last], hists[k_last]
+    assert int(out["n_accept"].sum().item()) == stats_last["accepted"]
+    accepted = stats_last["accepted"] * args.steps
     # whole-job aggregates: Σ ray-steps over ranks / max wall time over ranks
     total_steps, t_max, total_rays = reduce_totals(accepted, elapsed, n, world, device=eng.device)
 
@@ -241,11 +259,13 @@ def main():
                        else f"{args.rays} rays",
                        "m_a_eV": params.mass_a, "theta_m": params.theta_m, "omega_pul": params.omega_pul,
                        "B0_G": params.B0, "rNS_km": params.rNS, "abstol": params.abstol, "reltol": params.reltol,
-                       "interp_points": params.interp_points, "parallelism": f"rays sharded x{world}"},
+                       "interp_points": params.interp_points, "parallelism": f"rays sharded x{world}",
+                       "streams": args.streams},
             "roofline": {"bound": "fp64-valu", "achieved": achieved, "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
                          "frac": achieved / PEAK_FP64_TFLOPS, "traffic": traffic,
                          "kernel": f"propagate_kernel<{'RK4' if args.integrator == 'rk4' else 'Vern6'}>", "kernel_ms": kms,
                          "flops_per_launch": fpl, "flops_per_ray_step": fpl / stats_last["accepted"],
+                         "achieved_wall": fpl * args.steps / elapsed / 1e12,
                          "note": "FP64 VALU-bound (state in VGPRs, ~1 B of HBM per ray-step); peak = 78.6 TFLOP/s "
                                  "FP64 (vector = matrix dense peak). FLOPs from the kernel's counters x "
                                  "tools/flops.json (instrumented restatement).",
