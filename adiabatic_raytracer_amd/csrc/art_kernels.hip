@@ -1346,10 +1346,37 @@ __global__ __launch_bounds__(256) void sample_kernel(const KParams P, const doub
       // closest approach to the centre within [s0, s1]), all its points are negative. If the
       // point before is negative too, no sign change can occur: only the last point is
       // evaluated, for the value a bracket opening at the next step's first point starts from.
+      //
+      // Both bounds use b = Bz/B_n at the step's start point, b = cosθm (3z² - r²)/r² +
+      // 3 sinθm x z / r² (ψ = φ at t = 0), and its Lipschitz bound on the unit sphere,
+      // |∇b| <= |∂θ b| + |∂φ b|/sinθ <= 3 + 3|sinθm|, over the step's angular extent <= L/r_min
+      // (the radial projection shrinks lengths by 1/|x|): so |b| <= min(2, |b_a| + db) along the
+      // step, and |b| >= |b_a| - db.
+      //  * negative: ωp² <= wp2n |b|max / r_min³ < m_a² (see above);
+      //  * positive (the point before positive too): outside g_schwartz's interior patch
+      //    (r > 10 km), g^rr g^tt = -1, so Cauchy-Schwarz on k∥ with w on the axion shell gives
+      //    1 - g^rr k∥²/E² >= g^rr m_a²/E² and the condition >= ½ m_a² (ωp² g^rr/E² - 1)/E² > 0
+      //    when wp2n |b|min g^rr(r_min) > E² r_max³ (r_max: at an end of the step).
       bool cert = false;
-      if (active && cert_ok && c_prev < 0.0) {
+      if (active && cert_ok && c_prev != 0.0 && !isnan(c_prev)) {
         const double rm2 = line_rmin2(x0, va, s0, s1);
-        cert = cert_lhs < cert_rhs * (rm2 * sqrt(rm2));
+        const double rmin = sqrt(rm2);
+        double xa[3], xb[3];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) { xa[i] = x0[i] + va[i] * s0; xb[i] = x0[i] + va[i] * s1; }
+        const double ra2 = xa[0] * xa[0] + xa[1] * xa[1] + xa[2] * xa[2];
+        const double rb2 = xb[0] * xb[0] + xb[1] * xb[1] + xb[2] * xb[2];
+        const double ba = (P.cm * (3.0 * xa[2] * xa[2] - ra2) + 3.0 * P.sm * xa[0] * xa[2]) / ra2;
+        const double db = (3.0 + 3.0 * fabs(P.sm)) * (s1 - s0) / rmin * (1.0 + 1e-9) + 1e-9;
+        if (c_prev < 0.0) {
+          const double bmax = fmin(2.0, fabs(ba) + db);
+          cert = cert_lhs * 0.5 * bmax < cert_rhs * (rm2 * rmin);
+        } else if (rmin > 10.0) {
+          const double bmin = fabs(ba) - db;
+          const double rmax2 = fmax(ra2, rb2);
+          const double grr = 1.0 - P.rs_gr / rmin;
+          cert = bmin > 0.0 && P.wp2n * bmin * grr > E * E * (1.0 + 1e-6) * (rmax2 * sqrt(rmax2));
+        }
       }
       const bool unc = active && !cert;
       const unsigned long long mU = __ballot(unc), mC = __ballot(active && cert);

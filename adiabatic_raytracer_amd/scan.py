@@ -65,12 +65,14 @@ def run_point(kw: dict, rays: int, seed: int = 1769, nbins: int = 50, device: in
 
 
 def run_points(kws: list[dict], rays: int, seed: int = 1769, nbins: int = 50, device: int = 0,
-               streams: int = 4) -> tuple[list[dict], dict]:
+               streams: int = 16) -> tuple[list[dict], dict]:
     """Several grid points on one GPU, `streams` of them in flight: every point's forward
     roots are sampled first, then the points are propagated on `streams` HIP streams round
     robin -- each launch has its own device scratch (include/art.h), so a point's drain tail
     (its last long rays on a few CUs; 130-900 ms per 1e6-ray point when run alone) overlaps
-    the other points' bulk -- and each point's flux is binned on its stream. Returns the
+    the other points' bulk -- and each point's flux is binned on its stream. Streams only run
+    concurrently up to the process's hardware queues: main() raises GPU_MAX_HW_QUEUES to 16
+    (HIP's default is 4; 16 streams measured fastest on one MI355X). Returns the
     per-point records and a summary of the propagate phase (wall time, Σ accepted steps)."""
     import ctypes as C
 
@@ -78,6 +80,10 @@ def run_points(kws: list[dict], rays: int, seed: int = 1769, nbins: int = 50, de
 
     import adiabatic_raytracer_amd as A
     from adiabatic_raytracer_amd import Engine
+    main = torch.cuda.current_stream()
+    ss = [main] + [torch.cuda.Stream() for _ in range(max(1, streams) - 1)]
+    for s_ in ss[1:]:
+        s_.wait_stream(main)
     t0 = time.perf_counter()
     engs, inps, recs = [], [], []
     for kw in kws:
@@ -92,20 +98,17 @@ def run_points(kws: list[dict], rays: int, seed: int = 1769, nbins: int = 50, de
             inps.append(None)
             continue
         engs.append(eng)
-        inps.append(eng.forward_roots(rays, seed=seed))
+        with torch.cuda.stream(ss[len(inps) % len(ss)]):  # the samplers' tails overlap too
+            inps.append(eng.forward_roots(rays, seed=seed))
     torch.cuda.synchronize()
     t_sample = time.perf_counter() - t0
-    main = torch.cuda.current_stream()
-    ss = [main] + [torch.cuda.Stream() for _ in range(max(1, streams) - 1)]
-    for s_ in ss[1:]:
-        s_.wait_stream(main)
     outs, hists = [None] * len(kws), [None] * len(kws)
     t1 = time.perf_counter()
     k = 0
     for i, eng in enumerate(engs):
         if eng is None:
             continue
-        with torch.cuda.stream(ss[k % len(ss)]):
+        with torch.cuda.stream(ss[i % len(ss)]):
             outs[i] = eng.propagate(inps[i], max_crossings=-1)
             hists[i] = eng.flux_histogram(outs[i], inps[i]["species"], None, nbins)
         k += 1
@@ -131,7 +134,7 @@ def run_points(kws: list[dict], rays: int, seed: int = 1769, nbins: int = 50, de
     return recs, summary
 
 
-def run_scan(rays: int, n_points: int | None = None, seed: int = 1769, run=None, streams: int = 4):
+def run_scan(rays: int, n_points: int | None = None, seed: int = 1769, run=None, streams: int = 16):
     """This rank's share of the grid (run_points, or `run` point by point); with
     WORLD_SIZE > 1 the records are gathered on every rank (all_gather_object) and returned in
     grid order."""
@@ -159,8 +162,12 @@ def main():
     ap.add_argument("--points", type=int, default=None)
     ap.add_argument("--seed", type=int, default=1769)
     ap.add_argument("--out", default=None)
-    ap.add_argument("--streams", type=int, default=4)
+    ap.add_argument("--streams", type=int, default=16)
     args = ap.parse_args()
+    # concurrent kernels need hardware queues: one per stream in flight (read at HIP init)
+    want = min(16, max(4, args.streams))
+    if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < want:
+        os.environ["GPU_MAX_HW_QUEUES"] = str(want)
     import torch
     import torch.distributed as dist
     world = int(os.environ.get("WORLD_SIZE", "1"))

@@ -134,7 +134,8 @@ def main():
     ap.add_argument("--integrator", default="vern6", choices=["vern6", "rk4"])
     ap.add_argument("--seed", type=int, default=1769)
     ap.add_argument("--nbins", type=int, default=50)
-    ap.add_argument("--streams", type=int, default=2, help="batches in flight (HIP streams)")
+    ap.add_argument("--streams", type=int, default=0,
+                    help="batches in flight (HIP streams); 0: 1 for per-GPU batches of >= 4e6 rays, else 2")
     ap.add_argument("--cpu-rays", type=int, default=int(os.environ.get("ART_CPU_RAYS", "500000")))
     ap.add_argument("--cpu-rays-1t", type=int, default=int(os.environ.get("ART_CPU_RAYS_1T", "24000")))
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -175,6 +176,12 @@ def main():
     # `streams` batches in flight: step i runs on stream i % streams with its own outputs, so
     # the drain tail of one pass (its last long rays on a few CUs) overlaps the next pass's
     # bulk instead of idling the GPU. Each launch has its own scratch (include/art.h).
+    if args.streams <= 0:
+        # the drain tail (~3 ms: the last long rays) is ~3% of a 1e7-ray pass but ~20% of the
+        # 1.25e6 rays per GPU of the 8-GPU split; overlapping two passes hides part of it there.
+        # Overlapped launches also stretch each other's measured duration, so the roofline of
+        # the single-GPU headline is taken without overlap.
+        args.streams = 1 if n >= 4_000_000 else 2
     streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(args.streams - 1)]
     for st_ in streams[1:]:
         st_.wait_stream(streams[0])  # the sampled inputs

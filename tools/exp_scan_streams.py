@@ -8,7 +8,9 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from adiabatic_raytracer_amd.scan import run_points, scan_grid  # noqa: E402
 
 rays = int(sys.argv[1]) if len(sys.argv) > 1 else 1_000_000
-streams = int(sys.argv[2]) if len(sys.argv) > 2 else 4
+streams = int(sys.argv[2]) if len(sys.argv) > 2 else 16
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < min(16, max(4, streams)):
+    os.environ["GPU_MAX_HW_QUEUES"] = str(min(16, max(4, streams)))
 npts = int(sys.argv[3]) if len(sys.argv) > 3 else 32
 recs, summ = run_points(scan_grid()[:npts], rays, streams=streams)
 for i, r in enumerate(recs):
