@@ -18,7 +18,7 @@ for grp in "FETCH_SIZE" "WRITE_SIZE" \
            "SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_INST_ANY SQ_WAIT_ANY"; do
   i=$((i+1))
   timeout -k 10 300 rocprofv3 --kernel-trace --pmc $grp -d "$OUT/kernel/pass$i" -o pass$i --output-format csv \
-    -- python3 bench.py --rays "$RAYS" --steps 1 --warmup 0 --no-cpu-baseline > "$OUT/pass$i.log" 2>&1 \
+    -- python3 bench.py --rays "$RAYS" --steps 1 --warmup 0 --no-cpu-baseline --no-pcie > "$OUT/pass$i.log" 2>&1 \
     || { echo "pass $i ($grp) failed"; exit 1; }
 done
 python3 tools/pmc_summary.py "$OUT" "flat:$RAYS" "$OUT/pmc_summary.json"
