@@ -432,6 +432,9 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
 #else
 #define ART_TMARK(k)
 #endif
+#ifdef ART_COUNT_SUB
+  unsigned s_sub[4] = {0, 0, 0, 0};  // dev: uncertified steps, uniform 7-point sub-intervals, uniform +/- steps
+#endif
 #ifdef ART_COUNT_LOOPS
   unsigned s_lane_it = 0, s_main_it = 0;  // dev counters: wave iterations of the per-lane and main loops
   unsigned s_ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // per-lane evaluations by phase
@@ -530,7 +533,8 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
       // whose results nothing reads -- so the slot has no divergent control flow. Axion
       // segments (the tree driver's batches) take a wave-uniform detour and a select.
       double aux[2];
-      rhs_photon(P, y, ty, erg, kk, aux);
+      if constexpr (GEOM == GEOM_FLAT) rhs_photon_flat(P, y, ty, erg, kk, aux);
+      else rhs_photon(P, y, ty, erg, kk, aux);
       if (s == NSLOT - 1) {  // the end point's b and t for the scan certificate (lastv and codes are free)
         lastv[threadIdx.x] = aux[0];
         lastt[threadIdx.x] = aux[1];
@@ -716,6 +720,28 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
 #pragma unroll
       for (int w = 0; w < SCAN_WORDS; ++w)
         cw[w] = cert ? 0x55555555u * (unsigned)ccode : codes[w * BLOCK + threadIdx.x];
+#ifdef ART_COUNT_SUB
+      // dev: how much of the uncertified steps' grid a sub-interval certificate could skip:
+      // sub-intervals of 7 grid points whose codes are one nonzero sign / all NaN
+      if (!cert) {
+        s_sub[0] += 1;
+        bool all = true;
+        const unsigned first = cw[0] & 3u;
+        for (int k = 0; k < 7; ++k) {
+          const int j0 = 7 * k;
+          const unsigned c0 = (cw[j0 >> 4] >> (2 * (j0 & 15))) & 3u;
+          bool uni = c0 != 0u;
+          for (int jj = 1; jj < 7; ++jj) {
+            const int q = j0 + jj;
+            uni = uni && (((cw[q >> 4] >> (2 * (q & 15))) & 3u) == c0);
+          }
+          s_sub[1] += uni ? 1u : 0u;
+          all = all && uni && c0 == first;
+        }
+        s_sub[2] += (all && first == 1u) ? 1u : 0u;  // uniform positive steps
+        s_sub[3] += (all && first == 2u) ? 1u : 0u;  // uniform negative steps
+      }
+#endif
       // fast path: every grid point has the previous sign (or the previous sign is unknown
       // and every point has one common nonzero sign)
       const unsigned s0 = cw[0] & 3u;
@@ -1033,6 +1059,8 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
 #else
 #if defined(ART_COUNT_LOOPS)
   const unsigned v[7] = {s_main_it, s_lane_it, s_ph[1], s_ph[3], s_ph[5], s_ph[6], s_ph[7]};
+#elif defined(ART_COUNT_SUB)
+  const unsigned v[7] = {s_att, s_acc, s_sub[0], s_sub[1], s_sub[2], s_sub[3], s_cert};
 #else
   const unsigned v[7] = {s_att, s_acc, s_root, s_scan, s_interp, s_rays, s_cert};
 #endif
