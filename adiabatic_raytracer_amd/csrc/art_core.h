@@ -692,10 +692,11 @@ __host__ __device__ inline Hull bernstein_hull(double a, double fa, double b, do
 // the step, where the reference's √NrmSq is undefined and condition_nd returns NaN), or 0
 // when nothing is certain.
 // b1 = Bz/B_n and t1 = e^(τ + h) at the end point come from the step's last RHS evaluation
-// (rhs_photon's aux), so the certificate needs no transcendental of its own.
+// (rhs_photon's aux), so the certificate needs no transcendental of its own. b0, b at the
+// start point (the previous step's last RHS; NaN when unknown), tightens the range of b.
 __host__ __device__ inline int scan_certified_code(const KParams& P, const double* u0, const double* f0,
                                                    const double* u1, const double* f1, double h, double b1,
-                                                   double t1) {
+                                                   double t1, double b0 = NAN) {
   if (!(P.cert_fac < 1e300)) return 0;
   const Hull r = bernstein_hull(u0[0], f0[0], u1[0], f1[0], h);
   if (!(r.lo > P.cert_rmin)) return 0;
@@ -712,12 +713,26 @@ __host__ __device__ inline int scan_certified_code(const KParams& P, const doubl
   const double dth = fmax(th.hi - u1[1], u1[1] - th.lo);
   const double dps = fmax(ph.hi - u1[2], u1[2] - ph.lo) + fabs(P.omega) * t1 * h * (1.0 + 1e-12);
   const double db = 3.0 * dth + 1.5 * fabs(P.sm) * dps + 1e-12;
-  const double bmax = fmin(2.0, fabs(b1) + db);
+  double bmax = fmin(2.0, fabs(b1) + db);
+  double bmin = fabs(b1) - db;
+  if (b0 == b0) {
+    // Two-sided: along the step b moves by at most ℓ = 3 TV(θ) + 1.5|sinθm| TV(ψ) in total
+    // (TV: total variation; a Bézier curve's is at most its control polygon's, and
+    // TV(ψ) <= TV(φ) + |ω| (t1 - t0)). A point at variation d0 from the start and d1 from the
+    // end (d0 + d1 <= ℓ) has b >= max(b0 - d0, b1 - d1) >= (b0 + b1 - ℓ)/2, and likewise
+    // b <= (b0 + b1 + ℓ)/2: half the one-sided slack when the path is monotone.
+    const double h3 = h * (1.0 / 3.0);
+    const double tvt = fabs(h3 * f0[1]) + fabs((u1[1] - h3 * f1[1]) - (u0[1] + h3 * f0[1])) + fabs(h3 * f1[1]);
+    const double tvp = fabs(h3 * f0[2]) + fabs((u1[2] - h3 * f1[2]) - (u0[2] + h3 * f0[2])) + fabs(h3 * f1[2]);
+    const double ell = (3.0 * tvt + 1.5 * fabs(P.sm) * (tvp + fabs(P.omega) * t1 * h)) * (1.0 + 1e-12) + 1e-12;
+    const double lo = 0.5 * (b0 + b1 - ell), hi = 0.5 * (b0 + b1 + ell);
+    bmax = fmin(bmax, fmax(fabs(lo), fabs(hi)));
+    bmin = fmax(bmin, lo > 0.0 ? lo : (hi < 0.0 ? -hi : 0.0));
+  }
   if (P.wp2n * bmax * P.cert_fac < P.mass_a2 * (r.lo * r.lo * r.lo)) return 2;
   // positive: with ωp² g^rr > u7² everywhere. Cauchy-Schwarz gives B/A = g^rr num PP²/(DEN β E²)
   // <= g^rr num / E² = 1 - g^rr m_a² / E² (g^rr (-g^tt) = 1 outside 10 km), so
   // N / (r³ A) >= ωp² g^rr m_a² / E² - m_a² > 0. It needs r > rNS everywhere (zeroIn).
-  const double bmin = fabs(b1) - db;
   const double grr_lo = P.rs_eff == 0.0 ? 1.0 : 1.0 - P.rs_eff / r.lo;
   if (r.lo > P.rNS && bmin > 0.0 &&
       P.wp2n * bmin * grr_lo > ehi * ehi * P.cert_fac * (r.hi * r.hi * r.hi))

@@ -409,6 +409,7 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
   const double qpow_init = pow(1e-4, 1.0 / 15.0);
   double u[7], f[7], tau = 0.0, dt = 0.0, qpow = qpow_init;
   double cprev = 0.0;
+  double bstart = NAN;  // Bz/B_n at u (the previous step's last RHS) for the scan certificate
   bool cprev_ok = true;  // cprev holds the condition at the step start (false after a certified step)
   int sprev = 0;
   bool just_evented = false;
@@ -474,6 +475,7 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
           dt = in.u0[14 * n + ray];
           cprev = in.u0[15 * n + ray];
           cprev_ok = true;
+          bstart = NAN;
           sprev = isnan(cprev) ? 0 : sgn(cprev);
           tau = in.lnt0[ray];
           n_acc = n_rej = ncross = iter = 0;
@@ -638,8 +640,9 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
     //     cprev_ok = false).
     // without callbacks (make_tree = false: ART_NO_CALLBACKS) every step is "certified NaN":
     // no sign change can open a bracket, so nothing is scanned or recorded
-    const int ccode = !scan ? 0
-                      : (cbs ? scan_certified_code(P, u, f, y, kk, hs, lastv[threadIdx.x], lastt[threadIdx.x]) : 3);
+    const double bend = lastv[threadIdx.x];
+    const int ccode =
+        !scan ? 0 : (cbs ? scan_certified_code(P, u, f, y, kk, hs, bend, lastt[threadIdx.x], bstart) : 3);
     const bool cert = ccode != 0;
     s_cert += cert ? 1u : 0u;
     // every lane parks (u, f, y, kk, h, τ) in its LDS slots (free after the error estimate):
@@ -1010,6 +1013,7 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
       }
     }
     if (hit) mode = M_ROOT;
+    if (root_done || (scan && !hit)) bstart = bend;
     if (root_done) {
       const double tau_r = tau + hs;
       const int a = affect(P, in, out, n, ray, u, tau_r, erg, ncross, max_crossings);

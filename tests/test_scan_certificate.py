@@ -4,7 +4,8 @@ on the host build of the product header (tools/corecheck): for random steps
 condition (RayTracer.jl:254-298) is negative -- not NaN, not zero -- at every grid point the
 kernel would have scanned (interp_points = 50 on the cubic Hermite interpolant,
 RayTracer.jl:358), whenever it returns "positive" it is positive at every point, and
-whenever it returns "NaN" the condition is NaN at every grid point.
+whenever it returns "NaN" the condition is NaN at every grid point -- in the one-sided form
+(b at the end point only: a ray's first step) and the two-sided one (b at both ends).
 Both must fire on a good share of the steps, and "negative" never where |u7| < m_a or where
 the step can reach the conversion surface."""
 import os
@@ -26,8 +27,9 @@ def hermite(u0, f0, u1, f1, h, th):
     return a * u0 + th * u1 + b * ((1.0 - 2.0 * th) * (u1 - u0) + (th - 1.0) * h * f0 + th * h * f1)
 
 
+@pytest.mark.parametrize("two_sided", [False, True])
 @pytest.mark.parametrize("cfg", sorted(CONFIGS))
-def test_certificate_is_sound(cfg, oracle_lib):
+def test_certificate_is_sound(cfg, two_sided, oracle_lib):
     kw = dict(CONFIGS[cfg])
     p = oracle_lib.make_params(**kw)
     mr = oracle_lib.find_conversion_surface(p)
@@ -37,7 +39,7 @@ def test_certificate_is_sound(cfg, oracle_lib):
     U2, tau2 = random_states(400, seed=12, rmin=10.5, rmax=mr, erg=erg)  # inside the surface
     U, tau = np.concatenate([U1, U2], axis=1), np.concatenate([tau1, tau2])
     th_grid = np.arange(1, 50) / 49.0
-    fired = fired_nan = fired_pos = nan_side = 0
+    fired = fired_nan = fired_pos = nan_side = fired_more = 0
     for i in range(U.shape[1]):
         u0, t0 = U[:, i], tau[i]
         f0 = oracle_lib.rhs(p, 1, u0, t0, erg)
@@ -47,7 +49,11 @@ def test_certificate_is_sound(cfg, oracle_lib):
         f1 = oracle_lib.rhs(p, 1, u1, t0 + h, erg)
         if not (np.all(np.isfinite(u1)) and np.all(np.isfinite(f1))):
             continue
-        code = cc.certified_code(p, u0, f0, u1, f1, h, t0)
+        code = cc.certified_code(p, u0, f0, u1, f1, h, t0, two_sided)
+        if two_sided:  # the two-sided form certifies whatever the one-sided one does, alike
+            c1 = cc.certified_code(p, u0, f0, u1, f1, h, t0, False)
+            assert c1 == 0 or c1 == code, (i, c1, code)
+            fired_more += code != 0 and c1 == 0
         if abs(u0[6]) < kw["mass_a"] or abs(u1[6]) < kw["mass_a"]:
             nan_side += 1
             assert code not in (1, 2)  # a step that reaches |u7| < m_a is never certified signed
@@ -67,6 +73,8 @@ def test_certificate_is_sound(cfg, oracle_lib):
     if kw["flat"]:  # in GR, -g^tt > 1 keeps NrmSq > 0 unless u7 drops by ~rs/r
         assert fired_nan >= 20, fired_nan
     assert nan_side > 0
+    if two_sided and kw["flat"]:  # (the random GR steps here are too long to gain)
+        assert fired_more > 0
 
 
 def test_certificate_rejects_the_conversion_surface(oracle_lib):

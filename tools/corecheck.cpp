@@ -75,11 +75,13 @@ void cc_metric_d(double r, double rs, double* out) {
 
 extern "C" {
 // scan_certified_code (art_core.h) for one step (u0, f0) -> (u1, f1) over h from τ
+// (two_sided: with b at the start point too, as the kernel has it after its first step)
 int cc_certified_code(const art_params* p, const double* u0, const double* f0, const double* u1,
-                          const double* f1, double h, double tau) {
+                          const double* f1, double h, double tau, int two_sided) {
   KParams K = make_kparams(*p);
-  double du[7], aux[2];  // b and t at the end point, as the kernel takes them from its last RHS
+  double du[7], aux[2], aux0[2];  // b and t at the end point, as the kernel takes them from its last RHS
   rhs_photon(K, u1, tau + h, 1.0, du, aux);
-  return scan_certified_code(K, u0, f0, u1, f1, h, aux[0], aux[1]);
+  rhs_photon(K, u0, tau, 1.0, du, aux0);
+  return scan_certified_code(K, u0, f0, u1, f1, h, aux[0], aux[1], two_sided ? aux0[0] : NAN);
 }
 }

@@ -126,5 +126,6 @@ def metric_d(r, rs):
     return o
 
 
-def certified_code(p, u0, f0, u1, f1, h, tau):
-    return int(lib().cc_certified_code(C.byref(p), P(u0), P(f0), P(u1), P(f1), C.c_double(h), C.c_double(tau)))
+def certified_code(p, u0, f0, u1, f1, h, tau, two_sided=False):
+    return int(lib().cc_certified_code(C.byref(p), P(u0), P(f0), P(u1), P(f1), C.c_double(h), C.c_double(tau),
+                                       int(two_sided)))
