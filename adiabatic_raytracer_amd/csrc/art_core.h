@@ -416,15 +416,19 @@ __host__ __device__ inline void rhs_photon(const KParams& P, const T* u, const T
   }
 }
 
-// rhs_photon for flat space (g^rr = 1, g^tt = -1, no boundary layer, anisotropic plasma: the
-// headline workload), with the algebra the general form leaves to the hardware done by hand:
-// with a1t = ∂θ a1 = -a2, ∂θ b = -3(a2 cosθ + a1 sinθ), ∂φ b = 3 a1p cosθ, ∂θ β = -6 a1 a2,
-// w = ωp² G (= ½ ωp² ∂Q/∂p), and ∂H/∂t = -ω ∂H/∂φ, the same derivatives as rhs_photon in
-// about 35% fewer operations (equal up to rounding; tests/test_gpu_pointwise.py checks both
-// against the oracle's dual numbers).
+// rhs_photon for GJ plasma without a boundary layer, anisotropic (the headline workload in
+// flat space, configs[3] in Schwarzschild), with the algebra the general form leaves to the
+// hardware done by hand: with a1t = ∂θ a1 = -a2, ∂θ b = -3(a2 cosθ + a1 sinθ),
+// ∂φ b = 3 a1p cosθ, ∂θ β = -6 a1 a2, w = ωp² G (= ½ ωp² ∂Q/∂p) and ∂H/∂t = -ω ∂H/∂φ, the
+// same derivatives as rhs_photon in about a third fewer operations (equal up to rounding;
+// tests/test_gpu_pointwise.py and tests/test_corecheck.py check it against the oracle's dual
+// numbers). In flat space (rs_eff == 0, compile-time in the GEOM_FLAT kernel) the metric
+// terms drop out; in Schwarzschild
+//   H_r += ½ ∂g^tt E² + ½ ∂g^rr k_r² - ½ ωp² ∂g^rr Q/g^rr - w ∂g^rr/√g^rr k_r a1.
 template <class T>
-__host__ __device__ inline void rhs_photon_flat(const KParams& P, const T* u, const T& tau, double erg, T* du,
-                                                T* aux = nullptr) {
+__host__ __device__ inline void rhs_photon_gj(const KParams& P, const T* u, const T& tau, double erg, T* du,
+                                              T* aux = nullptr) {
+  const bool flat = P.rs_eff == 0.0;
   const T t = fexp(tau);
   const T r = u[0];
   const T E = -u[6];
@@ -443,6 +447,18 @@ __host__ __device__ inline void rhs_photon_flat(const KParams& P, const T* u, co
   const T ierg = RX1 * E;
   const T inv_rs = R * X2;
   const T ir = inv_rs * ast, iast = inv_rs * rc;
+  // Schwarzschild: g^rr at the clamped radius, its derivatives, and g^rr at the raw radius for
+  // the prefactor (:82), which differs only inside the star
+  T gtt = -1.0, grr = 1.0, dgtt = 0.0, dgrr = 0.0, grr_u = 1.0, sq = 1.0;
+  if (!flat) {
+    metric_tr_d(rc, P.rs_eff, gtt, grr, dgtt, dgrr);
+    grr_u = grr;
+    if (r < P.rNS) {
+      T gtt_u;
+      metric_tr(r, P.rs_eff, gtt_u, grr_u);
+    }
+    sq = msqrt(grr);
+  }
   // rotating dipole (dipole_ang)
   const T cmst = P.cm * st, smct = P.sm * ct, smst = P.sm * st;
   const T a1 = P.cm * ct + smst * cp;
@@ -457,31 +473,36 @@ __host__ __device__ inline void rhs_photon_flat(const KParams& P, const T* u, co
   const T cBs = cB * msign(b);
   const T iast2 = iast * iast;
   const T kpa3 = kp * a3;
+  const T krs = flat ? kr : sq * kr;  // √g^rr k_r
   const T pa = kt * a2 + kpa3 * iast;
-  const T p = 2.0 * kr * a1 + ir * pa;  // k∥ √β r |sinθ| / (r |sinθ|)
-  const T G = p * ibeta * (iE * iE);
+  const T p = 2.0 * krs * a1 + ir * pa;  // k∥ √β r |sinθ| / (r |sinθ|)
+  const T Gp = p * ibeta * (iE * iE);   // G / g^rr
+  const T G = flat ? Gp : grr * Gp;
   const T Q = G * p;
   const T w = wp2 * G;
   const T omQ = 1.0 - Q;
-  const T p_t = -2.0 * kr * a2 + ir * (kt * a1 - kpa3 * sgn_st * ct * iast2);
-  const T p_p = 2.0 * kr * a1p + ir * (kt * a2p + kp * a3p * iast);
+  const T p_t = -2.0 * krs * a2 + ir * (kt * a1 - kpa3 * sgn_st * ct * iast2);
+  const T p_p = 2.0 * krs * a1p + ir * (kt * a2p + kp * a3p * iast);
   const T Qib = wp2 * Q * ibeta;
   const T beta_p = 8.0 * a1 * a1p + 2.0 * (a2 * a2p + a3 * a3p);
   const T kp2 = kp * kp;
-  const T H_r = w * ir2 * pa - ir3 * (kt * kt + iast2 * kp2) - 1.5 * wp2 * ir * omQ;
+  T H_r = w * ir2 * pa - ir3 * (kt * kt + iast2 * kp2) - 1.5 * wp2 * ir * omQ;
+  if (!flat)
+    H_r += 0.5 * (dgtt * (E * E) + dgrr * (kr * kr) - wp2 * dgrr * Gp * p) - w * dgrr * frcp(sq) * kr * a1;
   const T H_t = -ct * ir2 * iast2 * iast * sgn_st * kp2 - 1.5 * cBs * (a2 * ct + a1 * st) * omQ - w * p_t -
                 3.0 * Qib * a1 * a2;
   const T H_p = 1.5 * cBs * a1p * ct * omQ - w * p_p + 0.5 * Qib * beta_p;
   // rows 1..6 vanish for r <= 1.01 rNS (:86)
-  const T facx = (r <= P.rNS101) ? T(0.0) : C_KM * t * iE;
+  const T tg = flat ? t : t * grr_u;
+  const T facx = (r <= P.rNS101) ? T(0.0) : C_KM * tg * iE;
   const T fx = -facx * ierg;
-  du[0] = (kr - 2.0 * w * a1) * facx;
+  du[0] = flat ? (kr - 2.0 * w * a1) * facx : (grr * kr - 2.0 * w * (sq * a1)) * facx;
   du[1] = (ir2 * kt - w * ir * a2) * facx;
   du[2] = (ir2 * iast2 * kp - w * ir * a3 * iast) * facx;
   du[3] = H_r * fx;
   du[4] = H_t * fx;
   du[5] = H_p * fx;
-  du[6] = -P.omega * H_p * t * iE;  // ∂H/∂t = -ω ∂H/∂φ
+  du[6] = -P.omega * H_p * tg * iE;  // ∂H/∂t = -ω ∂H/∂φ
   if (aux) {
     aux[0] = b;
     aux[1] = t;
@@ -516,7 +537,7 @@ __host__ __device__ inline void rhs_axion(const KParams& P, const T* u, const T&
 template <class T>
 __host__ __device__ inline void rhs(const KParams& P, bool photon, const T* u, const T& tau, double erg, T* du) {
   if (!photon) rhs_axion(P, u, tau, erg, du);
-  else if (P.rs_eff == 0.0 && !(P.bndry_lyr > 0.0) && !P.isotropic) rhs_photon_flat(P, u, tau, erg, du);
+  else if (!(P.bndry_lyr > 0.0) && !P.isotropic) rhs_photon_gj(P, u, tau, erg, du);
   else rhs_photon(P, u, tau, erg, du);
 }
 
@@ -739,6 +760,44 @@ __host__ __device__ inline int scan_certified_code(const KParams& P, const doubl
     return 1;
   return 0;
 }
+
+#ifdef ART_COUNT_SUB
+// dev: why a step was not certified. Bit 0: the two-sided bmin <= 0; bit 1: the positive
+// test's ratio lhs/rhs in (0.5, 1]; bit 2: the negative test's ratio in (0.5, 1]; bit 3: u7
+// too close to the shell (elo² <= cert_e2); bit 4: positive ratio <= 0.5 with bmin > 0.
+__host__ __device__ inline int scan_cert_diag(const KParams& P, const double* u0, const double* f0,
+                                              const double* u1, const double* f1, double h, double b1, double t1,
+                                              double b0) {
+  const Hull r = bernstein_hull(u0[0], f0[0], u1[0], f1[0], h);
+  const Hull e = bernstein_hull(u0[6], f0[6], u1[6], f1[6], h);
+  const double elo = e.lo > 0.0 ? e.lo : (e.hi < 0.0 ? -e.hi : 0.0);
+  const double ehi = fmax(fabs(e.lo), fabs(e.hi));
+  int d = (elo * elo > P.cert_e2) ? 0 : 8;
+  const Hull th = bernstein_hull(u0[1], f0[1], u1[1], f1[1], h);
+  const Hull ph = bernstein_hull(u0[2], f0[2], u1[2], f1[2], h);
+  const double dth = fmax(th.hi - u1[1], u1[1] - th.lo);
+  const double dps = fmax(ph.hi - u1[2], u1[2] - ph.lo) + fabs(P.omega) * t1 * h * (1.0 + 1e-12);
+  const double db = 3.0 * dth + 1.5 * fabs(P.sm) * dps + 1e-12;
+  double bmax = fmin(2.0, fabs(b1) + db), bmin = fabs(b1) - db;
+  if (b0 == b0) {
+    const double h3 = h * (1.0 / 3.0);
+    const double tvt = fabs(h3 * f0[1]) + fabs((u1[1] - h3 * f1[1]) - (u0[1] + h3 * f0[1])) + fabs(h3 * f1[1]);
+    const double tvp = fabs(h3 * f0[2]) + fabs((u1[2] - h3 * f1[2]) - (u0[2] + h3 * f0[2])) + fabs(h3 * f1[2]);
+    const double ell = (3.0 * tvt + 1.5 * fabs(P.sm) * (tvp + fabs(P.omega) * t1 * h)) * (1.0 + 1e-12) + 1e-12;
+    const double lo = 0.5 * (b0 + b1 - ell), hi = 0.5 * (b0 + b1 + ell);
+    bmax = fmin(bmax, fmax(fabs(lo), fabs(hi)));
+    bmin = fmax(bmin, lo > 0.0 ? lo : (hi < 0.0 ? -hi : 0.0));
+  }
+  if (!(bmin > 0.0)) d |= 1;
+  const double neg = P.wp2n * bmax * P.cert_fac / (P.mass_a2 * (r.lo * r.lo * r.lo));
+  if (neg >= 1.0 && neg < 2.0) d |= 4;
+  const double grr_lo = P.rs_eff == 0.0 ? 1.0 : 1.0 - P.rs_eff / r.lo;
+  const double pos = P.wp2n * bmin * grr_lo / (ehi * ehi * P.cert_fac * (r.hi * r.hi * r.hi));
+  if (pos > 0.5 && pos <= 1.0) d |= 2;
+  if (bmin > 0.0 && pos <= 0.5) d |= 16;
+  return d;
+}
+#endif
 
 template <class T>
 __host__ __device__ inline T condition(const KParams& P, const T* u, const T& tau) {

@@ -420,9 +420,13 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
   int save_k = 1;  // SAVE: the next interior saveat index
   bool exhausted = false;
   unsigned s_att = 0, s_acc = 0, s_root = 0, s_scan = 0, s_interp = 0, s_rays = 0, s_cert = 0;
+#ifdef ART_SLOT_TIMING
+#define ART_SECTION_TIMING
+#endif
 #ifdef ART_SECTION_TIMING
   // dev build: s_memtime cycles per main-loop section, summed over the wave's iterations
-  unsigned long long t_sec[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  // (ART_SLOT_TIMING: also the stage slots' parts, 8 combination, 9 RHS, 10 the rest)
+  unsigned long long t_sec[11] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   unsigned long long t_last = __builtin_amdgcn_s_memtime();
 #define ART_TMARK(k)                                                  \
   {                                                                   \
@@ -433,8 +437,24 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
 #else
 #define ART_TMARK(k)
 #endif
+#ifdef ART_SLOT_TIMING
+#define ART_SMARK(k) ART_TMARK(k)
+#else
+#define ART_SMARK(k)
+#endif
 #ifdef ART_COUNT_SUB
-  unsigned s_sub[4] = {0, 0, 0, 0};  // dev: uncertified steps, uniform 7-point sub-intervals, uniform +/- steps
+  // dev: uncertified steps; all-positive ones; of those bmin <= 0; of those a positive-test near
+  // miss; all-negative ones; ones with a sign change; first steps of a ray
+  unsigned s_sub[7] = {0, 0, 0, 0, 0, 0, 0};
+#endif
+#ifdef ART_COUNT_PASSES
+  // dev: wave-level counts (lane 0): main iterations, grid passes, iterations with a grid pass,
+  // cooperative passes, iterations that refill, iterations with a code walk, fallback iterations
+  unsigned s_pc[7] = {0, 0, 0, 0, 0, 0, 0};
+#define ART_PC(k) \
+  if (lane == 0) s_pc[k] += 1;
+#else
+#define ART_PC(k)
 #endif
 #ifdef ART_COUNT_LOOPS
   unsigned s_lane_it = 0, s_main_it = 0;  // dev counters: wave iterations of the per-lane and main loops
@@ -447,6 +467,9 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
     // ---- refill idle lanes from the wave's chunk (one atomicAdd per 64 rays) ----
     if (!exhausted) {
       unsigned long long need = __ballot(mode == M_IDLE);
+#ifdef ART_COUNT_PASSES
+      if (need != 0ull) ART_PC(4)
+#endif
       while (need != 0ull) {
         if (wnext >= wend) {
           unsigned long long base = 0;
@@ -489,6 +512,7 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
       }
     }
     if (__ballot(mode != M_IDLE) == 0ull) break;  // every lane idle and the queue drained
+    ART_PC(0)
     ART_TMARK(0)  // refill
 #ifdef ART_COUNT_LOOPS
     if (lane == 0) s_main_it += 1;
@@ -531,12 +555,14 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
 #pragma unroll
       for (int i = 0; i < 7; ++i) y[i] = u[i] + hs * acc[i];
       const double ty = tau + R.ct * hs;
+      ART_SMARK(8)
       // Every lane evaluates the photon RHS -- idle lanes (a draining wave) on stale state,
       // whose results nothing reads -- so the slot has no divergent control flow. Axion
       // segments (the tree driver's batches) take a wave-uniform detour and a select.
       double aux[2];
-      if constexpr (GEOM == GEOM_FLAT) rhs_photon_flat(P, y, ty, erg, kk, aux);
+      if constexpr (GEOM != GEOM_ANY) rhs_photon_gj(P, y, ty, erg, kk, aux);
       else rhs_photon(P, y, ty, erg, kk, aux);
+      ART_SMARK(9)
       if (s == NSLOT - 1) {  // the end point's b and t for the scan certificate (lastv and codes are free)
         lastv[threadIdx.x] = aux[0];
         lastt[threadIdx.x] = aux[1];
@@ -556,6 +582,7 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
 #pragma unroll
         for (int i = 0; i < 7; ++i) L[(sl * 7 + i) * BLOCK] = kk[i];
       }
+      ART_SMARK(10)
     }
     ART_TMARK(1)  // step size and stage slots
     // y = u_{n+1}, kk = f(u_{n+1}) for stepping lanes
@@ -644,6 +671,9 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
     const int ccode =
         !scan ? 0 : (cbs ? scan_certified_code(P, u, f, y, kk, hs, bend, lastt[threadIdx.x], bstart) : 3);
     const bool cert = ccode != 0;
+#ifdef ART_COUNT_SUB
+    const int cdiag = (scan && !cert) ? scan_cert_diag(P, u, f, y, kk, hs, bend, lastt[threadIdx.x], bstart) : 0;
+#endif
     s_cert += cert ? 1u : 0u;
     // every lane parks (u, f, y, kk, h, τ) in its LDS slots (free after the error estimate):
     // the scan reads the interpolants from there, and the registers stay free until the
@@ -664,6 +694,7 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
     const unsigned long long rmask = __ballot(mode == M_ROOT);
     ART_TMARK(2)  // error norm, controller, certificate and parking
     if ((smask | rmask) != 0ull) {
+      ART_PC(2)
       const int ns = __popcll(smask), nr = __popcll(rmask);
       if (grid) {
         srcl[wbase + __popcll(smask & ((1ull << lane) - 1ull))] = lane;
@@ -679,6 +710,7 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
       int c = ns ? lane % ns : 0, j = ns ? lane / ns + 1 : 0;
 #pragma unroll 1
       for (int w0 = 0; w0 < total; w0 += 64) {
+        ART_PC(1)
         const int t = w0 + lane;
         if (t < total) {  // one evaluation site for both kinds of item (no divergent second copy)
           const bool gi = t < tg;
@@ -724,25 +756,26 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
       for (int w = 0; w < SCAN_WORDS; ++w)
         cw[w] = cert ? 0x55555555u * (unsigned)ccode : codes[w * BLOCK + threadIdx.x];
 #ifdef ART_COUNT_SUB
-      // dev: how much of the uncertified steps' grid a sub-interval certificate could skip:
-      // sub-intervals of 7 grid points whose codes are one nonzero sign / all NaN
+      // dev: what the uncertified steps are (see s_sub)
       if (!cert) {
         s_sub[0] += 1;
-        bool all = true;
-        const unsigned first = cw[0] & 3u;
-        for (int k = 0; k < 7; ++k) {
-          const int j0 = 7 * k;
-          const unsigned c0 = (cw[j0 >> 4] >> (2 * (j0 & 15))) & 3u;
-          bool uni = c0 != 0u;
-          for (int jj = 1; jj < 7; ++jj) {
-            const int q = j0 + jj;
-            uni = uni && (((cw[q >> 4] >> (2 * (q & 15))) & 3u) == c0);
-          }
-          s_sub[1] += uni ? 1u : 0u;
-          all = all && uni && c0 == first;
+        bool allp = true, alln = true, chg = false;
+        int ls = 0;
+        for (int q = 0; q < nper; ++q) {
+          const unsigned c0 = (cw[q >> 4] >> (2 * (q & 15))) & 3u;
+          allp = allp && c0 == 1u;
+          alln = alln && c0 == 2u;
+          const int si = c0 == 1u ? 1 : (c0 == 2u ? -1 : 0);
+          if (c0 == 3u) ls = 0;
+          if (si != 0 && ls != 0 && si != ls) chg = true;
+          if (si != 0) ls = si;
         }
-        s_sub[2] += (all && first == 1u) ? 1u : 0u;  // uniform positive steps
-        s_sub[3] += (all && first == 2u) ? 1u : 0u;  // uniform negative steps
+        s_sub[1] += allp ? 1u : 0u;
+        s_sub[2] += (allp && (cdiag & 1)) ? 1u : 0u;
+        s_sub[3] += (allp && (cdiag & 2)) ? 1u : 0u;
+        s_sub[4] += alln ? 1u : 0u;
+        s_sub[5] += chg ? 1u : 0u;
+        s_sub[6] += (n_acc == 1) ? 1u : 0u;
       }
 #endif
       // fast path: every grid point has the previous sign (or the previous sign is unknown
@@ -868,6 +901,9 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
       polish(lastv[threadIdx.x]);
     }
     ART_TMARK(4)  // sign-code fast paths
+#ifdef ART_COUNT_PASSES
+    if (__ballot(ph == 2) != 0ull) ART_PC(5)
+#endif
     if (ph == 2) walk();
     ART_TMARK(5)  // code walk
     // (c) One cooperative pass evaluates the pending condition values of the whole wave at
@@ -881,6 +917,7 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
       const unsigned long long b1 = __ballot(nq >= 1), b2 = __ballot(nq == 2);
       const int total = __popcll(b1) + __popcll(b2);
       if (total > 0 && total <= 64) {
+        ART_PC(3)
         const int off = __popcll(b1 & lt) + __popcll(b2 & lt);
         wave_lds_sync();  // the walk's lastv reads are done
         if (nq >= 1) {
@@ -925,6 +962,9 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
     while (ph != 0) {
 #ifdef ART_COUNT_LOOPS
       if (lane == __ffsll((long long)__ballot(1)) - 1) s_lane_it += 1;
+#endif
+#ifdef ART_COUNT_PASSES
+      if (lane == __ffsll((long long)__ballot(1)) - 1) s_pc[6] += 1;
 #endif
       if (ph == 2) {
         walk();
@@ -1055,16 +1095,25 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
   }
 
   // wave-reduce the statistics and add them once per wave
-#if defined(ART_SECTION_TIMING)
+#if defined(ART_SLOT_TIMING)
+  if (lane == 0) {  // [refill etc, combination, RHS, slot rest, norm..park, grid, fast+walk+coop, fallback]
+    const unsigned long long v[8] = {t_sec[0], t_sec[8] + t_sec[1], t_sec[9], t_sec[10], t_sec[2], t_sec[3],
+                                     t_sec[4] + t_sec[5] + t_sec[6], t_sec[7]};
+#pragma unroll
+    for (int k = 0; k < 8; ++k) atomicAdd(&stats[k], v[k]);
+  }
+#elif defined(ART_SECTION_TIMING)
   if (lane == 0) {
 #pragma unroll
     for (int k = 0; k < 8; ++k) atomicAdd(&stats[k], t_sec[k]);
   }
 #else
-#if defined(ART_COUNT_LOOPS)
+#if defined(ART_COUNT_PASSES)
+  const unsigned v[7] = {s_pc[0], s_pc[1], s_pc[2], s_pc[3], s_pc[4], s_pc[5], s_pc[6]};
+#elif defined(ART_COUNT_LOOPS)
   const unsigned v[7] = {s_main_it, s_lane_it, s_ph[1], s_ph[3], s_ph[5], s_ph[6], s_ph[7]};
 #elif defined(ART_COUNT_SUB)
-  const unsigned v[7] = {s_att, s_acc, s_sub[0], s_sub[1], s_sub[2], s_sub[3], s_cert};
+  const unsigned v[7] = {s_sub[0], s_sub[1], s_sub[2], s_sub[3], s_sub[4], s_sub[5], s_sub[6]};
 #else
   const unsigned v[7] = {s_att, s_acc, s_root, s_scan, s_interp, s_rays, s_cert};
 #endif

@@ -67,8 +67,8 @@ def run_point(kw: dict, rays: int, seed: int = 1769, nbins: int = 50, device: in
 def run_points(kws: list[dict], rays: int, seed: int = 1769, nbins: int = 50, device: int = 0,
                streams: int = 16) -> tuple[list[dict], dict]:
     """Several grid points on one GPU, `streams` of them in flight: every point's forward
-    roots are sampled first, then the points are propagated on `streams` HIP streams round
-    robin -- each launch has its own device scratch (include/art.h), so a point's drain tail
+    roots are sampled first, then the points are propagated on `streams` HIP streams, each
+    next point on the first stream to go idle (dispatch) -- each launch has its own device scratch (include/art.h), so a point's drain tail
     (its last long rays on a few CUs; 130-900 ms per 1e6-ray point when run alone) overlaps
     the other points' bulk -- and each point's flux is binned on its stream. Streams only run
     concurrently up to the process's hardware queues: main() raises GPU_MAX_HW_QUEUES to 16
@@ -85,53 +85,82 @@ def run_points(kws: list[dict], rays: int, seed: int = 1769, nbins: int = 50, de
     for s_ in ss[1:]:
         s_.wait_stream(main)
     t0 = time.perf_counter()
-    engs, inps, recs = [], [], []
+    engs, recs = [], []
     for kw in kws:
         p = A.Params(**kw)
-        eng = Engine(p, device=device)
-        max_r = p.max_r()
-        rec = dict(kw, rays=rays, max_r_km=max_r)
+        rec = dict(kw, rays=rays, max_r_km=p.max_r())
         recs.append(rec)
-        if max_r < p.rNS:  # no conversion surface outside the star (MainRunner.jl:387-396)
+        if rec["max_r_km"] < p.rNS:  # no conversion surface outside the star (MainRunner.jl:387-396)
             rec["skipped"] = "maxR < rNS"
             engs.append(None)
-            inps.append(None)
-            continue
-        engs.append(eng)
-        with torch.cuda.stream(ss[len(inps) % len(ss)]):  # the samplers' tails overlap too
-            inps.append(eng.forward_roots(rays, seed=seed))
+        else:
+            engs.append(Engine(p, device=device))
+    live = [i for i, e in enumerate(engs) if e is not None]
+    inps, outs, hists = {}, {}, {}
+
+    def sample(i):  # the samplers' tails overlap too
+        inps[i] = engs[i].forward_roots(rays, seed=seed)
+
+    dispatch(live, sample, ss)
     torch.cuda.synchronize()
     t_sample = time.perf_counter() - t0
-    outs, hists = [None] * len(kws), [None] * len(kws)
+
+    def prop(i):
+        outs[i] = engs[i].propagate(inps[i], max_crossings=-1)
+        hists[i] = engs[i].flux_histogram(outs[i], inps[i]["species"], None, nbins)
+
     t1 = time.perf_counter()
-    k = 0
-    for i, eng in enumerate(engs):
-        if eng is None:
-            continue
-        with torch.cuda.stream(ss[i % len(ss)]):
-            outs[i] = eng.propagate(inps[i], max_crossings=-1)
-            hists[i] = eng.flux_histogram(outs[i], inps[i]["species"], None, nbins)
-        k += 1
+    order = dispatch(live, prop, ss)
     torch.cuda.synchronize()
     wall = time.perf_counter() - t1
+    k = len(order)
     ms = (C.c_double * max(1, k))()
     got = A._lib.load().art_recent_kernel_ms(k, ms)
-    kms = list(ms)[:max(0, got)]
-    acc_total, j = 0, 0
-    for i, eng in enumerate(engs):
-        if eng is None:
-            continue
+    kms = dict(zip(order, list(ms)[:max(0, got)]))  # the ring holds launch order
+    acc_total = 0
+    for i in live:
         o = outs[i]
         acc = int(o["n_accept"].sum().item())
         att = acc + int(o["n_reject"].sum().item())
         acc_total += acc
-        recs[i].update(kernel_ms=kms[j] if j < len(kms) else None, accepted=acc, attempts=att,
+        recs[i].update(kernel_ms=kms.get(i), accepted=acc, attempts=att,
                        status_counts=torch.bincount(o["status"].long(), minlength=5).tolist(),
                        flux_photon=hists[i][nbins:].tolist())
-        j += 1
     summary = {"points": k, "streams": len(ss), "sample_s": t_sample, "propagate_wall_s": wall,
                "accepted": acc_total, "kernel_ray_steps_per_s": acc_total / wall if wall > 0 else None}
     return recs, summary
+
+
+def dispatch(items, launch, streams, poll_s=2e-4):
+    """Runs launch(item) on the first of `streams` that has gone idle, in item order: one
+    item per stream up front, then each next item on whichever stream finishes first (an
+    event per launch, polled from the host). A round-robin assignment would queue item
+    k + len(streams) behind item k even when item k holds a long drain tail (a 1e6-ray
+    scan point's last ray can take ~0.8 s on its own) while the other streams sit idle.
+    Returns the items in launch order."""
+    import torch
+    order, busy = [], {}
+    todo = list(items)
+    free = list(range(len(streams)))
+    while todo or busy:
+        while todo and free:
+            j = free.pop(0)
+            it = todo.pop(0)
+            with torch.cuda.stream(streams[j]):
+                launch(it)
+                ev = torch.cuda.Event()
+                ev.record()
+            busy[j] = ev
+            order.append(it)
+        if not todo:
+            break
+        done = [j for j, ev in busy.items() if ev.query()]
+        if not done:
+            time.sleep(poll_s)
+        for j in done:
+            del busy[j]
+            free.append(j)
+    return order
 
 
 def run_scan(rays: int, n_points: int | None = None, seed: int = 1769, run=None, streams: int = 16):

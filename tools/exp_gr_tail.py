@@ -2,7 +2,8 @@
 attempts in the 1e6-ray GR batch, then integrates the longest one as a batch of one ray (one
 lane of one wave: the latency floor of that configuration) and prints µs per attempt; with
 the ART_SECTION_TIMING build (ART_LIB=...) also the lone wave's section split.
-Usage: [ART_LIB=...] exp_gr_tail.py [n] [ray]"""
+Usage: [ART_LIB=...] [TAIL_KW='{"mass_a": ...}'] exp_gr_tail.py [n] [ray]  (TAIL_KW: another
+Params keyword set, e.g. a scan point)"""
 import json
 import os
 import sys
@@ -12,8 +13,9 @@ import adiabatic_raytracer_amd as A  # noqa: E402
 from adiabatic_raytracer_amd import Engine  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 1_000_000
-eng = Engine(A.Params(theta_m=0.0, mass_a=1e-6, flat=False))
-sect = "sect" in os.environ.get("ART_LIB", "")
+KW = json.loads(os.environ.get("TAIL_KW", '{"theta_m": 0.0, "mass_a": 1e-6, "flat": false}'))
+eng = Engine(A.Params(**KW))
+sect = any(k in os.environ.get("ART_LIB", "") for k in ("sect", "slot"))
 if len(sys.argv) > 2:
     ray = int(sys.argv[2])
 else:
@@ -35,6 +37,9 @@ line = {"ray": ray, "kernel_ms": ms, "attempts": a, "us_per_attempt": ms * 1e3 /
 if sect:
     NAMES = ["refill etc", "stage slots", "norm/controller/cert/park", "grid pass", "fast paths", "walk", "coop pass",
              "fallback"]
+    if "slot" in os.environ.get("ART_LIB", ""):
+        NAMES = ["refill etc", "slot combination", "slot RHS", "slot rest", "norm/controller/cert/park", "grid pass",
+                 "fast+walk+coop", "fallback"]
     v = list(st.values())[:8]
     v[6] -= 2
     tot = sum(v)

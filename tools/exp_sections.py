@@ -11,6 +11,9 @@ from adiabatic_raytracer_amd import Engine  # noqa: E402
 
 NAMES = ["refill + reload, events, finish, stores", "step size + stage slots", "error norm, controller, certificate, parking",
          "grid pass", "sign-code fast paths", "code walk", "cooperative pass", "per-lane fallback"]
+if "slot" in os.environ.get("ART_LIB", ""):
+    NAMES = ["refill etc", "slot combination", "slot RHS", "slot rest", "norm/controller/cert/park", "grid pass",
+             "fast+walk+coop", "fallback"]
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 10_000_000
 eng = Engine(A.Params(theta_m=0.2, mass_a=1e-5, flat=True))
 inp = eng.forward_roots(n, seed=1769)
