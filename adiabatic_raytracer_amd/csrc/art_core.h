@@ -57,6 +57,37 @@ __host__ __device__ inline void msincos(double x, double& s, double& c) {
   s = (q & 2) ? -ss : ss;
   c = ((q + 1) & 2) ? -cc : cc;
 }
+// max(|a|, |b|), min(a, b) and max(a, b) as one instruction each. LLVM's fmax/fmin in IEEE
+// mode first quiet signaling NaNs with a v_max x, x per operand it cannot prove canonical
+// (anything loaded or passed in); the integrator never holds signaling NaNs, and a quiet NaN
+// operand gives the other operand either way.
+__host__ __device__ inline double fmax_abs(double a, double b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  double r;
+  asm("v_max_f64 %0, |%1|, |%2|" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+#else
+  return fmax(fabs(a), fabs(b));
+#endif
+}
+__host__ __device__ inline double fmin_q(double a, double b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  double r;
+  asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+#else
+  return fmin(a, b);
+#endif
+}
+__host__ __device__ inline double fmax_q(double a, double b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  double r;
+  asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+#else
+  return fmax(a, b);
+#endif
+}
 // 1/x from the hardware reciprocal and two Newton steps (~0.5 ulp; 1/0 and 1/inf give NaN,
 // which the integrator reports as a non-finite state either way). The host build, which the
 // CPU tests compare with the oracle, divides.
@@ -705,7 +736,7 @@ __host__ __device__ inline Hull bernstein_hull(double a, double fa, double b, do
   const double c1 = a + h3 * fa, c2 = b - h3 * fb;
   const double s = 1e-12 * (fabs(a) + fabs(b) + fabs(h * fa) + fabs(h * fb));
   if (!(fabs(c1) + fabs(c2) + s < __builtin_inf())) return {NAN, NAN};  // non-finite: no bound
-  return {fmin(fmin(a, b), fmin(c1, c2)) - s, fmax(fmax(a, b), fmax(c1, c2)) + s};
+  return {fmin_q(fmin_q(a, b), fmin_q(c1, c2)) - s, fmax_q(fmax_q(a, b), fmax_q(c1, c2)) + s};
 }
 
 // Returns the certified sign code of every grid point of the step: 2 (negative, above), 1

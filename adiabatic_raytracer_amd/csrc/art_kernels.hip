@@ -341,6 +341,9 @@ enum LaneMode { M_IDLE = 0, M_STEP = 2, M_ROOT = 3 };
 constexpr int BLOCK = ART_BLOCK;
 constexpr int SCAN_WORDS = 4;  // 2-bit codes for up to 64 grid points (interp_points <= 65)
 // Waves per SIMD the integrator is register-budgeted for (1: 512 VGPR+AGPR, 2: 256).
+#ifndef ART_PRIO_ITERS
+#define ART_PRIO_ITERS 1024
+#endif
 #ifndef ART_WAVES_PER_SIMD
 #define ART_WAVES_PER_SIMD 2
 #endif
@@ -512,6 +515,12 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
       }
     }
     if (__ballot(mode != M_IDLE) == 0ull) break;  // every lane idle and the queue drained
+    // A wave holding an outlier ray (ART_PRIO_ITERS attempts and more: ~20x the mean) asks the
+    // SIMD's arbiter for issue priority. The one ray that sets a launch's (or a scan point's)
+    // drain time then runs at close to its lone-wave speed while the bulk of the batch still
+    // shares its SIMD; the other waves fill the issue slots it leaves.
+    if (__ballot(iter >= ART_PRIO_ITERS) != 0ull) __builtin_amdgcn_s_setprio(2);
+    else __builtin_amdgcn_s_setprio(0);
     ART_PC(0)
     ART_TMARK(0)  // refill
 #ifdef ART_COUNT_LOOPS
@@ -599,7 +608,7 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
 #pragma unroll
           for (int q = 1; q < LDS_SLOTS; ++q) e += T.e_L[q] * L[(q * 7 + i) * BLOCK];
           e *= hs;
-          const double q = e * frcp(P.abstol + fmax(fabs(u[i]), fabs(y[i])) * P.reltol);
+          const double q = e * frcp(P.abstol + fmax_abs(u[i], y[i]) * P.reltol);
           acc += q * q;
         }
         EEst2 = acc * (1.0 / 7.0);
