@@ -701,6 +701,9 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
     // lanes polishing a crossing need the condition at the end of their re-step (th = 1 of the
     // parked step): those items ride in the same pass, after the grid items
     const unsigned long long rmask = __ballot(mode == M_ROOT);
+    const int ns_g = __popcll(smask), crank = __popcll(smask & ((1ull << lane) - 1ull));
+    // N and D of the items this lane evaluates in the first two passes (see (c0) below)
+    double gN0 = 0.0, gD0 = 1.0, gN1 = 0.0, gD1 = 1.0;
     ART_TMARK(2)  // error norm, controller, certificate and parking
     if ((smask | rmask) != 0ull) {
       ART_PC(2)
@@ -726,6 +729,13 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
           const int src = srcl[wbase + (gi ? c : ns + (t - tg))];
           double N, D;
           scan_nd_lds(P, lds + wbase + src, BLOCK, gi ? thgrid[j] : 1.0, N, D);
+          if (w0 == 0) {
+            gN0 = N;
+            gD0 = D;
+          } else if (w0 == 64) {
+            gN1 = N;
+            gD1 = D;
+          }
           if (!gi || j == nper) {  // a root item's value; the end value opens the next step's brackets
             const double cv = 0.5 * N / D;  // = scan_point_lds, bit for bit
             lastv[wbase + src] = cv;
@@ -915,6 +925,37 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
 #endif
     if (ph == 2) walk();
     ART_TMARK(5)  // code walk
+    // (c0) The values a bracket (ph 5: at the change point and, when unknown, at the last
+    //      nonzero point before it) or the next step's bracket start (ph 7) needs are grid
+    //      points of this step: item (j - 1) ns + c of the grid pass (c: this lane's rank among
+    //      the sources), evaluated by lane w & 63 in pass w >> 6, whose N and D from the first
+    //      two passes are still in that lane's registers. ½ N / D there is scan_point_lds's
+    //      value bit for bit, so no second evaluation is needed. (The step's start point,
+    //      last_j = 0, and later passes go to the cooperative pass.)
+    {
+      const bool want = grid && (ph == 5 || ph == 7);
+      const int ja = (ph == 5) ? ip : last_j;
+      const int wa = (want && ja >= 1) ? (ja - 1) * ns_g + crank : (want ? 1 << 20 : 0);
+      const bool needb = want && ph == 5 && !lc_ok;
+      const int wb = needb ? (last_j >= 1 ? (last_j - 1) * ns_g + crank : 1 << 20) : 0;
+      if (__ballot(want) != 0ull) {
+        const int la = wa & 63, lb = wb & 63;
+        const double nA0 = __shfl(gN0, la), dA0 = __shfl(gD0, la), nA1 = __shfl(gN1, la), dA1 = __shfl(gD1, la);
+        const double nB0 = __shfl(gN0, lb), dB0 = __shfl(gD0, lb), nB1 = __shfl(gN1, lb), dB1 = __shfl(gD1, lb);
+        if (want && wa < 128 && wb < 128) {
+          const double va = 0.5 * ((wa >> 6) ? nA1 : nA0) / ((wa >> 6) ? dA1 : dA0);
+          if (ph == 7) {
+            last_c = va;
+            lc_ok = true;
+            ph = 0;
+          } else {
+            i_cg = va;
+            if (needb) last_c = 0.5 * ((wb >> 6) ? nB1 : nB0) / ((wb >> 6) ? dB1 : dB0);
+            open_bracket();
+          }
+        }
+      }
+    }
     // (c) One cooperative pass evaluates the pending condition values of the whole wave at
     //     once: the re-stepped end of polishing lanes (ph 1, th = 1 of their parked step), the
     //     change point of a bracket (ph 5) and its start when unknown, and the step's last

@@ -22,6 +22,7 @@ inline OC operator-(OC a, OC b) { ++OC::n; return OC(a.v - b.v); }
 inline OC operator*(OC a, OC b) { ++OC::n; return OC(a.v * b.v); }
 inline OC operator/(OC a, OC b) { ++OC::n; return OC(a.v / b.v); }
 inline OC operator-(OC a) { return OC(-a.v); }
+inline OC& operator+=(OC& a, OC b) { return a = a + b; }
 inline OC operator+(OC a, double b) { return a + OC(b); }
 inline OC operator+(double a, OC b) { return OC(a) + b; }
 inline OC operator-(OC a, double b) { return a - OC(b); }
@@ -67,7 +68,9 @@ static void emit(bool flat, bool last) {
   // a typical exterior photon state (r > 1.01 rNS: all seven components computed)
   OC u[7] = {OC(20.0), OC(1.1), OC(0.3), OC(0.8), OC(5.0), OC(3.0), OC(-1.00000027e-5)};
   OC du[7], tau(-12.0);
-  const long long f_rhs = count([&] { rhs_photon(K, u, tau, 1.00000027e-5, du); });
+  // the photon RHS the kernels run for this parameter set (rhs dispatches: GJ plasma without a
+  // boundary layer -> rhs_photon_gj)
+  const long long f_rhs = count([&] { rhs(K, true, u, tau, 1.00000027e-5, du); });
   const long long f_rhs_ax = count([&] { rhs_axion(K, u, tau, 1.00000027e-5, du); });
   const long long f_cond = count([&] { (void)condition(K, u, tau); });
   // a grid point of the scan: condition at t from the geometric recurrence (t *= q: 1 FLOP)
@@ -95,8 +98,9 @@ static void emit(bool flat, bool last) {
   OC pos[3] = {OC(15.0), OC(3.0), OC(4.0)}, kp[3] = {OC(1e-6), OC(2e-6), OC(-1e-6)};
   const long long f_prob = count([&] { (void)prob_nonad_single(K, pos, kp, OC(1.00000027e-5)); });
   // scan_certified_code (double only, hand count): 4 Bernstein hulls x 11, the u7 bounds 4,
-  // t0 and t1 3, two sincos 4 + ψ 2, b(end) 8, Δθ 2, Δψ 6, |b|max 5, the final test 5
-  const long long f_cert = 4 * 11 + 4 + 3 + 6 + 8 + 2 + 6 + 5 + 5;
+  // t0 and t1 3, two sincos 4 + ψ 2, b(end) 8, Δθ 2, Δψ 6, |b|max 5, the final test 5, and
+  // the two-sided bound on b (two control-polygon variations 2 x 9, ℓ 7, lo/hi 5)
+  const long long f_cert = 4 * 11 + 4 + 3 + 6 + 8 + 2 + 6 + 5 + 5 + 18 + 7 + 5;
   std::printf(
       "  \"%s\": {\n    \"rhs_photon\": %lld,\n    \"rhs_axion\": %lld,\n    \"condition\": %lld,\n"
       "    \"condition_scan_point\": %lld,\n    \"hermite_point\": %lld,\n"
