@@ -341,6 +341,12 @@ enum LaneMode { M_IDLE = 0, M_STEP = 2, M_ROOT = 3 };
 constexpr int BLOCK = ART_BLOCK;
 constexpr int SCAN_WORDS = 4;  // 2-bit codes for up to 64 grid points (interp_points <= 65)
 // Waves per SIMD the integrator is register-budgeted for (1: 512 VGPR+AGPR, 2: 256).
+#ifndef ART_SUNROLL
+#define ART_SUNROLL 1  // the stage slot loop: one RHS site
+#endif
+#ifndef ART_SUNROLL_GR
+#define ART_SUNROLL_GR 2  // GR: two RHS sites (A/B: lone GR tail ray -6%; flat: bulk +-0, lone +1%)
+#endif
 #ifndef ART_QUNROLL
 #define ART_QUNROLL 5  // = LDS_SLOTS: the slot range fully unrolled (A/B: -0.8% bulk, -3% lone ray)
 #endif
@@ -392,6 +398,7 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
   // the callbacks (RayTracer.jl:357-368) are installed only when make_tree (:361-377)
   const bool cbs = max_crossings != ART_NO_CALLBACKS;
   constexpr int NSLOT = RK4 ? 4 : 8;
+  constexpr int SUNROLL = GEOM == GEOM_GR ? ART_SUNROLL_GR : ART_SUNROLL;
   const StageTable& T = RK4 ? c_rk4 : c_vern6;
   __shared__ double lds[LDS_SLOTS * 7 * BLOCK];  // [slot][component][lane]: conflict-free ds_read_b64
   __shared__ unsigned codes[SCAN_WORDS * BLOCK];  // [word][lane]: 2-bit sign codes of the grid scan
@@ -545,7 +552,7 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
     double kA[7], y[7], kk[7];
 #pragma unroll
     for (int i = 0; i < 7; ++i) kA[i] = 0.0;  // read (times a zero coefficient) before its first store
-#pragma unroll 1
+#pragma unroll SUNROLL
     for (int s = 0; s < NSLOT; ++s) {
       const SlotRow R = T.row[s];
       const double cf = R.cf, cA = R.cA;
