@@ -65,15 +65,17 @@ def run_point(kw: dict, rays: int, seed: int = 1769, nbins: int = 50, device: in
 
 
 def run_points(kws: list[dict], rays: int, seed: int = 1769, nbins: int = 50, device: int = 0,
-               streams: int = 16) -> tuple[list[dict], dict]:
-    """Several grid points on one GPU, `streams` of them in flight: every point's forward
-    roots are sampled first, then the points are propagated on `streams` HIP streams, each
-    next point on the first stream to go idle (dispatch) -- each launch has its own device scratch (include/art.h), so a point's drain tail
-    (its last long rays on a few CUs; 130-900 ms per 1e6-ray point when run alone) overlaps
-    the other points' bulk -- and each point's flux is binned on its stream. Streams only run
-    concurrently up to the process's hardware queues: main() raises GPU_MAX_HW_QUEUES to 16
-    (HIP's default is 4; 16 streams measured fastest on one MI355X). Returns the
-    per-point records and a summary of the propagate phase (wall time, Σ accepted steps)."""
+               streams: int = 8) -> tuple[list[dict], dict]:
+    """Several grid points on one GPU, `streams` of them in flight. Every point's forward
+    roots are sampled first; then the points are propagated on `streams` HIP streams, longest
+    expected drain (largest conversion radius) first, each next point on the first stream to
+    go idle (dispatch). Each launch has its own device scratch (include/art.h), so a point's
+    drain tail (its last long rays on a few CUs; 20-840 ms per 1e6-ray point) overlaps the
+    other points' bulk, and each point's flux is binned on its stream. Streams run
+    concurrently only up to the process's hardware queues: main() raises GPU_MAX_HW_QUEUES
+    to the stream count (HIP's default is 4; 8 streams measured fastest on one MI355X, 16
+    slower). Returns the per-point records (grid order) and a summary of the propagate
+    phase (wall time, Σ accepted steps)."""
     import ctypes as C
 
     import torch
@@ -95,7 +97,10 @@ def run_points(kws: list[dict], rays: int, seed: int = 1769, nbins: int = 50, de
             engs.append(None)
         else:
             engs.append(Engine(p, device=device))
-    live = [i for i, e in enumerate(engs) if e is not None]
+    # Longest expected drain first: a point's kernel time grows with its conversion radius
+    # (maxR: 29 km -> 20 ms ... 342 km -> 835 ms per 1e6 rays, profiles/r02b_scan_order.txt),
+    # and the longest single ray bounds the whole scan, so it should start at once.
+    live = sorted((i for i, e in enumerate(engs) if e is not None), key=lambda i: -recs[i]["max_r_km"])
     inps, outs, hists = {}, {}, {}
 
     def sample(i):  # the samplers' tails overlap too
@@ -163,7 +168,7 @@ def dispatch(items, launch, streams, poll_s=2e-4):
     return order
 
 
-def run_scan(rays: int, n_points: int | None = None, seed: int = 1769, run=None, streams: int = 16):
+def run_scan(rays: int, n_points: int | None = None, seed: int = 1769, run=None, streams: int = 8):
     """This rank's share of the grid (run_points, or `run` point by point); with
     WORLD_SIZE > 1 the records are gathered on every rank (all_gather_object) and returned in
     grid order."""
@@ -191,7 +196,7 @@ def main():
     ap.add_argument("--points", type=int, default=None)
     ap.add_argument("--seed", type=int, default=1769)
     ap.add_argument("--out", default=None)
-    ap.add_argument("--streams", type=int, default=16)
+    ap.add_argument("--streams", type=int, default=8)
     args = ap.parse_args()
     # concurrent kernels need hardware queues: one per stream in flight (read at HIP init)
     want = min(16, max(4, args.streams))
