@@ -227,7 +227,8 @@ def main():
     total_steps, t_max, total_rays = reduce_totals(accepted, elapsed, n, world, device=eng.device)
 
     if rank == 0:
-        fl = json.load(open(os.path.join(HERE, "tools", "flops.json")))[args.config]
+        fl_all = json.load(open(os.path.join(HERE, "tools", "flops.json")))
+        fl, fl_r1 = fl_all[args.config], fl_all[args.config + "_round1"]
         kms = float(np.mean(kernel_ms))
         fpl = flops_per_launch(stats_last, fl, args.integrator)
         achieved = fpl / (kms * 1e-3) / 1e12
@@ -272,6 +273,8 @@ def main():
                          "frac": achieved / PEAK_FP64_TFLOPS, "traffic": traffic,
                          "kernel": f"propagate_kernel<{'RK4' if args.integrator == 'rk4' else 'Vern6'}>", "kernel_ms": kms,
                          "flops_per_launch": fpl, "flops_per_ray_step": fpl / stats_last["accepted"],
+                         "frac_round1_flop_table": flops_per_launch(stats_last, fl_r1, args.integrator) / (kms * 1e-3)
+                                                   / 1e12 / PEAK_FP64_TFLOPS,
                          "achieved_wall": fpl * args.steps / elapsed / 1e12,
                          "note": "FP64 VALU-bound (state in VGPRs, ~1 B of HBM per ray-step); peak = 78.6 TFLOP/s "
                                  "FP64 (vector = matrix dense peak). FLOPs from the kernel's counters x "
