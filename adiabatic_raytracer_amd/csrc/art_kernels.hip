@@ -341,6 +341,11 @@ enum LaneMode { M_IDLE = 0, M_STEP = 2, M_ROOT = 3 };
 constexpr int BLOCK = ART_BLOCK;
 constexpr int SCAN_WORDS = 4;  // 2-bit codes for up to 64 grid points (interp_points <= 65)
 // Waves per SIMD the integrator is register-budgeted for (1: 512 VGPR+AGPR, 2: 256).
+// Loop-carried per-lane flags: bool lets the compiler keep them as 64-bit lane masks in SGPR
+// pairs, which the integrator's SGPR pressure spills to VGPR lanes; int keeps them in VGPRs.
+#ifndef ART_LBOOL
+#define ART_LBOOL int
+#endif
 #ifndef ART_SUNROLL
 #define ART_SUNROLL 1  // the stage slot loop: one RHS site
 #endif
@@ -419,16 +424,16 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
 
   int mode = M_IDLE;
   int ray = -1;
-  bool photon = true;
+  ART_LBOOL photon = true;
   double erg = 0.0;
   // qpow = qold^(1/15) of the PI controller, updated only when qold changes (on accept)
   const double qpow_init = pow(1e-4, 1.0 / 15.0);
   double u[7], f[7], tau = 0.0, dt = 0.0, qpow = qpow_init;
   double cprev = 0.0;
   double bstart = NAN;  // Bz/B_n at u (the previous step's last RHS) for the scan certificate
-  bool cprev_ok = true;  // cprev holds the condition at the step start (false after a certified step)
+  ART_LBOOL cprev_ok = true;  // cprev holds the condition at the step start (false after a certified step)
   int sprev = 0;
-  bool just_evented = false;
+  ART_LBOOL just_evented = false;
   int n_acc = 0, n_rej = 0, ncross = 0, iter = 0;
   double hroot = 0.0, r_tha = 0.0, r_ca = 0.0, r_thb = 0.0, r_cb = 0.0, r_t = 0.0, r_slope = 1.0, post_c = 0.0;
   int post_s = 0, r_side = 0, r_it = 0;
