@@ -346,6 +346,9 @@ constexpr int SCAN_WORDS = 4;  // 2-bit codes for up to 64 grid points (interp_p
 #ifndef ART_LBOOL
 #define ART_LBOOL int
 #endif
+#ifndef ART_LBOOL2
+#define ART_LBOOL2 int  // per-iteration flags too (A/B: 1e7 flat -0.7%)
+#endif
 #ifndef ART_SUNROLL
 #define ART_SUNROLL 1  // the stage slot loop: one RHS site
 #endif
@@ -554,7 +557,7 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
 #endif
 
     // ---- this iteration's step size ----
-    bool last = false, forced = false;
+    ART_LBOOL2 last = false, forced = false;
     double hs = 0.0;
     if (mode == M_ROOT) {
       hs = r_t * hroot;
@@ -643,7 +646,7 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
 
     // ---- controller (STEP lanes) ----
     int finish = -1;
-    bool scan = false;  // accepted step to be scanned for sign changes
+    ART_LBOOL2 scan = false;  // accepted step to be scanned for sign changes
     double dtnext = dt;
     if (mode == M_STEP) {
       s_att += 1;
@@ -705,7 +708,7 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
     const double bend = lastv[threadIdx.x];
     const int ccode =
         !scan ? 0 : (cbs ? scan_certified_code(P, u, f, y, kk, hs, bend, lastt[threadIdx.x], bstart) : 3);
-    const bool cert = ccode != 0;
+    const ART_LBOOL2 cert = ccode != 0;
 #ifdef ART_COUNT_SUB
     const int cdiag = (scan && !cert) ? scan_cert_diag(P, u, f, y, kk, hs, bend, lastt[threadIdx.x], bstart) : 0;
 #endif
@@ -722,7 +725,7 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
     }
     L[(4 * 7 + 0) * BLOCK] = hs;
     L[(4 * 7 + 1) * BLOCK] = tau;
-    const bool grid = scan && !cert;
+    const ART_LBOOL2 grid = scan && !cert;
     const unsigned long long smask = __ballot(grid);
     // lanes polishing a crossing need the condition at the end of their re-step (th = 1 of the
     // parked step): those items ride in the same pass, after the grid items
@@ -794,7 +797,7 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
     int ip = 1, last_j = 0;
     int last_s = sprev;
     double last_c = cprev;
-    bool lc_ok = cprev_ok;  // last_c is the value at grid point last_j (0: the step start)
+    ART_LBOOL2 lc_ok = cprev_ok;  // last_c is the value at grid point last_j (0: the step start)
     unsigned cw[SCAN_WORDS] = {0u, 0u, 0u, 0u};
     if (ph == 2) {
 #pragma unroll
@@ -860,7 +863,7 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
     }
     double i_tha = 0.0, i_ca = 0.0, i_thb = 0.0, i_cb = 0.0, i_tr = 0.0, i_cg = 0.0;
     int i_side = 0, i_it = 0;
-    bool hit = false, root_done = false;
+    ART_LBOOL2 hit = false, root_done = false;
     // a crossing in (θ_last, θ_ip]: polish it on the true trajectory (mode ROOT), from t_int
     auto open_root = [&](double t_int) {
       const double thg = thgrid[ip];
@@ -903,7 +906,7 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
     // walk the codes from grid point ip (no evaluations): ph 5 at a sign change, 7 when the
     // value at the last nonzero point is still needed, else 0
     auto walk = [&]() {
-      WalkState ws{ip, last_s, last_j, lc_ok};
+      WalkState ws{ip, last_s, last_j, lc_ok != 0};
       bool found = false;
       if (!walk_codes_bits(cw, nper, ws, found)) walk_codes_loop(cw, nper, ws, found);
       ip = ws.ip;
