@@ -54,8 +54,11 @@ __host__ __device__ inline void msincos(double x, double& s, double& c) {
   const int q = ((int)n) & 3;
   const double ss = (q & 1) ? cr : sr;
   const double cc = (q & 1) ? sr : cr;
-  s = (q & 2) ? -ss : ss;
-  c = ((q + 1) & 2) ? -cc : cc;
+  // the quadrant's signs by flipping the sign bit (an XOR of the high word instead of a
+  // compare and a select of both words): -x exactly
+  const unsigned long long ms = (unsigned long long)(q & 2) << 62, mc = (unsigned long long)((q + 1) & 2) << 62;
+  s = __builtin_bit_cast(double, __builtin_bit_cast(unsigned long long, ss) ^ ms);
+  c = __builtin_bit_cast(double, __builtin_bit_cast(unsigned long long, cc) ^ mc);
 }
 // max(|a|, |b|), min(a, b) and max(a, b) as one instruction each. LLVM's fmax/fmin in IEEE
 // mode first quiet signaling NaNs with a v_max x, x per operand it cannot prove canonical
@@ -87,6 +90,14 @@ __host__ __device__ inline double fmax_q(double a, double b) {
 #else
   return fmax(a, b);
 #endif
+}
+// The radius clamped to rNS (:531): max(r, rNS) for the double path (one v_max_f64 instead
+// of a compare and two selects; a NaN radius gives rNS here, and the NaN state itself is
+// what the integrator reports), the select for the op-counting and dual types.
+__host__ __device__ inline double rclamp(double r, double rns) { return fmax(r, rns); }
+template <class T>
+__host__ __device__ inline T rclamp(const T& r, double rns) {
+  return (r < rns) ? T(rns) : r;
 }
 // 1/x from the hardware reciprocal and two Newton steps (~0.5 ulp; 1/0 and 1/inf give NaN,
 // which the integrator reports as a non-finite state either way). The host build, which the
@@ -463,7 +474,7 @@ __host__ __device__ inline void rhs_photon_gj(const KParams& P, const T* u, cons
   const T t = fexp(tau);
   const T r = u[0];
   const T E = -u[6];
-  const T rc = (r < P.rNS) ? T(P.rNS) : r;
+  const T rc = rclamp(r, P.rNS);  // max(r, rNS) in one instruction
   T st, ct, sp, cp;
   msincos(u[1], st, ct);
   msincos(u[2] - P.omega * t, sp, cp);
