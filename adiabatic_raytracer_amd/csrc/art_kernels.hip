@@ -1074,17 +1074,26 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
         else open_bracket();
       } else {  // ph == 3: Illinois on the interpolant inside (i_tha, i_thb]
         bool stop = ci == 0.0 || isnan(ci) || (i_thb - i_tha) < 1e-12;
+        bool below = false;
         if (!stop) {
           if (sgn(ci) == sgn(i_ca)) { i_tha = i_tr; i_ca = ci; if (i_side == -1) i_cb *= 0.5; i_side = -1; }
           else { i_thb = i_tr; i_cb = ci; if (i_side == 1) i_ca *= 0.5; i_side = 1; }
-          const double tn = i_tha - i_ca * (i_thb - i_tha) / (i_cb - i_ca);
-          if (tn == i_tr) stop = true;
-          else i_tr = tn;
-          if (++i_it >= 40) stop = true;
+          // Every later iterate stays in [i_tha, i_thb]: once that lies below θ = 0.01 right
+          // after an event, the root is ignored (repeat_nudge) wherever Illinois would end,
+          // so the search stops here with the same outcome
+          below = just_evented && i_thb < 0.01;
+          if (below) {
+            stop = true;
+          } else {
+            const double tn = i_tha - i_ca * (i_thb - i_tha) / (i_cb - i_ca);
+            if (tn == i_tr) stop = true;
+            else i_tr = tn;
+            if (++i_it >= 40) stop = true;
+          }
         }
         if (stop) {
           const double t_int = i_tr;
-          if (!(just_evented && t_int < 0.01)) {  // DiffEq repeat_nudge after an event
+          if (!below && !(just_evented && t_int < 0.01)) {  // DiffEq repeat_nudge after an event
             open_root(t_int);
             ph = 0;
           } else {  // ignored: continue the walk after the change point
