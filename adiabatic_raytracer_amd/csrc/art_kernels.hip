@@ -467,8 +467,9 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
 #define ART_SMARK(k)
 #endif
 #ifdef ART_COUNT_SUB
-  // dev: uncertified steps; all-positive ones; of those bmin <= 0; of those a positive-test near
-  // miss; all-negative ones; ones with a sign change; first steps of a ray
+  // dev: uncertified steps; all-positive ones; all-negative ones failing on u7 (cert_e2); all-
+  // positive positive-test near misses; all-negative ones; ones with a sign change; all-negative
+  // negative-test near misses
   unsigned s_sub[7] = {0, 0, 0, 0, 0, 0, 0};
 #endif
 #ifdef ART_COUNT_PASSES
@@ -819,11 +820,11 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
           if (si != 0) ls = si;
         }
         s_sub[1] += allp ? 1u : 0u;
-        s_sub[2] += (allp && (cdiag & 1)) ? 1u : 0u;
+        s_sub[2] += (alln && (cdiag & 8)) ? 1u : 0u;  // all-negative, u7 too close to the shell
         s_sub[3] += (allp && (cdiag & 2)) ? 1u : 0u;
         s_sub[4] += alln ? 1u : 0u;
         s_sub[5] += chg ? 1u : 0u;
-        s_sub[6] += (n_acc == 1) ? 1u : 0u;
+        s_sub[6] += (alln && (cdiag & 4)) ? 1u : 0u;  // all-negative, negative test within 2x
       }
 #endif
       // fast path: every grid point has the previous sign (or the previous sign is unknown

@@ -9,7 +9,7 @@ import adiabatic_raytracer_amd as A  # noqa: E402
 from adiabatic_raytracer_amd import Engine  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 1_000_000
-NAMES = ["uncertified", "all_pos", "all_pos_bmin_le0", "all_pos_near_miss", "all_neg", "sign_change", "first_step"]
+NAMES = ["uncertified", "all_pos", "all_neg_e2_fail", "all_pos_near_miss", "all_neg", "sign_change", "all_neg_near_miss"]
 for name, kw in (("flat", dict(theta_m=0.2, mass_a=1e-5, flat=True)), ("gr", dict(theta_m=0.0, mass_a=1e-6, flat=False))):
     eng = Engine(A.Params(**kw))
     inp = eng.forward_roots(n, seed=1769)
