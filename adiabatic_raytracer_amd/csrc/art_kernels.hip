@@ -578,7 +578,11 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
       const double cf = R.cf, cA = R.cA;
       double acc[7];
 #pragma unroll
-      for (int i = 0; i < 7; ++i) acc[i] = cf * f[i] + cA * kA[i];
+      for (int i = 0; i < 7; ++i) acc[i] = cf * f[i];
+      if (cA != 0.0) {  // wave-uniform: only Vern6's a32 and a98 rows use the register stage
+#pragma unroll
+        for (int i = 0; i < 7; ++i) acc[i] = fma(cf, f[i], cA * kA[i]);  // (the rounding of the general form)
+      }
       // the LDS slots this stage reads form one contiguous range [qlo, qhi) (lmask): no
       // per-slot load-compare-branch, and each coefficient load overlaps the slot's LDS reads
       const int lm = R.lmask;
