@@ -491,15 +491,26 @@ __host__ __device__ inline void rhs_photon_gj(const KParams& P, const T* u, cons
   const T ir = inv_rs * ast, iast = inv_rs * rc;
   // Schwarzschild: g^rr at the clamped radius, its derivatives, and g^rr at the raw radius for
   // the prefactor (:82), which differs only inside the star
-  T gtt = -1.0, grr = 1.0, dgtt = 0.0, dgrr = 0.0, grr_u = 1.0, sq = 1.0;
+  T grr = 1.0, dgtt = 0.0, dgrr = 0.0, grr_u = 1.0, sq = 1.0, isq = 1.0;
   if (!flat) {
-    metric_tr_d(rc, P.rs_eff, gtt, grr, dgtt, dgrr);
+    if (rc <= 10.0) {  // g_schwartz's interior patch (a radius clamped to rNS <= 10 km)
+      T gtt;
+      metric_tr_d(rc, P.rs_eff, gtt, grr, dgtt, dgrr);
+      sq = msqrt(grr);
+      isq = trcp(sq);
+    } else {  // metric_tr_d's exterior branch on the shared 1/r: one reciprocal, 1/g^rr
+      grr = 1.0 - P.rs_eff * ir;
+      dgrr = P.rs_eff * ir * ir;
+      const T ig = trcp(grr);
+      dgtt = dgrr * ig * ig;
+      sq = msqrt(grr);
+      isq = sq * ig;  // 1/√g^rr = √g^rr / g^rr
+    }
     grr_u = grr;
     if (r < P.rNS) {
       T gtt_u;
       metric_tr(r, P.rs_eff, gtt_u, grr_u);
     }
-    sq = msqrt(grr);
   }
   // rotating dipole (dipole_ang)
   const T cmst = P.cm * st, smct = P.sm * ct, smst = P.sm * st;
@@ -530,7 +541,7 @@ __host__ __device__ inline void rhs_photon_gj(const KParams& P, const T* u, cons
   const T kp2 = kp * kp;
   T H_r = w * ir2 * pa - ir3 * (kt * kt + iast2 * kp2) - 1.5 * wp2 * ir * omQ;
   if (!flat)
-    H_r += 0.5 * (dgtt * (E * E) + dgrr * (kr * kr) - wp2 * dgrr * Gp * p) - w * dgrr * frcp(sq) * kr * a1;
+    H_r += 0.5 * (dgtt * (E * E) + dgrr * (kr * kr) - wp2 * dgrr * Gp * p) - w * dgrr * isq * kr * a1;
   const T H_t = -ct * ir2 * iast2 * iast * sgn_st * kp2 - 1.5 * cBs * (a2 * ct + a1 * st) * omQ - w * p_t -
                 3.0 * Qib * a1 * a2;
   const T H_p = 1.5 * cBs * a1p * ct * omQ - w * p_p + 0.5 * Qib * beta_p;
