@@ -178,10 +178,12 @@ def main():
     # bulk instead of idling the GPU. Each launch has its own scratch (include/art.h).
     if args.streams <= 0:
         # the drain tail (~3 ms: the last long rays) is ~3% of a 1e7-ray pass but ~20% of the
-        # 1.25e6 rays per GPU of the 8-GPU split; overlapping two passes hides part of it there.
-        # Overlapped launches also stretch each other's measured duration, so the roofline of
-        # the single-GPU headline is taken without overlap.
-        args.streams = 1 if n >= 4_000_000 else 2
+        # 1.25e6 rays per GPU of the 8-GPU split; overlapping passes hides part of it there.
+        # Measured per shard size (profiles/r02b_streams_by_shard.txt): 1.25e6 and 2.5e6 rays
+        # best with 3 passes in flight, 5e6 (the 2-GPU split) with 2, 1e7 with 1 (2 and 3 are
+        # 14% and 4% slower there). Overlapped launches also stretch each other's measured
+        # duration, so the roofline of the single-GPU headline is taken without overlap.
+        args.streams = 1 if n >= 8_000_000 else (2 if n >= 4_000_000 else 3)
     streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(args.streams - 1)]
     for st_ in streams[1:]:
         st_.wait_stream(streams[0])  # the sampled inputs
