@@ -131,7 +131,7 @@ def run_points(kws: list[dict], rays: int, seed: int = 1769, nbins: int = 50, de
         recs[i].update(kernel_ms=kms.get(i), accepted=acc, attempts=att,
                        status_counts=torch.bincount(o["status"].long(), minlength=5).tolist(),
                        flux_photon=hists[i][nbins:].tolist())
-    summary = {"points": k, "streams": len(ss), "sample_s": t_sample, "propagate_wall_s": wall,
+    summary = {"points": k, "streams": len(ss), "order": order, "sample_s": t_sample, "propagate_wall_s": wall,
                "accepted": acc_total, "kernel_ray_steps_per_s": acc_total / wall if wall > 0 else None}
     return recs, summary
 

@@ -29,3 +29,21 @@ def test_scan_points_run():
         assert a["accepted"] == b["accepted"] and a["status_counts"] == b["status_counts"]
         assert a["flux_photon"] == b["flux_photon"]
 
+
+
+def test_run_points_dispatch_order_and_records():
+    """More points than streams: every point runs (largest conversion radius first, each next
+    point on the first idle stream), the records come back in grid order with their own
+    kernel times, and each equals the point run alone."""
+    import adiabatic_raytracer_amd as A
+    from adiabatic_raytracer_amd.scan import run_point, run_points, scan_grid
+    kws = [scan_grid()[i] for i in (24, 6, 17, 1, 30)]
+    recs, summ = run_points(kws, 1500, streams=2)
+    maxr = [A.Params(**kw).max_r() for kw in kws]
+    assert summ["order"] == sorted(range(len(kws)), key=lambda i: -maxr[i])
+    assert summ["points"] == len(kws) and summ["accepted"] == sum(r["accepted"] for r in recs)
+    for kw, r in zip(kws, recs):
+        assert r["mass_a"] == kw["mass_a"] and r["B0"] == kw["B0"] and r["kernel_ms"] > 0
+        alone = run_point(kw, 1500, 1769)
+        assert r["accepted"] == alone["accepted"] and r["status_counts"] == alone["status_counts"]
+        assert r["flux_photon"] == alone["flux_photon"]
