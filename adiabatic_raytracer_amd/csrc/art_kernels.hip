@@ -358,9 +358,6 @@ constexpr int SCAN_WORDS = 4;  // 2-bit codes for up to 64 grid points (interp_p
 #ifndef ART_QUNROLL
 #define ART_QUNROLL 5  // = LDS_SLOTS: the slot range fully unrolled (A/B: -0.8% bulk, -3% lone ray)
 #endif
-#ifndef ART_DRAIN_PRIO
-#define ART_DRAIN_PRIO 0
-#endif
 #ifndef ART_PRIO_ITERS
 #define ART_PRIO_ITERS 1024
 #endif
@@ -541,16 +538,8 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
     // SIMD's arbiter for issue priority. The one ray that sets a launch's (or a scan point's)
     // drain time then runs at close to its lone-wave speed while the bulk of the batch still
     // shares its SIMD; the other waves fill the issue slots it leaves.
-#if ART_DRAIN_PRIO
-    // dev: a draining wave (queue exhausted, few live lanes) yields issue slots to full waves,
-    // e.g. the next batch's on another stream
-    if (__ballot(iter >= ART_PRIO_ITERS) != 0ull) __builtin_amdgcn_s_setprio(3);
-    else if (exhausted && __popcll(__ballot(mode != M_IDLE)) < ART_DRAIN_PRIO) __builtin_amdgcn_s_setprio(0);
-    else __builtin_amdgcn_s_setprio(1);
-#else
     if (__ballot(iter >= ART_PRIO_ITERS) != 0ull) __builtin_amdgcn_s_setprio(2);
     else __builtin_amdgcn_s_setprio(0);
-#endif
     ART_PC(0)
     ART_TMARK(0)  // refill
 #ifdef ART_COUNT_LOOPS
@@ -1813,13 +1802,7 @@ int persistent_blocks(const void* func, int64_t work, int block) {
   (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, func, block, 0) != hipSuccess || per_cu < 1) per_cu = 1;
   const int64_t need = (work + block - 1) / block;
-  int64_t full = (int64_t)ncu * per_cu;
-  static const double share = [] {  // dev: ART_GRID_SHARE=f sizes persistent grids at f of the device
-    const char* e = getenv("ART_GRID_SHARE");
-    const double f = e ? atof(e) : 1.0;
-    return f > 0.0 && f < 1.0 ? f : 1.0;
-  }();
-  if (share < 1.0) full = (int64_t)(full * share) > 0 ? (int64_t)(full * share) : 1;
+  const int64_t full = (int64_t)ncu * per_cu;
   return (int)(need < full ? need : full);
 }
 
