@@ -74,6 +74,7 @@ SIGNATURES = {
     "art_event_weight_host": (C.c_int, [_P, _d, _d, _d, _i64, _v, _v, _v, _v]),
     "art_event_weight_device": (C.c_int, [_P, _d, _d, _d, _i64, _v, _v, _v, _v, _v]),
     "art_recent_kernel_ms": (C.c_int, [_i32, _v]),
+    "art_set_tail_donation": (C.c_int, [_i32]),
     "art_flux_histogram_phi_device": (C.c_int, [_i64, _v, _v, _v, _i32, _v, _v]),
     "art_comm_unique_id": (C.c_int, [_v]),
     "art_comm_init": (C.c_int, [_i32, _i32, _v]),

@@ -46,6 +46,7 @@ struct DeviceCtx {
   LaunchRec ring[RING];
   int next = 0, last = -1;       // next ring slot; the most recent propagate launch
   int64_t launches = 0;          // propagate launches issued so far
+  int32_t donate = 0;            // tail donation (art_set_tail_donation): lanes per wave, 0 = off
   std::vector<std::pair<void*, size_t>> pool;  // host-entry staging buffers (grow-only, used under g_mu by the
                                                // synchronous *_host calls only)
 };
@@ -184,10 +185,18 @@ int propagate_device_impl(const art_params* p, int64_t n, const double* x0, cons
   const size_t nd = (size_t)n;
   const size_t head = 256, u0b = nd * 16 * sizeof(double), recb = nd * art::END_REC * sizeof(double);
   const size_t xrb = (size_t)cap * nd * art::X_REC * sizeof(double);
+  // tail donation: at most (resident waves) x donate records of CONT_REC doubles
+  size_t ncont = 0;
+  if (c->donate > 0) {
+    int ncu = 0;
+    HIP_OK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device));
+    ncont = std::min(nd, (size_t)ncu * 32 * (size_t)c->donate);
+  }
+  const size_t contb = ncont * art::CONT_REC * sizeof(double);
   LaunchRec* L;
   if ((rc = take_slot(c, &L))) return rc;
   void* blk = nullptr;
-  if ((rc = scratch_alloc(s, head + u0b + recb + xrb, &blk))) return rc;
+  if ((rc = scratch_alloc(s, head + u0b + recb + xrb + contb, &blk))) return rc;
   unsigned long long* words = (unsigned long long*)blk;
   double* u0 = (double*)((char*)blk + head);
   double* rec = (double*)((char*)blk + head + u0b);
@@ -207,6 +216,12 @@ int propagate_device_impl(const art_params* p, int64_t n, const double* x0, cons
     so.traj_n = tr.count;
   }
   so.rec = rec;
+  if (ncont) {
+    so.cont = (double*)((char*)blk + head + u0b + recb + xrb);
+    so.cont_count = words + 16;  // head words 16 and 17 (zeroed with the head)
+    so.cont_queue = words + 17;
+    so.donate = c->donate;
+  }
   HIP_OK(hipMemsetAsync(words, 0, head, s));
   HIP_OK(art::launch_propagate(K, n, in, so, max_crossings, words, words + 1, s, &L->grid, L->ev0, L->ev1));
   HIP_OK(hipMemcpyAsync(L->host_stats, words + 1, sizeof(unsigned long long) * art::N_STATS, hipMemcpyDeviceToHost, s));
@@ -249,6 +264,16 @@ int art_device_count(int32_t* count) {
 int art_set_device(int32_t device) {
   std::lock_guard<std::mutex> lk(g_mu);
   HIP_OK(hipSetDevice(device));
+  return ART_OK;
+}
+
+int art_set_tail_donation(int32_t lanes) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (lanes < 0 || lanes > 63) return fail(ART_E_INVALID, "tail donation lanes must be in [0, 63]");
+  DeviceCtx* c;
+  int rc = current_ctx(&c);
+  if (rc) return rc;
+  c->donate = lanes;
   return ART_OK;
 }
 

@@ -34,9 +34,19 @@ struct SegOut {
   // crossings affect! records: [x (3) | k (3) | t | Δω] at ((ray cap + j) X_REC), spread into
   // xpos / xk / xt / xdw by finalize_kernel
   double* xrec;
+  // Tail donation (art_set_tail_donation): once the queue is drained, a wave whose live rays
+  // (all at a step boundary) number at most `donate` writes their complete integrator state
+  // as CONT_REC-double records to cont[] (count in *cont_count) and retires, so its CU slot
+  // goes to the next launch in flight; a continuation launch (cont_mode = 1) then integrates
+  // those rays packed into full waves, bit for bit as if they had never moved.
+  double* cont;
+  unsigned long long* cont_count;
+  unsigned long long* cont_queue;
+  int32_t donate, cont_mode;
 };
 constexpr int END_REC = 16;
 constexpr int X_REC = 8;
+constexpr int CONT_REC = 24;  // [u (7) | f (7) | τ, dt, qpow, cprev, bstart, erg | int4 {ray, n_acc, n_rej, ncross} | int4 {iter, sprev, flags, save_k}]
 constexpr int N_STATS = 8;  // propagate statistics: attempts, accepted, root re-steps, scan evals,
                             // interpolant-root evals, rays, init RHS, (reserved)
 int persistent_blocks(const void* func, int64_t work, int block);

@@ -403,6 +403,9 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
                                                                               unsigned long long* __restrict__ stats) {
   const KParams P = specialize<GEOM>(P_in);
   constexpr bool RK4 = (INTEG == ART_RK4);
+  // the work queue: fresh rays [0, n), or in a continuation launch the donated records
+  const int64_t nq = out.cont_mode ? (int64_t)*out.cont_count : n;
+  unsigned long long* const rqueue = out.cont_mode ? out.cont_queue : queue;
   // the callbacks (RayTracer.jl:357-368) are installed only when make_tree (:361-377)
   const bool cbs = max_crossings != ART_NO_CALLBACKS;
   constexpr int NSLOT = RK4 ? 4 : 8;
@@ -496,16 +499,49 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
         if (wnext >= wend) {
           unsigned long long base = 0;
           const int leader = __ffsll((long long)need) - 1;
-          if (lane == leader) base = atomicAdd(queue, (unsigned long long)CHUNK);
+          if (lane == leader) base = atomicAdd(rqueue, (unsigned long long)CHUNK);
           base = __shfl(base, leader);
-          if ((int64_t)base >= n) { exhausted = true; break; }
+          if ((int64_t)base >= nq) { exhausted = true; break; }
           wnext = __builtin_amdgcn_readfirstlane((int)base);
-          wend = __builtin_amdgcn_readfirstlane((int)((int64_t)base + CHUNK < n ? (int64_t)base + CHUNK : n));
+          wend = __builtin_amdgcn_readfirstlane((int)((int64_t)base + CHUNK < nq ? (int64_t)base + CHUNK : nq));
         }
         const int rank = __popcll(need & ((1ull << lane) - 1ull));
         const int cnt = __popcll(need);
         const int take = (wend - wnext) < cnt ? (wend - wnext) : cnt;
-        if (mode == M_IDLE && rank < take) {
+        if (mode == M_IDLE && rank < take && out.cont_mode) {
+          // a donated ray: its complete state from the tail-donation record
+          mode = M_STEP;
+          const double2* rq = reinterpret_cast<const double2*>(out.cont + (int64_t)(wnext + rank) * CONT_REC);
+          double v[20];
+#pragma unroll
+          for (int i = 0; i < 10; ++i) {
+            const double2 q = rq[i];
+            v[2 * i] = q.x;
+            v[2 * i + 1] = q.y;
+          }
+#pragma unroll
+          for (int i = 0; i < 7; ++i) {
+            u[i] = v[i];
+            f[i] = v[7 + i];
+          }
+          tau = v[14];
+          dt = v[15];
+          qpow = v[16];
+          cprev = v[17];
+          bstart = v[18];
+          erg = v[19];
+          const int4 i0 = reinterpret_cast<const int4*>(rq + 10)[0], i1 = reinterpret_cast<const int4*>(rq + 10)[1];
+          ray = i0.x;
+          n_acc = i0.y;
+          n_rej = i0.z;
+          ncross = i0.w;
+          iter = i1.x;
+          sprev = i1.y;
+          save_k = i1.w;
+          photon = i1.z & 1;
+          cprev_ok = (i1.z >> 1) & 1;
+          just_evented = (i1.z >> 2) & 1;
+        } else if (mode == M_IDLE && rank < take) {
           ray = wnext + rank;
           mode = M_STEP;
           // fresh segment: u0, f(u0), the initial dt and the initial condition value, all
@@ -1174,6 +1210,30 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
       mode = M_IDLE;
     }
     ART_TMARK(0)  // saveat, reload, events, finish and the output stores (+ refill)
+    // tail donation (SegOut::donate): the drained wave's last few rays, all at a step
+    // boundary, leave for the continuation launch and the wave retires
+    if (exhausted && out.donate > 0) {
+      const unsigned long long live = __ballot(mode != M_IDLE);
+      if (live != 0ull && __popcll(live) <= out.donate && __ballot(mode == M_ROOT) == 0ull) {
+        const int leader = __ffsll((long long)live) - 1;
+        unsigned long long base = 0;
+        if (lane == leader) base = atomicAdd(out.cont_count, (unsigned long long)__popcll(live));
+        base = __shfl(base, leader);
+        if (mode != M_IDLE) {
+          const int64_t slot = (int64_t)base + __popcll(live & ((1ull << lane) - 1ull));
+          double2* rq = reinterpret_cast<double2*>(out.cont + slot * CONT_REC);
+          const double v[20] = {u[0], u[1], u[2], u[3], u[4], u[5], u[6], f[0], f[1], f[2],
+                                f[3], f[4], f[5], f[6], tau, dt, qpow, cprev, bstart, erg};
+#pragma unroll
+          for (int i = 0; i < 10; ++i) rq[i] = make_double2(v[2 * i], v[2 * i + 1]);
+          int4* ri = reinterpret_cast<int4*>(rq + 10);
+          ri[0] = make_int4(ray, n_acc, n_rej, ncross);
+          ri[1] = make_int4(iter, sprev, (photon ? 1 : 0) | (cprev_ok ? 2 : 0) | (just_evented ? 4 : 0), save_k);
+          ray = -1;
+          mode = M_IDLE;
+        }
+      }
+    }
   }
 
   // wave-reduce the statistics and add them once per wave
@@ -1833,6 +1893,15 @@ hipError_t launch_propagate(const KParams& P, int64_t n, const SegIn& in, const 
   if (ev0 && (e = hipEventRecord(ev0, s)) != hipSuccess) return e;
   hipLaunchKernelGGL(fn, dim3(grid), dim3(BLOCK), 0, s, P, n, in, out, max_crossings, queue, stats);
   if ((e = hipGetLastError()) != hipSuccess) return e;
+  if (out.donate > 0) {  // the donated tail rays, packed into full waves (at most waves x donate of them)
+    SegOut oc = out;
+    oc.cont_mode = 1;
+    oc.donate = 0;
+    const int64_t maxc = (int64_t)grid * (BLOCK / 64) * out.donate;
+    const int cgrid = (int)((maxc + BLOCK - 1) / BLOCK);
+    hipLaunchKernelGGL(fn, dim3(cgrid), dim3(BLOCK), 0, s, P, n, in, oc, max_crossings, queue, stats);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+  }
   if (ev1 && (e = hipEventRecord(ev1, s)) != hipSuccess) return e;
   hipLaunchKernelGGL(finalize_kernel, dim3(g1), dim3(256), 0, s, P, n, in, out);
   return hipGetLastError();

@@ -76,6 +76,12 @@ class Engine:
             int(max_crossings), C.byref(so), C.byref(xb), _stream()))
         return out
 
+    def set_tail_donation(self, lanes: int) -> None:
+        """Tail donation for launches pipelined with others on other streams
+        (art_set_tail_donation, include/art.h): a drained wave with <= lanes live rays hands
+        them to a continuation launch and retires. Bit-identical results; 0 = off."""
+        check(self.lib.art_set_tail_donation(int(lanes)))
+
     def kernel_ms(self) -> float:
         """Duration of the last propagate kernel (HIP events on its stream); synchronizes."""
         check(self.lib.art_synchronize())

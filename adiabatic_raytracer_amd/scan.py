@@ -65,7 +65,7 @@ def run_point(kw: dict, rays: int, seed: int = 1769, nbins: int = 50, device: in
 
 
 def run_points(kws: list[dict], rays: int, seed: int = 1769, nbins: int = 50, device: int = 0,
-               streams: int = 8) -> tuple[list[dict], dict]:
+               streams: int = 8, donate: int = 0) -> tuple[list[dict], dict]:
     """Several grid points on one GPU, `streams` of them in flight. Every point's forward
     roots are sampled first; then the points are propagated on `streams` HIP streams, longest
     expected drain (largest conversion radius) first, each next point on the first stream to
@@ -97,6 +97,7 @@ def run_points(kws: list[dict], rays: int, seed: int = 1769, nbins: int = 50, de
             engs.append(None)
         else:
             engs.append(Engine(p, device=device))
+            engs[-1].set_tail_donation(donate)
     # Longest expected drain first: a point's kernel time grows with its conversion radius
     # (maxR: 29 km -> 20 ms ... 342 km -> 835 ms per 1e6 rays, profiles/r02b_scan_order.txt),
     # and the longest single ray bounds the whole scan, so it should start at once.

@@ -138,6 +138,8 @@ def main():
                     help="batches in flight (HIP streams); 0: 1 for per-GPU batches of >= 4e6 rays, else 2")
     ap.add_argument("--cpu-rays", type=int, default=int(os.environ.get("ART_CPU_RAYS", "500000")))
     ap.add_argument("--cpu-rays-1t", type=int, default=int(os.environ.get("ART_CPU_RAYS_1T", "24000")))
+    ap.add_argument("--donate", type=int, default=-1,
+                    help="tail donation lanes (art_set_tail_donation); -1: auto by streams in flight")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pcie", action="store_true")
     args = ap.parse_args()
@@ -184,6 +186,12 @@ def main():
         # 14% and 4% slower there). Overlapped launches also stretch each other's measured
         # duration, so the roofline of the single-GPU headline is taken without overlap.
         args.streams = 1 if n >= 8_000_000 else (2 if n >= 4_000_000 else 3)
+    if args.donate < 0:
+        # tail donation only pays when another pass in flight can take the freed CU slots:
+        # 1e6 rays on 3 streams +9%, 1.25e6 +6%; a lone pass loses 0.6-1.7% (its donated rays
+        # resume only after the pass; profiles/r02d_tail_donation.txt)
+        args.donate = 16 if args.streams > 1 else 0
+    eng.set_tail_donation(args.donate)
     streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(args.streams - 1)]
     for st_ in streams[1:]:
         st_.wait_stream(streams[0])  # the sampled inputs
@@ -270,7 +278,7 @@ def main():
                        "m_a_eV": params.mass_a, "theta_m": params.theta_m, "omega_pul": params.omega_pul,
                        "B0_G": params.B0, "rNS_km": params.rNS, "abstol": params.abstol, "reltol": params.reltol,
                        "interp_points": params.interp_points, "parallelism": f"rays sharded x{world}",
-                       "streams": args.streams},
+                       "streams": args.streams, "tail_donation": args.donate},
             "roofline": {"bound": "fp64-valu", "achieved": achieved, "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
                          "frac": achieved / PEAK_FP64_TFLOPS, "traffic": traffic,
                          "kernel": f"propagate_kernel<{'RK4' if args.integrator == 'rk4' else 'Vern6'}>", "kernel_ms": kms,

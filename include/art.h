@@ -148,6 +148,14 @@ int art_last_stats(uint64_t* stats, int32_t* grid);
  * device, oldest first, each from the HIP events around that launch on its own stream (waits
  * for them). Returns the number written (>= 0) or a negative ART_E* code. */
 int art_recent_kernel_ms(int32_t n, double* ms);
+/* Tail donation for propagate launches that are pipelined with others (several batches in
+ * flight on different streams): once a launch's work queue is drained, a wave with at most
+ * `lanes` live rays (all between steps) hands them to a continuation launch on the same
+ * stream and retires, so its CU slot goes to the next batch instead of idling behind one
+ * long ray. The continuation launch integrates the donated rays packed into full waves;
+ * results are bit-identical to lanes = 0 (the default: off). Applies to the current
+ * device's subsequent launches. No reference counterpart (an execution policy). */
+int art_set_tail_donation(int32_t lanes);
 /* The Vern6 tableau the kernel uses: c[9], A[81] row-major, b[9], bhat[9]. */
 int art_vern6_tableau(double* c, double* A, double* b, double* bhat);
 

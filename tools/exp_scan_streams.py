@@ -12,7 +12,8 @@ streams = int(sys.argv[2]) if len(sys.argv) > 2 else 16
 if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < min(16, max(4, streams)):
     os.environ["GPU_MAX_HW_QUEUES"] = str(min(16, max(4, streams)))
 npts = int(sys.argv[3]) if len(sys.argv) > 3 else 32
-recs, summ = run_points(scan_grid()[:npts], rays, streams=streams)
+donate = int(sys.argv[4]) if len(sys.argv) > 4 else 0
+recs, summ = run_points(scan_grid()[:npts], rays, streams=streams, donate=donate)
 for i, r in enumerate(recs):
     print(json.dumps({k: r.get(k) for k in ("mass_a", "B0", "omega_pul", "kernel_ms", "accepted", "attempts")} | {"point": i}))
 print(json.dumps(summ), flush=True)
