@@ -180,12 +180,13 @@ def main():
     # bulk instead of idling the GPU. Each launch has its own scratch (include/art.h).
     if args.streams <= 0:
         # the drain tail (~3 ms: the last long rays) is ~3% of a 1e7-ray pass but ~20% of the
-        # 1.25e6 rays per GPU of the 8-GPU split; overlapping passes hides part of it there.
-        # Measured per shard size (profiles/r02b_streams_by_shard.txt): 1.25e6 and 2.5e6 rays
-        # best with 3 passes in flight, 5e6 (the 2-GPU split) with 2, 1e7 with 1 (2 and 3 are
-        # 14% and 4% slower there). Overlapped launches also stretch each other's measured
-        # duration, so the roofline of the single-GPU headline is taken without overlap.
-        args.streams = 1 if n >= 8_000_000 else (2 if n >= 4_000_000 else 3)
+        # 1.25e6 rays per GPU of the 8-GPU split; overlapping passes (with tail donation, below)
+        # hides most of it there. Measured per shard size with donation
+        # (profiles/r02d_streams_by_shard_donation.txt): 1e6-5e6 rays best with 3 passes in
+        # flight. Overlapped launches stretch each other's measured duration, so the
+        # single-GPU headline (1e7 rays) runs one pass at a time and its roofline is the
+        # kernel's own (2 passes with donation were within 1% there).
+        args.streams = 1 if n >= 8_000_000 else 3
     if args.donate < 0:
         # tail donation only pays when another pass in flight can take the freed CU slots:
         # 1e6 rays on 3 streams +9%, 1.25e6 +6%; a lone pass loses 0.6-1.7% (its donated rays
