@@ -395,7 +395,9 @@ __device__ inline KParams specialize(const KParams& P) {
   return Q;
 }
 
-template <int INTEG, int GEOM, bool SAVE>
+// DON: the tail-donation instantiations (SegOut::donate / cont_mode honoured); the others
+// carry none of that code, so a lone pass pays nothing for it
+template <int INTEG, int GEOM, bool SAVE, bool DON>
 __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(const KParams P_in, const int64_t n,
                                                                               const SegIn in, const SegOut out,
                                                                               const int32_t max_crossings,
@@ -404,8 +406,9 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
   const KParams P = specialize<GEOM>(P_in);
   constexpr bool RK4 = (INTEG == ART_RK4);
   // the work queue: fresh rays [0, n), or in a continuation launch the donated records
-  const int64_t nq = out.cont_mode ? (int64_t)*out.cont_count : n;
-  unsigned long long* const rqueue = out.cont_mode ? out.cont_queue : queue;
+  const bool cont = DON && out.cont_mode;
+  const int64_t nq = cont ? (int64_t)*out.cont_count : n;
+  unsigned long long* const rqueue = cont ? out.cont_queue : queue;
   // the callbacks (RayTracer.jl:357-368) are installed only when make_tree (:361-377)
   const bool cbs = max_crossings != ART_NO_CALLBACKS;
   constexpr int NSLOT = RK4 ? 4 : 8;
@@ -508,7 +511,7 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
         const int rank = __popcll(need & ((1ull << lane) - 1ull));
         const int cnt = __popcll(need);
         const int take = (wend - wnext) < cnt ? (wend - wnext) : cnt;
-        if (mode == M_IDLE && rank < take && out.cont_mode) {
+        if (mode == M_IDLE && rank < take && cont) {
           // a donated ray: its complete state from the tail-donation record
           mode = M_STEP;
           const double2* rq = reinterpret_cast<const double2*>(out.cont + (int64_t)(wnext + rank) * CONT_REC);
@@ -1212,7 +1215,7 @@ __global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(co
     ART_TMARK(0)  // saveat, reload, events, finish and the output stores (+ refill)
     // tail donation (SegOut::donate): the drained wave's last few rays, all at a step
     // boundary, leave for the continuation launch and the wave retires
-    if (exhausted && out.donate > 0) {
+    if (DON && exhausted && out.donate > 0) {
       const unsigned long long live = __ballot(mode != M_IDLE);
       if (live != 0ull && __popcll(live) <= out.donate && __ballot(mode == M_ROOT) == 0ull) {
         const int leader = __ffsll((long long)live) - 1;
@@ -1866,6 +1869,22 @@ int persistent_blocks(const void* func, int64_t work, int block) {
   return (int)(need < full ? need : full);
 }
 
+using KFn = void (*)(const KParams, const int64_t, const SegIn, const SegOut, const int32_t, unsigned long long*,
+                     unsigned long long*);
+
+template <bool DON>
+static KFn pick_propagate(bool save, bool rk4, bool flat, bool sch) {
+  if (save)  // saveat requested: the saving instantiations
+    return rk4 ? propagate_kernel<ART_RK4, GEOM_ANY, true, DON>
+               : (flat ? propagate_kernel<ART_VERN6, GEOM_FLAT, true, DON>
+                       : (sch ? propagate_kernel<ART_VERN6, GEOM_GR, true, DON>
+                              : propagate_kernel<ART_VERN6, GEOM_ANY, true, DON>));
+  return rk4 ? (flat ? propagate_kernel<ART_RK4, GEOM_FLAT, false, DON> : propagate_kernel<ART_RK4, GEOM_ANY, false, DON>)
+             : (flat ? propagate_kernel<ART_VERN6, GEOM_FLAT, false, DON>
+                     : (sch ? propagate_kernel<ART_VERN6, GEOM_GR, false, DON>
+                            : propagate_kernel<ART_VERN6, GEOM_ANY, false, DON>));
+}
+
 hipError_t launch_propagate(const KParams& P, int64_t n, const SegIn& in, const SegOut& out, int32_t max_crossings,
                             unsigned long long* queue, unsigned long long* stats, hipStream_t s, int* grid_out,
                             hipEvent_t ev0, hipEvent_t ev1) {
@@ -1877,17 +1896,8 @@ hipError_t launch_propagate(const KParams& P, int64_t n, const SegIn& in, const 
   const bool flat = P.rs_eff == 0.0 && !(P.bndry_lyr > 0.0) && !P.isotropic;
   const bool sch = P.rs_eff > 0.0 && !(P.bndry_lyr > 0.0) && !P.isotropic;
   const bool rk4 = P.integrator == ART_RK4;
-  using KFn = void (*)(const KParams, const int64_t, const SegIn, const SegOut, const int32_t, unsigned long long*,
-                       unsigned long long*);
-  KFn fn;
-  if (out.ntimes >= 2)  // saveat requested: the saving instantiations
-    fn = rk4 ? propagate_kernel<ART_RK4, GEOM_ANY, true>
-             : (flat ? propagate_kernel<ART_VERN6, GEOM_FLAT, true>
-                     : (sch ? propagate_kernel<ART_VERN6, GEOM_GR, true> : propagate_kernel<ART_VERN6, GEOM_ANY, true>));
-  else
-    fn = rk4 ? (flat ? propagate_kernel<ART_RK4, GEOM_FLAT, false> : propagate_kernel<ART_RK4, GEOM_ANY, false>)
-             : (flat ? propagate_kernel<ART_VERN6, GEOM_FLAT, false>
-                     : (sch ? propagate_kernel<ART_VERN6, GEOM_GR, false> : propagate_kernel<ART_VERN6, GEOM_ANY, false>));
+  const KFn fn = out.donate > 0 ? pick_propagate<true>(out.ntimes >= 2, rk4, flat, sch)
+                                 : pick_propagate<false>(out.ntimes >= 2, rk4, flat, sch);
   const int grid = persistent_blocks((const void*)fn, n, BLOCK);
   if (grid_out) *grid_out = grid;
   if (ev0 && (e = hipEventRecord(ev0, s)) != hipSuccess) return e;
@@ -1969,24 +1979,5 @@ hipError_t launch_eval_condition(const KParams& P, int64_t n, const double* u, c
   hipLaunchKernelGGL(eval_condition_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, P, n, u, tau, out);
   return hipGetLastError();
 }
-
-template __global__ void propagate_kernel<ART_VERN6, GEOM_ANY, false>(const KParams, const int64_t, const SegIn, const SegOut,
-    const int32_t, unsigned long long*, unsigned long long*);
-template __global__ void propagate_kernel<ART_VERN6, GEOM_FLAT, false>(const KParams, const int64_t, const SegIn, const SegOut,
-    const int32_t, unsigned long long*, unsigned long long*);
-template __global__ void propagate_kernel<ART_VERN6, GEOM_GR, false>(const KParams, const int64_t, const SegIn, const SegOut,
-    const int32_t, unsigned long long*, unsigned long long*);
-template __global__ void propagate_kernel<ART_RK4, GEOM_ANY, false>(const KParams, const int64_t, const SegIn, const SegOut,
-    const int32_t, unsigned long long*, unsigned long long*);
-template __global__ void propagate_kernel<ART_RK4, GEOM_FLAT, false>(const KParams, const int64_t, const SegIn, const SegOut,
-    const int32_t, unsigned long long*, unsigned long long*);
-template __global__ void propagate_kernel<ART_VERN6, GEOM_ANY, true>(const KParams, const int64_t, const SegIn, const SegOut,
-    const int32_t, unsigned long long*, unsigned long long*);
-template __global__ void propagate_kernel<ART_VERN6, GEOM_FLAT, true>(const KParams, const int64_t, const SegIn, const SegOut,
-    const int32_t, unsigned long long*, unsigned long long*);
-template __global__ void propagate_kernel<ART_VERN6, GEOM_GR, true>(const KParams, const int64_t, const SegIn, const SegOut,
-    const int32_t, unsigned long long*, unsigned long long*);
-template __global__ void propagate_kernel<ART_RK4, GEOM_ANY, true>(const KParams, const int64_t, const SegIn, const SegOut,
-    const int32_t, unsigned long long*, unsigned long long*);
 
 }  // namespace art

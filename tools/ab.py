@@ -6,8 +6,16 @@ import os
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import ctypes  # noqa: E402
 import adiabatic_raytracer_amd as A  # noqa: E402
-from adiabatic_raytracer_amd import Engine  # noqa: E402
+from adiabatic_raytracer_amd import Engine, _lib  # noqa: E402
+
+# older builds under comparison may predate entry points this tree binds: drop those from the
+# signature table here (dev tool only; the product loader stays strict)
+if "ART_LIB" in os.environ:
+    _probe = ctypes.CDLL(os.environ["ART_LIB"])
+    for _name in [k for k in _lib.SIGNATURES if not hasattr(_probe, k)]:
+        del _lib.SIGNATURES[_name]
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 1_000_000
 only = sys.argv[2] if len(sys.argv) > 2 else None  # "flat" or "gr"
