@@ -248,7 +248,7 @@ def main():
         basis_ms = kms if len(streams) == 1 else elapsed * 1e3 / args.steps
         achieved = fpl / (basis_ms * 1e-3) / 1e12
         st = out["status"].cpu().numpy()
-        traffic = None
+        traffic, traffic_src = None, None
         pmc_path = os.path.join(HERE, "profiles", "pmc_summary.json")
         if os.path.exists(pmc_path):
             pm = json.load(open(pmc_path))
@@ -257,6 +257,9 @@ def main():
             sha = hashlib.sha256(open(A._lib.load()._name, "rb").read()).hexdigest()
             if pm.get("workload") == f"{args.config}:{n}" and pm.get("libart_sha256") == sha:
                 traffic = pm.get("hbm_bytes_per_launch")
+                traffic_src = ("stored PMC pass of this libart.so build (profiles/pmc_summary.json, sha "
+                               f"{sha[:12]}, tools/pmc_passes.sh: FETCH_SIZE/WRITE_SIZE in separate passes, "
+                               "calibrated by tools/calib_hbm.hip); not measured in this run")
         ncross = int((out["n_cross"].clamp(max=out["capacity"])).sum().item())
         att = (out["n_accept"] + out["n_reject"]).double()
         q = torch.quantile(att[:min(n, 1 << 24)], torch.tensor([0.5, 0.99, 0.999], dtype=torch.float64,
@@ -285,7 +288,7 @@ def main():
                        "interp_points": params.interp_points, "parallelism": f"rays sharded x{world}",
                        "streams": args.streams, "tail_donation": args.donate},
             "roofline": {"bound": "fp64-valu", "achieved": achieved, "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
-                         "frac": achieved / PEAK_FP64_TFLOPS, "traffic": traffic,
+                         "frac": achieved / PEAK_FP64_TFLOPS, "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": f"propagate_kernel<{'RK4' if args.integrator == 'rk4' else 'Vern6'}>", "kernel_ms": kms,
                          "flops_per_launch": fpl, "flops_per_ray_step": fpl / stats_last["accepted"],
                          "time_basis": "launch duration (HIP events)" if len(streams) == 1
