@@ -160,25 +160,39 @@ struct TrajArgs {
   int32_t* count = nullptr;
 };
 
-int propagate_device_impl(const art_params* p, int64_t n, const double* x0, const double* k0, const double* erg,
-                          const double* dw, const double* ln_t0, const int8_t* species, int32_t max_crossings,
-                          art_segment_out* out, art_crossing_buf* xc, void* stream, const TrajArgs& tr = TrajArgs()) {
+// Argument checks shared by the host and device entry points, before any device call (the
+// host path stages buffers of n elements, so a bad n or a NULL buffer must stop it first).
+// Returns ART_OK with *empty set for n == 0 (nothing to do, nothing written).
+int check_segment_args(const art_params* p, int64_t n, const double* x0, const double* k0, const double* erg,
+                       const double* dw, const double* ln_t0, const int8_t* species, const art_segment_out* out,
+                       const art_crossing_buf* xc, const TrajArgs& tr, bool* empty) {
   int rc = validate(p);
   if (rc) return rc;
   if (n < 0 || n > 2147483647LL) return fail(ART_E_INVALID, "n must be in [0, 2^31)");
   if (!out || !out->x_end || !out->k_end || !out->u7_end || !out->tau_end || !out->status || !out->n_accept || !out->n_reject)
     return fail(ART_E_INVALID, "segment output buffers must be non-NULL");
+  *empty = n == 0;
   if (n == 0) return ART_OK;
   if (!x0 || !k0 || !erg || !dw || !ln_t0 || !species) return fail(ART_E_INVALID, "input buffers must be non-NULL");
-  DeviceCtx* c;
-  if ((rc = current_ctx(&c))) return rc;
-  hipStream_t s = pick(c, stream);
-  const art::KParams K = kparams(*p);
   const int cap = (xc && xc->count) ? xc->capacity : 0;
   if (cap && (cap < 1 || !xc->pos || !xc->k || !xc->t || !xc->dw || !xc->p_nonad))
     return fail(ART_E_INVALID, "crossing buffer incomplete");
   if (tr.ntimes != 0 && (tr.ntimes < 2 || !tr.traj || !tr.t || !tr.count))
     return fail(ART_E_INVALID, "saveat needs ntimes >= 2 and buffers");
+  return ART_OK;
+}
+
+int propagate_device_impl(const art_params* p, int64_t n, const double* x0, const double* k0, const double* erg,
+                          const double* dw, const double* ln_t0, const int8_t* species, int32_t max_crossings,
+                          art_segment_out* out, art_crossing_buf* xc, void* stream, const TrajArgs& tr = TrajArgs()) {
+  bool empty = false;
+  int rc = check_segment_args(p, n, x0, k0, erg, dw, ln_t0, species, out, xc, tr, &empty);
+  if (rc || empty) return rc;
+  DeviceCtx* c;
+  if ((rc = current_ctx(&c))) return rc;
+  hipStream_t s = pick(c, stream);
+  const art::KParams K = kparams(*p);
+  const int cap = (xc && xc->count) ? xc->capacity : 0;
   // this launch's scratch: [queue head + statistics (256 B) | u0: 16n doubles of fresh state
   // (init_kernel -> the integrator) | END_REC n doubles of end records | X_REC cap n doubles of
   // crossing records (the integrator -> finalize_kernel)]
@@ -384,9 +398,9 @@ namespace {
 int propagate_host_impl(const art_params* p, int64_t n, const double* x0, const double* k0, const double* erg,
                         const double* dw, const double* ln_t0, const int8_t* species, int32_t max_crossings,
                         art_segment_out* out, art_crossing_buf* xc, const TrajArgs& htr) {
-  int rc = validate(p);
-  if (rc) return rc;
-  if (n == 0) return ART_OK;
+  bool empty = false;
+  int rc = check_segment_args(p, n, x0, k0, erg, dw, ln_t0, species, out, xc, htr, &empty);
+  if (rc || empty) return rc;
   DeviceCtx* c;
   if ((rc = current_ctx(&c))) return rc;
   const int cap = (xc && xc->count) ? xc->capacity : 0;
@@ -416,12 +430,14 @@ int propagate_host_impl(const art_params* p, int64_t n, const double* x0, const 
   if (cap) {
     int32_t* cnt = (int32_t*)dxc;
     double* xd = (double*)((char*)dxc + cnt_bytes);
+    // slots without a crossing come back as NaN, not as whatever the pooled staging buffer
+    // last held (every dword 0x7FF80000: each double is 0x7FF800007FF80000, a quiet NaN)
+    HIP_OK(hipMemsetD32Async((hipDeviceptr_t)xd, 0x7FF80000, (size_t)cap * nd * 9 * 2, s));
     dxb = art_crossing_buf{cap, cnt, xd, xd + 3 * cap * nd, xd + 6 * cap * nd, xd + 7 * cap * nd, xd + 8 * cap * nd};
     dxbp = &dxb;
   }
   TrajArgs dtr;
   if (htr.ntimes != 0) {
-    if (htr.ntimes < 2 || !htr.traj || !htr.t || !htr.count) return fail(ART_E_INVALID, "saveat needs ntimes >= 2 and buffers");
     void* dt_ = nullptr;
     const size_t nt = (size_t)htr.ntimes * nd;
     if ((rc = pool_get(c, 7, nt * 4 * sizeof(double) + nd * sizeof(int32_t), &dt_))) return rc;
@@ -486,6 +502,7 @@ int art_get_prob_nonad_device(const art_params* p, int64_t nc, const double* pos
   int rc = validate(p);
   if (rc) return rc;
   if (nc == 0) return ART_OK;
+  if (nc < 0 || nc > 2147483647LL) return fail(ART_E_INVALID, "nc must be in [0, 2^31)");
   if (!pos || !kpos || !erg_eff || !out) return fail(ART_E_INVALID, "NULL buffer");
   if (!group_start) n_groups = nc;
   DeviceCtx* c;
@@ -500,8 +517,11 @@ int art_get_prob_nonad_host(const art_params* p, int64_t nc, const double* pos, 
   int rc = validate(p);
   if (rc) return rc;
   if (nc == 0) return ART_OK;
+  if (nc < 0 || nc > 2147483647LL) return fail(ART_E_INVALID, "nc must be in [0, 2^31)");
+  if (!pos || !kpos || !erg_eff || !out) return fail(ART_E_INVALID, "NULL buffer");
   if (!group_start) n_groups = nc;
   if (group_start) {  // groups must tile [0, nc)
+    if (n_groups < 1) return fail(ART_E_INVALID, "n_groups must be >= 1");
     if (group_start[0] != 0 || group_start[n_groups] != nc) return fail(ART_E_INVALID, "group_start must span [0, nc]");
     for (int64_t g = 0; g < n_groups; ++g)
       if (group_start[g + 1] <= group_start[g]) return fail(ART_E_INVALID, "empty or unsorted group");
@@ -582,6 +602,8 @@ int art_sample_conversion_points_host(const art_params* p, double max_r, uint64_
   if (rc) return rc;
   if (n == 0) return ART_OK;
   if (n < 0 || n > 2147483647LL) return fail(ART_E_INVALID, "n must be in [0, 2^31)");
+  if (!(max_r > p->rNS)) return fail(ART_E_INVALID, "max_r must exceed rNS (MainRunner.jl:389-396 quits otherwise)");
+  if (!x || !k_init || !erg_inf || !vifty || !weights || !attempts) return fail(ART_E_INVALID, "NULL buffer");
   DeviceCtx* c;
   if ((rc = current_ctx(&c))) return rc;
   void* d;
@@ -615,7 +637,8 @@ int art_event_weight_host(const art_params* p, double max_r, double rho_dm, doub
   int rc = validate(p);
   if (rc) return rc;
   if (n == 0) return ART_OK;
-  if (n < 0) return fail(ART_E_INVALID, "n must be >= 0");
+  if (n < 0 || n > 2147483647LL) return fail(ART_E_INVALID, "n must be in [0, 2^31)");
+  if (!x || !k_init || !vifty || !out) return fail(ART_E_INVALID, "NULL buffer");
   DeviceCtx* c;
   if ((rc = current_ctx(&c))) return rc;
   void* d;

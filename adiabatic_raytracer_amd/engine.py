@@ -56,12 +56,14 @@ class Engine:
                 "species": torch.ones(n, dtype=torch.int8, device=self.device), "sample": s}
 
     def alloc_out(self, n: int, capacity: int = 1) -> dict:
+        # crossing slots a ray does not fill stay as allocated (include/art.h): NaN here, once
+        nan = lambda m: self.empty(m).fill_(float("nan"))  # noqa: E731
         return {"x_end": self.empty(3 * n), "k_end": self.empty(3 * n), "u7_end": self.empty(n),
                 "tau_end": self.empty(n), "status": self.empty(n, dtype=torch.int32),
                 "n_accept": self.empty(n, dtype=torch.int32), "n_reject": self.empty(n, dtype=torch.int32),
-                "n_cross": self.empty(n, dtype=torch.int32), "xc_pos": self.empty(3 * capacity * n),
-                "xc_k": self.empty(3 * capacity * n), "xc_t": self.empty(capacity * n),
-                "xc_dw": self.empty(capacity * n), "xc_p": self.empty(capacity * n), "capacity": capacity}
+                "n_cross": self.empty(n, dtype=torch.int32), "xc_pos": nan(3 * capacity * n),
+                "xc_k": nan(3 * capacity * n), "xc_t": nan(capacity * n),
+                "xc_dw": nan(capacity * n), "xc_p": nan(capacity * n), "capacity": capacity}
 
     # ---- RT.propagate (RayTracer.jl:171-452), asynchronous on the current stream
     def propagate(self, inp: dict, out: dict | None = None, max_crossings: int = -1, capacity: int = 1) -> dict:

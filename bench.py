@@ -194,10 +194,10 @@ def main():
         args.donate = 16 if args.streams > 1 else 0
     eng.set_tail_donation(args.donate)
     streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(args.streams - 1)]
-    for st_ in streams[1:]:
-        st_.wait_stream(streams[0])  # the sampled inputs
     outs = [eng.alloc_out(n, capacity=1) for _ in streams]
     hists = [torch.zeros(2 * args.nbins, dtype=torch.float64, device=eng.device) for _ in streams]
+    for st_ in streams[1:]:
+        st_.wait_stream(streams[0])  # the sampled inputs and the outputs' initialisation
     out, hist = outs[0], hists[0]
 
     def one_step(i):

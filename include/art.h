@@ -120,7 +120,9 @@ typedef struct art_segment_out {
 } art_segment_out;
 
 /* Resonance crossings (xc..Δωc of RayTracer.jl:325-342), layout [(c*cap + j)*n + i]
- * for component c, crossing j < capacity, ray i. */
+ * for component c, crossing j < capacity, ray i. Slots j >= min(count[i], capacity) hold no
+ * crossing (the reference's arrays simply end there): the *_device entry points leave them
+ * unwritten, the *_host entry points fill them with NaN. */
 typedef struct art_crossing_buf {
   int32_t capacity; /* crossings stored per ray (1 for forward trees)               */
   int32_t* count;   /* n  crossings recorded (> capacity means overflow)            */

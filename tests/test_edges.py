@@ -1,0 +1,136 @@
+"""Edge cases of the drop-in boundary and of the batch.
+
+Without a GPU:
+* argument validation runs before any device call. Out-of-range sizes and missing buffers
+  give ART_E_INVALID with a message. An empty batch (n = 0) is ART_OK and writes nothing.
+
+On the GPU (`-m gpu`):
+* a ray's result does not depend on the batch around it. The same rays in ragged batches
+  (1, 63, 65, 257 rays) and in a shuffled batch of 1000 give bit-identical outputs. That
+  holds for every lane assignment, wave composition and queue order of the persistent
+  integrator. Crossing slots a ray does not fill come back as NaN from the host entry point,
+  never as stale staging memory.
+* crossing-buffer overflow. An all-crossings axion backtrace (MainRunner.jl:588) into
+  capacity 1 reports each ray's full count (> capacity, as include/art.h specifies). It
+  stores the same first crossing and end state as the same batch with capacity 8.
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from conftest import CONFIGS
+
+
+def _bufs(n, cap=1):
+    from adiabatic_raytracer_amd._lib import CrossingBuf, SegmentOut
+    out = {"x_end": np.full(3 * n, 7.0), "k_end": np.full(3 * n, 7.0), "u7_end": np.full(n, 7.0),
+           "tau_end": np.full(n, 7.0), "status": np.full(n, 7, np.int32), "n_accept": np.full(n, 7, np.int32),
+           "n_reject": np.full(n, 7, np.int32), "n_cross": np.full(n, 7, np.int32),
+           "xc_pos": np.full(3 * cap * n, 7.0), "xc_k": np.full(3 * cap * n, 7.0), "xc_t": np.full(cap * n, 7.0),
+           "xc_dw": np.full(cap * n, 7.0), "xc_p": np.full(cap * n, 7.0)}
+    P = lambda a: a.ctypes.data_as(C.c_void_p)  # noqa: E731
+    so = SegmentOut(*[P(out[k]) for k in ("x_end", "k_end", "u7_end", "tau_end", "status", "n_accept", "n_reject")])
+    xb = CrossingBuf(cap, *[P(out[k]) for k in ("n_cross", "xc_pos", "xc_k", "xc_t", "xc_dw", "xc_p")])
+    return out, so, xb
+
+
+def _host_call(n, so, xb, arrays=True):
+    import adiabatic_raytracer_amd as A
+    lib = A.load_library()
+    cp = A.Params(**CONFIGS["flat"]).to_c()
+    m = min(max(n, 1), 16)  # out-of-range n must fail before any buffer is read
+    x = np.ones(3 * m)
+    e = np.ones(m)
+    sp = np.ones(m, np.int8)
+    P = lambda a: a.ctypes.data_as(C.c_void_p) if arrays else None  # noqa: E731
+    return lib, lib.art_propagate_host(C.byref(cp), n, P(x), P(x), P(e), P(e), P(e), P(sp), -1,
+                                       C.byref(so), C.byref(xb))
+
+
+def test_empty_batch_is_ok_and_writes_nothing():
+    out, so, xb = _bufs(1)
+    lib, rc = _host_call(0, so, xb)
+    assert rc == 0
+    assert np.all(out["x_end"] == 7.0) and np.all(out["status"] == 7)
+
+
+@pytest.mark.parametrize("n", [-1, 2**31])
+def test_batch_size_out_of_range(n):
+    out, so, xb = _bufs(1)
+    lib, rc = _host_call(n, so, xb)
+    assert rc == -1 and b"n must be" in lib.art_last_error()
+
+
+def test_missing_buffers_fail_loudly():
+    out, so, xb = _bufs(4)
+    lib, rc = _host_call(4, so, xb, arrays=False)
+    assert rc == -1 and b"non-NULL" in lib.art_last_error()
+    so.x_end = None
+    lib, rc = _host_call(4, so, xb)
+    assert rc == -1 and b"non-NULL" in lib.art_last_error()
+
+
+# ---------------------------------------------------------------------------------------
+KEYS = ("x_end", "k_end", "u7_end", "tau_end", "status", "n_accept", "n_reject", "n_cross", "xc_pos", "xc_k", "xc_t",
+        "xc_dw", "xc_p")
+
+
+def _rows(r, idx, n):
+    """Per-ray outputs of rays idx (numpy SoA layout [component][ray]) as one dict."""
+    out = {}
+    for k in KEYS:
+        a = np.asarray(r[k])
+        m = a.size // n
+        out[k] = a.reshape(m, n)[:, idx]
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg", ["flat", "gr"])
+def test_ray_result_independent_of_batch(cfg, oracle_lib):
+    import adiabatic_raytracer_amd as A
+    p = A.Params(**CONFIGS[cfg])
+    n = 1000
+    s = A.sample_conversion_points(p, n, seed=1769)
+    x, k, e = s["x"].reshape(3, n), s["k_init"].reshape(3, n), s["erg"]
+
+    def run(idx):
+        m = len(idx)
+        r = A.propagate_batch(p, x[:, idx].ravel(), k[:, idx].ravel(), e[idx], -np.ones(m), np.full(m, -30.0),
+                              np.ones(m, np.int8), max_crossings=-1, capacity=1)
+        return r, m
+
+    full, _ = run(np.arange(n))
+    ref = _rows(full, np.arange(n), n)
+    perm = np.random.default_rng(7).permutation(n)
+    batches = [np.arange(1), np.arange(63), np.arange(100, 165), np.arange(500, 757), perm]
+    # slots without a crossing come back as NaN from the host entry point (include/art.h)
+    empty = ref["n_cross"][0] == 0
+    assert empty.any() and np.all(np.isnan(ref["xc_pos"][:, empty])) and np.all(np.isnan(ref["xc_p"][:, empty]))
+    for idx in batches:
+        r, m = run(idx)
+        got = _rows(r, np.arange(m), m)
+        for key in KEYS:
+            want = ref[key][:, idx]
+            assert np.array_equal(got[key], want, equal_nan=True), (cfg, len(idx), key)
+
+
+@pytest.mark.gpu
+def test_crossing_buffer_overflow_reports_count(oracle_lib):
+    import adiabatic_raytracer_amd as A
+    p = A.Params(**CONFIGS["gr"])
+    n = 256
+    s = A.sample_conversion_points(p, n, seed=1769)
+    # the backtrace segment: axion, -k, every crossing recorded (MainRunner.jl:581-588)
+    args = (s["x"], -s["k_init"], s["erg"], -np.ones(n), np.full(n, -30.0), np.zeros(n, np.int8))
+    r1 = A.propagate_batch(p, *args, max_crossings=100000, capacity=1)
+    r8 = A.propagate_batch(p, *args, max_crossings=100000, capacity=8)
+    assert np.array_equal(r1["n_cross"], r8["n_cross"])
+    assert (r1["n_cross"] > 1).any(), "no ray overflowed capacity 1"
+    for key in ("xc_pos", "xc_k"):
+        assert np.array_equal(r1[key].reshape(3, n), r8[key].reshape(3, 8, n)[:, 0, :], equal_nan=True)
+    for key in ("xc_t", "xc_dw", "xc_p"):
+        assert np.array_equal(r1[key], r8[key].reshape(8, n)[0], equal_nan=True)
+    for key in ("x_end", "k_end", "status", "n_accept"):
+        assert np.array_equal(r1[key], r8[key], equal_nan=True)

@@ -93,9 +93,9 @@ def test_configs2_segment_shards_match_single_process(tmp_path):
         lo, hi = int(z["lo"]), int(z["hi"])
         m = hi - lo
         for k in ("u7_end", "tau_end", "status", "n_accept", "n_reject", "n_cross", "xc_p"):
-            assert np.array_equal(z[k], full[k][lo:hi]), k
+            assert np.array_equal(z[k], full[k][lo:hi], equal_nan=True), k  # (NaN: no crossing)
         for k in ("x_end", "k_end", "xc_pos"):
-            assert np.array_equal(z[k].reshape(3, m), full[k].reshape(3, n)[:, lo:hi]), k
+            assert np.array_equal(z[k].reshape(3, m), full[k].reshape(3, n)[:, lo:hi], equal_nan=True), k
     assert h_full[NBINS:].sum() > 0
 
 
