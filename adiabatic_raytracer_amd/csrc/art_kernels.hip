@@ -397,8 +397,10 @@ __device__ inline KParams specialize(const KParams& P) {
 
 // DON: the tail-donation instantiations (SegOut::donate / cont_mode honoured); the others
 // carry none of that code, so a lone pass pays nothing for it
-template <int INTEG, int GEOM, bool SAVE, bool DON>
-__global__ __launch_bounds__(BLOCK, ART_WAVES_PER_SIMD) void propagate_kernel(const KParams P_in, const int64_t n,
+// WPS: waves per SIMD the registers are budgeted for (the default 2; the GR continuation
+// launch, below, uses 1)
+template <int INTEG, int GEOM, bool SAVE, bool DON, int WPS = ART_WAVES_PER_SIMD>
+__global__ __launch_bounds__(BLOCK, WPS) void propagate_kernel(const KParams P_in, const int64_t n,
                                                                               const SegIn in, const SegOut out,
                                                                               const int32_t max_crossings,
                                                                               unsigned long long* __restrict__ queue,
@@ -1909,7 +1911,17 @@ hipError_t launch_propagate(const KParams& P, int64_t n, const SegIn& in, const 
     oc.donate = 0;
     const int64_t maxc = (int64_t)grid * (BLOCK / 64) * out.donate;
     const int cgrid = (int)((maxc + BLOCK - 1) / BLOCK);
-    hipLaunchKernelGGL(fn, dim3(cgrid), dim3(BLOCK), 0, s, P, n, in, oc, max_crossings, queue, stats);
+#ifndef ART_CONT_W2
+    // GR continuations at 1 wave/SIMD: no spills (68 VGPRs spill to scratch at 2), and their
+    // work is the batch's lone long-tail rays, configs[3]'s floor. A/B on the configs[3] bench
+    // line (3 passes in flight): 3.21e8 -> 3.35e8 ray-steps/s, bit-identical. Flat
+    // continuations stay at 2: at 1 their waves take whole SIMDs from the passes still in
+    // flight (1.25e6 rays per GPU -3.5%; profiles/r02h_continuation_w1_ab.txt).
+    const KFn cfn = (sch && !rk4 && out.ntimes < 2) ? propagate_kernel<ART_VERN6, GEOM_GR, false, true, 1> : fn;
+#else
+    const KFn cfn = fn;
+#endif
+    hipLaunchKernelGGL(cfn, dim3(cgrid), dim3(BLOCK), 0, s, P, n, in, oc, max_crossings, queue, stats);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
   if (ev1 && (e = hipEventRecord(ev1, s)) != hipSuccess) return e;
