@@ -1898,8 +1898,20 @@ hipError_t launch_propagate(const KParams& P, int64_t n, const SegIn& in, const 
   const bool flat = P.rs_eff == 0.0 && !(P.bndry_lyr > 0.0) && !P.isotropic;
   const bool sch = P.rs_eff > 0.0 && !(P.bndry_lyr > 0.0) && !P.isotropic;
   const bool rk4 = P.integrator == ART_RK4;
-  const KFn fn = out.donate > 0 ? pick_propagate<true>(out.ntimes >= 2, rk4, flat, sch)
-                                 : pick_propagate<false>(out.ntimes >= 2, rk4, flat, sch);
+  KFn fn = out.donate > 0 ? pick_propagate<true>(out.ntimes >= 2, rk4, flat, sch)
+                           : pick_propagate<false>(out.ntimes >= 2, rk4, flat, sch);
+#ifndef ART_SMALL_W2
+  // A batch that fits one ray per lane of 1 wave per SIMD has no use for the second wave's
+  // registers: it runs the 1-wave/SIMD build, which does not spill (a lone long ray -- the GR
+  // tail, a tree wavefront's last nodes -- waits on no scratch reload)
+  if (out.donate <= 0 && out.ntimes < 2 && !rk4 && (flat || sch)) {
+    int dev = 0, ncu = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    if (n <= (int64_t)ncu * 4 * 64)
+      fn = flat ? propagate_kernel<ART_VERN6, GEOM_FLAT, false, false, 1> : propagate_kernel<ART_VERN6, GEOM_GR, false, false, 1>;
+  }
+#endif
   const int grid = persistent_blocks((const void*)fn, n, BLOCK);
   if (grid_out) *grid_out = grid;
   if (ev0 && (e = hipEventRecord(ev0, s)) != hipSuccess) return e;

@@ -10,6 +10,8 @@ On the GPU (`-m gpu`):
   holds for every lane assignment, wave composition and queue order of the persistent
   integrator. Crossing slots a ray does not fill come back as NaN from the host entry point,
   never as stale staging memory.
+* the 1-wave/SIMD build that batches of at most one ray per lane of 1 wave/SIMD run
+  (launch_propagate) gives the same bits as the 2-wave/SIMD build of larger batches.
 * crossing-buffer overflow. An all-crossings axion backtrace (MainRunner.jl:588) into
   capacity 1 reports each ray's full count (> capacity, as include/art.h specifies). It
   stores the same first crossing and end state as the same batch with capacity 8.
@@ -134,3 +136,24 @@ def test_crossing_buffer_overflow_reports_count(oracle_lib):
         assert np.array_equal(r1[key], r8[key].reshape(8, n)[0], equal_nan=True)
     for key in ("x_end", "k_end", "status", "n_accept"):
         assert np.array_equal(r1[key], r8[key], equal_nan=True)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg", ["flat", "gr"])
+def test_small_batch_build_matches_large_batch_build(cfg):
+    """Rays of a 70000-ray batch (2-wave/SIMD build) against the same rays as a batch of 2000
+    (1-wave/SIMD build, n <= 256 CUs x 4 SIMDs x 64 lanes): bit-identical per ray."""
+    import adiabatic_raytracer_amd as A
+    p = A.Params(**CONFIGS[cfg])
+    n, m = 70000, 2000
+    s = A.sample_conversion_points(p, n, seed=1769)
+    x, k, e = s["x"].reshape(3, n), s["k_init"].reshape(3, n), s["erg"]
+
+    def run(idx):
+        c = len(idx)
+        return A.propagate_batch(p, x[:, idx].ravel(), k[:, idx].ravel(), e[idx], -np.ones(c), np.full(c, -30.0),
+                                 np.ones(c, np.int8), max_crossings=-1, capacity=1)
+    big = _rows(run(np.arange(n)), np.arange(m), n)
+    small = _rows(run(np.arange(m)), np.arange(m), m)
+    for key in KEYS:
+        assert np.array_equal(small[key], big[key], equal_nan=True), (cfg, key)
