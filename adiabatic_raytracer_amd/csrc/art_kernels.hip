@@ -1900,10 +1900,12 @@ hipError_t launch_propagate(const KParams& P, int64_t n, const SegIn& in, const 
   const bool rk4 = P.integrator == ART_RK4;
   KFn fn = out.donate > 0 ? pick_propagate<true>(out.ntimes >= 2, rk4, flat, sch)
                            : pick_propagate<false>(out.ntimes >= 2, rk4, flat, sch);
-#ifndef ART_SMALL_W2
-  // A batch that fits one ray per lane of 1 wave per SIMD has no use for the second wave's
-  // registers: it runs the 1-wave/SIMD build, which does not spill (a lone long ray -- the GR
-  // tail, a tree wavefront's last nodes -- waits on no scratch reload)
+#ifdef ART_SMALL_W1
+  // (dev, off by default) A batch that fits one ray per lane of 1 wave per SIMD runs the
+  // 1-wave/SIMD build, which does not spill: lone GR tail ray -3%, flat -4.5% per attempt,
+  // bit-identical where it ran. Disabled: its flat build fails to launch ("unknown error") on
+  // a 2000-ray batch with crossing capacity 8, where the 2-wave build runs
+  // (profiles/r02j_w1_disabled.txt).
   if (out.donate <= 0 && out.ntimes < 2 && !rk4 && (flat || sch)) {
     int dev = 0, ncu = 0;
     (void)hipGetDevice(&dev);
@@ -1923,12 +1925,11 @@ hipError_t launch_propagate(const KParams& P, int64_t n, const SegIn& in, const 
     oc.donate = 0;
     const int64_t maxc = (int64_t)grid * (BLOCK / 64) * out.donate;
     const int cgrid = (int)((maxc + BLOCK - 1) / BLOCK);
-#ifndef ART_CONT_W2
-    // GR continuations at 1 wave/SIMD: no spills (68 VGPRs spill to scratch at 2), and their
-    // work is the batch's lone long-tail rays, configs[3]'s floor. A/B on the configs[3] bench
-    // line (3 passes in flight): 3.21e8 -> 3.35e8 ray-steps/s, bit-identical. Flat
-    // continuations stay at 2: at 1 their waves take whole SIMDs from the passes still in
-    // flight (1.25e6 rays per GPU -3.5%; profiles/r02h_continuation_w1_ab.txt).
+#ifdef ART_CONT_W1
+    // (dev, off by default) GR continuations at 1 wave/SIMD: no spills (68 VGPRs spill to
+    // scratch at 2). A/B on the configs[3] bench line: 3.21e8 -> 3.35e8 ray-steps/s,
+    // bit-identical (profiles/r02h_continuation_w1_ab.txt). Off with the 1-wave/SIMD small-batch
+    // build, whose flat instantiation failed to launch on one batch shape (profiles/r02j_w1_disabled.txt).
     const KFn cfn = (sch && !rk4 && out.ntimes < 2) ? propagate_kernel<ART_VERN6, GEOM_GR, false, true, 1> : fn;
 #else
     const KFn cfn = fn;

@@ -10,8 +10,10 @@ On the GPU (`-m gpu`):
   holds for every lane assignment, wave composition and queue order of the persistent
   integrator. Crossing slots a ray does not fill come back as NaN from the host entry point,
   never as stale staging memory.
-* the 1-wave/SIMD build that batches of at most one ray per lane of 1 wave/SIMD run
-  (launch_propagate) gives the same bits as the 2-wave/SIMD build of larger batches.
+* a 70000-ray batch and its first 2000 rays as a batch of their own agree bit for bit (with the
+  dev switch ART_SMALL_W1 the small batch runs the 1-wave/SIMD build).
+* crossing capacity 8 on flat photon and axion batches of 2000 rays (the batch shape the
+  1-wave/SIMD build failed to launch) records the same first crossing as capacity 1.
 * crossing-buffer overflow. An all-crossings axion backtrace (MainRunner.jl:588) into
   capacity 1 reports each ray's full count (> capacity, as include/art.h specifies). It
   stores the same first crossing and end state as the same batch with capacity 8.
@@ -141,8 +143,8 @@ def test_crossing_buffer_overflow_reports_count(oracle_lib):
 @pytest.mark.gpu
 @pytest.mark.parametrize("cfg", ["flat", "gr"])
 def test_small_batch_build_matches_large_batch_build(cfg):
-    """Rays of a 70000-ray batch (2-wave/SIMD build) against the same rays as a batch of 2000
-    (1-wave/SIMD build, n <= 256 CUs x 4 SIMDs x 64 lanes): bit-identical per ray."""
+    """Rays of a 70000-ray batch against the same rays as a batch of 2000: bit-identical per ray
+    (with ART_SMALL_W1 the second runs the 1-wave/SIMD build)."""
     import adiabatic_raytracer_amd as A
     p = A.Params(**CONFIGS[cfg])
     n, m = 70000, 2000
@@ -157,3 +159,23 @@ def test_small_batch_build_matches_large_batch_build(cfg):
     small = _rows(run(np.arange(m)), np.arange(m), m)
     for key in KEYS:
         assert np.array_equal(small[key], big[key], equal_nan=True), (cfg, key)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("species", [1, 0])
+def test_flat_capacity_8(species):
+    """Flat batches of 2000 photons (first crossing) or backtrace axions (every crossing) with
+    crossing capacity 8: the first crossing slot and the end states equal capacity 1's."""
+    import adiabatic_raytracer_amd as A
+    from dataclasses import replace
+    p = A.Params(**CONFIGS["flat"])
+    n = 2000
+    s = A.sample_conversion_points(p, n, seed=1769)
+    q, k, mc = (p, s["k_init"], -1) if species == 1 else (replace(p, B0=-p.B0), -s["k_init"], 100000)
+    args = (s["x"], k, s["erg"], -np.ones(n), np.full(n, -30.0), np.full(n, species, np.int8))
+    r1 = A.propagate_batch(q, *args, max_crossings=mc, capacity=1)
+    r8 = A.propagate_batch(q, *args, max_crossings=mc, capacity=8)
+    for key in ("x_end", "k_end", "status", "n_accept", "n_cross"):
+        assert np.array_equal(r1[key], r8[key], equal_nan=True), key
+    assert np.array_equal(r1["xc_pos"].reshape(3, n), r8["xc_pos"].reshape(3, 8, n)[:, 0, :], equal_nan=True)
+    assert np.array_equal(r1["xc_p"], r8["xc_p"].reshape(8, n)[0], equal_nan=True)
