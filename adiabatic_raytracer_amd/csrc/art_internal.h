@@ -49,7 +49,7 @@ constexpr int X_REC = 8;
 constexpr int CONT_REC = 24;  // [u (7) | f (7) | τ, dt, qpow, cprev, bstart, erg | int4 {ray, n_acc, n_rej, ncross} | int4 {iter, sprev, flags, save_k}]
 constexpr int N_STATS = 8;  // propagate statistics: attempts, accepted, root re-steps, scan evals,
                             // interpolant-root evals, rays, init RHS, (reserved)
-int persistent_blocks(const void* func, int64_t work, int block);
+int persistent_blocks(const void* func, int64_t work, int block, int fallback_per_cu);
 // propagate = init (u0 of every ray) -> the persistent integrator -> finalize (Cartesian
 // end state, conversion probability at the crossings); ev0/ev1 (may be null) bracket the
 // integrator kernel alone.

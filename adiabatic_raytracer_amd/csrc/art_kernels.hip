@@ -13,6 +13,9 @@
 //     state and its crossings (Σ ≈ 220 B per segment).
 #include <hip/hip_runtime.h>
 
+#include <cstdio>
+#include <cstdlib>
+
 #include "art_core.h"
 #include "art_event.h"
 #include "art_internal.h"
@@ -1861,11 +1864,45 @@ __global__ __launch_bounds__(256) void event_weight_kernel(const KParams P, cons
 
 // ---------------------------------------------------------------------------
 // host-side launch wrappers (art_internal.h)
-int persistent_blocks(const void* func, int64_t work, int block) {
+// Resident blocks of `func` per CU from its own resource use: the unified 512-entry VGPR file
+// of a CDNA SIMD (arch VGPRs + AGPRs, granule 8), 8 waves per SIMD at most, and the 160 KB of
+// LDS per CU.
+static int blocks_per_cu_from_attributes(const void* func, int block, int fallback) {
+  hipFuncAttributes a{};
+  if (hipFuncGetAttributes(&a, func) != hipSuccess) {
+    (void)hipGetLastError();
+    return fallback;
+  }
+  const int regs = a.numRegs > 0 ? ((a.numRegs + 7) / 8) * 8 : 8;
+  int wps = 512 / regs;
+  wps = wps > 8 ? 8 : wps;
+  const int waves = (block + 63) / 64;
+  int per_cu = (4 * wps) / waves;
+  if (a.sharedSizeBytes > 0) {
+    const int by_lds = (int)(163840 / a.sharedSizeBytes);
+    per_cu = per_cu < by_lds ? per_cu : by_lds;
+  }
+  return per_cu < 1 ? 1 : per_cu;
+}
+
+int persistent_blocks(const void* func, int64_t work, int block, int fallback_per_cu) {
   int dev = 0, ncu = 0, per_cu = 0;
   (void)hipGetDevice(&dev);
   (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, func, block, 0) != hipSuccess || per_cu < 1) per_cu = 1;
+  const hipError_t oe = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, func, block, 0);
+#ifdef ART_LAUNCH_DEBUG
+  fprintf(stderr, "[art-debug] occupancy rc=%d (%s) per_cu=%d ncu=%d\n", (int)oe, hipGetErrorString(oe), per_cu, ncu);
+#endif
+  if (oe != hipSuccess || per_cu < 1) {
+    // The runtime's occupancy calculator returns hipErrorUnknown (and 0 blocks) for the
+    // 1-wave/SIMD flat integrator (270 unified VGPRs: 256 arch + 14 AGPRs), a kernel that
+    // launches and runs correctly. That error stays the thread's last error, and the
+    // hipGetLastError() after the next launch then reported the launch as failed (round 2's
+    // "unknown error" on a 2000-ray flat batch, profiles/r03a_w1_launch_debug.txt). Clear it
+    // and size the grid from the kernel's own resource use instead.
+    (void)hipGetLastError();
+    per_cu = blocks_per_cu_from_attributes(func, block, fallback_per_cu);
+  }
   const int64_t need = (work + block - 1) / block;
   const int64_t full = (int64_t)ncu * per_cu;
   return (int)(need < full ? need : full);
@@ -1887,12 +1924,35 @@ static KFn pick_propagate(bool save, bool rk4, bool flat, bool sch) {
                             : propagate_kernel<ART_VERN6, GEOM_ANY, false, DON>));
 }
 
+// The 1-wave/SIMD instantiations (small batches, GR continuations) are on unless ART_W1=0.
+static bool w1_builds() {
+  static const bool on = [] {
+    const char* e = std::getenv("ART_W1");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 hipError_t launch_propagate(const KParams& P, int64_t n, const SegIn& in, const SegOut& out, int32_t max_crossings,
                             unsigned long long* queue, unsigned long long* stats, hipStream_t s, int* grid_out,
                             hipEvent_t ev0, hipEvent_t ev1) {
   const int64_t gr = (n + 255) / 256;
   const unsigned g1 = (unsigned)((n + 255) / 256);
+#ifdef ART_LAUNCH_DEBUG
+  // dev: every launch synchronised and checked on its own, errors named by stage
+#define ART_DBG(stage)                                                                                       \
+  {                                                                                                          \
+    const hipError_t le_ = hipGetLastError();                                                                \
+    const hipError_t se_ = hipStreamSynchronize(s);                                                          \
+    fprintf(stderr, "[art-debug] %s: last=%d (%s) sync=%d (%s)\n", stage, (int)le_, hipGetErrorString(le_), \
+            (int)se_, hipGetErrorString(se_));                                                               \
+  }
+  ART_DBG("entry")
+#else
+#define ART_DBG(stage)
+#endif
   hipLaunchKernelGGL(init_kernel, dim3((unsigned)(gr < 2048 ? gr : 2048)), dim3(256), 0, s, P, n, in, stats);
+  ART_DBG("init_kernel")
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   const bool flat = P.rs_eff == 0.0 && !(P.bndry_lyr > 0.0) && !P.isotropic;
@@ -1900,24 +1960,26 @@ hipError_t launch_propagate(const KParams& P, int64_t n, const SegIn& in, const 
   const bool rk4 = P.integrator == ART_RK4;
   KFn fn = out.donate > 0 ? pick_propagate<true>(out.ntimes >= 2, rk4, flat, sch)
                            : pick_propagate<false>(out.ntimes >= 2, rk4, flat, sch);
-#ifdef ART_SMALL_W1
-  // (dev, off by default) A batch that fits one ray per lane of 1 wave per SIMD runs the
-  // 1-wave/SIMD build, which does not spill: lone GR tail ray -3%, flat -4.5% per attempt,
-  // bit-identical where it ran. Disabled: its flat build fails to launch ("unknown error") on
-  // a 2000-ray batch with crossing capacity 8, where the 2-wave build runs
-  // (profiles/r02j_w1_disabled.txt).
-  if (out.donate <= 0 && out.ntimes < 2 && !rk4 && (flat || sch)) {
+  // A batch that fits one ray per lane of 1 wave per SIMD runs the 1-wave/SIMD build, which
+  // does not spill: lone GR tail ray -3%, flat -4.5% per attempt, bit-identical
+  // (profiles/r02j_small_batch_w1_ab.txt, tests/test_edges.py). ART_W1=0 switches it off (A/B).
+  bool w1 = false;
+  if (w1_builds() && out.donate <= 0 && out.ntimes < 2 && !rk4 && (flat || sch)) {
     int dev = 0, ncu = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-    if (n <= (int64_t)ncu * 4 * 64)
+    if (n <= (int64_t)ncu * 4 * 64) {
       fn = flat ? propagate_kernel<ART_VERN6, GEOM_FLAT, false, false, 1> : propagate_kernel<ART_VERN6, GEOM_GR, false, false, 1>;
+      w1 = true;
+    }
   }
-#endif
-  const int grid = persistent_blocks((const void*)fn, n, BLOCK);
+  // (the integrator's blocks per CU by design: its waves per SIMD, 4 waves a block)
+  const int grid = persistent_blocks((const void*)fn, n, BLOCK, w1 ? 1 : ART_WAVES_PER_SIMD * 4 / (BLOCK / 64));
+  ART_DBG("persistent_blocks")
   if (grid_out) *grid_out = grid;
   if (ev0 && (e = hipEventRecord(ev0, s)) != hipSuccess) return e;
   hipLaunchKernelGGL(fn, dim3(grid), dim3(BLOCK), 0, s, P, n, in, out, max_crossings, queue, stats);
+  ART_DBG("propagate_kernel")
   if ((e = hipGetLastError()) != hipSuccess) return e;
   if (out.donate > 0) {  // the donated tail rays, packed into full waves (at most waves x donate of them)
     SegOut oc = out;
@@ -1925,27 +1987,24 @@ hipError_t launch_propagate(const KParams& P, int64_t n, const SegIn& in, const 
     oc.donate = 0;
     const int64_t maxc = (int64_t)grid * (BLOCK / 64) * out.donate;
     const int cgrid = (int)((maxc + BLOCK - 1) / BLOCK);
-#ifdef ART_CONT_W1
-    // (dev, off by default) GR continuations at 1 wave/SIMD: no spills (68 VGPRs spill to
-    // scratch at 2). A/B on the configs[3] bench line: 3.21e8 -> 3.35e8 ray-steps/s,
-    // bit-identical (profiles/r02h_continuation_w1_ab.txt). Off with the 1-wave/SIMD small-batch
-    // build, whose flat instantiation failed to launch on one batch shape (profiles/r02j_w1_disabled.txt).
-    const KFn cfn = (sch && !rk4 && out.ntimes < 2) ? propagate_kernel<ART_VERN6, GEOM_GR, false, true, 1> : fn;
-#else
-    const KFn cfn = fn;
-#endif
+    // GR continuations at 1 wave/SIMD: no spills (68 VGPRs spill to scratch at 2). A/B on the
+    // configs[3] bench line: 3.21e8 -> 3.35e8 ray-steps/s, bit-identical
+    // (profiles/r02h_continuation_w1_ab.txt); flat stays at 2 (measured -3.5% at 1).
+    const KFn cfn = (w1_builds() && sch && !rk4 && out.ntimes < 2) ? propagate_kernel<ART_VERN6, GEOM_GR, false, true, 1> : fn;
     hipLaunchKernelGGL(cfn, dim3(cgrid), dim3(BLOCK), 0, s, P, n, in, oc, max_crossings, queue, stats);
+    ART_DBG("continuation")
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
   if (ev1 && (e = hipEventRecord(ev1, s)) != hipSuccess) return e;
   hipLaunchKernelGGL(finalize_kernel, dim3(g1), dim3(256), 0, s, P, n, in, out);
+  ART_DBG("finalize_kernel")
   return hipGetLastError();
 }
 
 hipError_t launch_sample(const KParams& P, double maxR, uint64_t seed, int64_t ray_offset, int64_t n, double* x,
                          double* k, double* erg, double* vifty, int32_t* w, int32_t* att, unsigned long long* queue,
                          hipStream_t s) {
-  const int grid = persistent_blocks((const void*)sample_kernel, n, 256);
+  const int grid = persistent_blocks((const void*)sample_kernel, n, 256, 1);
   hipLaunchKernelGGL(sample_kernel, dim3(grid), dim3(256), 0, s, P, maxR, seed, ray_offset, n, x, k, erg, vifty, w, att,
                      queue);
   return hipGetLastError();

@@ -122,7 +122,10 @@ def run_points(kws: list[dict], rays: int, seed: int = 1769, nbins: int = 50, de
     k = len(order)
     ms = (C.c_double * max(1, k))()
     got = A._lib.load().art_recent_kernel_ms(k, ms)
-    kms = dict(zip(order, list(ms)[:max(0, got)]))  # the ring holds launch order
+    # the ring holds the device's last min(k, 64) propagate launches, oldest first: they are the
+    # last `got` points of the dispatch order only when all k were recorded (got == k); past the
+    # ring's 64 entries the durations are not attributed at all rather than to the wrong points
+    kms = dict(zip(order[-got:], list(ms)[:got])) if got == k else {}
     acc_total = 0
     for i in live:
         o = outs[i]

@@ -244,7 +244,10 @@ def main_runner_tree(params: Params, Ntajs: int, *, seed=1769, ntimes=1000, rho_
                           elapsed=time.perf_counter() - t_start, ev_offset=lo)
     # the run's totals: [flux (2 nbins, weight * sln_prob before the f_inx division) | f_inx |
     # Σ weight * sln_prob (axions, photons) | rows], ONE sum over the ranks
-    flux = radiated_flux(rows[:, 3], rows[:, 1], rows[:, 8] * rows[:, 7], nbins) if len(rows) else np.zeros(2 * nbins)
+    # the binned flux (a GPU histogram) only when someone reads it: the reduced run_info, or the
+    # other ranks' sum (every rank must contribute its part); f_inx alone normalises column 8
+    want_flux = len(rows) and (world > 1 or run_info is not None)
+    flux = radiated_flux(rows[:, 3], rows[:, 1], rows[:, 8] * rows[:, 7], nbins) if want_flux else np.zeros(2 * nbins)
     pps = rows[:, 8] * rows[:, 7] if len(rows) else np.zeros(0)
     tot = np.concatenate([flux, [float(f_inx), float(pps[rows[:, 1] == 0].sum()) if len(rows) else 0.0,
                                  float(pps[rows[:, 1] == 1].sum()) if len(rows) else 0.0, float(len(rows))]])

@@ -10,10 +10,13 @@ On the GPU (`-m gpu`):
   holds for every lane assignment, wave composition and queue order of the persistent
   integrator. Crossing slots a ray does not fill come back as NaN from the host entry point,
   never as stale staging memory.
-* a 70000-ray batch and its first 2000 rays as a batch of their own agree bit for bit (with the
-  dev switch ART_SMALL_W1 the small batch runs the 1-wave/SIMD build).
-* crossing capacity 8 on flat photon and axion batches of 2000 rays (the batch shape the
-  1-wave/SIMD build failed to launch) records the same first crossing as capacity 1.
+* a 70000-ray batch and its first 2000 rays as a batch of their own agree bit for bit (the
+  small batch runs the 1-wave/SIMD build, the large one the 2-wave build).
+* crossing capacity 8 on flat photon and axion batches of 2000 rays (the batch shape whose
+  1-wave/SIMD launch round 2 reported as failed) records the same first crossing as
+  capacity 1, also as the first propagate launch of a fresh process (the reproducer of that
+  report): the runtime's occupancy query fails for that kernel, and its error must not be
+  taken for a launch failure.
 * crossing-buffer overflow. An all-crossings axion backtrace (MainRunner.jl:588) into
   capacity 1 reports each ray's full count (> capacity, as include/art.h specifies). It
   stores the same first crossing and end state as the same batch with capacity 8.
@@ -144,7 +147,7 @@ def test_crossing_buffer_overflow_reports_count(oracle_lib):
 @pytest.mark.parametrize("cfg", ["flat", "gr"])
 def test_small_batch_build_matches_large_batch_build(cfg):
     """Rays of a 70000-ray batch against the same rays as a batch of 2000: bit-identical per ray
-    (with ART_SMALL_W1 the second runs the 1-wave/SIMD build)."""
+    (the second runs the 1-wave/SIMD build)."""
     import adiabatic_raytracer_amd as A
     p = A.Params(**CONFIGS[cfg])
     n, m = 70000, 2000
@@ -179,3 +182,39 @@ def test_flat_capacity_8(species):
         assert np.array_equal(r1[key], r8[key], equal_nan=True), key
     assert np.array_equal(r1["xc_pos"].reshape(3, n), r8["xc_pos"].reshape(3, 8, n)[:, 0, :], equal_nan=True)
     assert np.array_equal(r1["xc_p"], r8["xc_p"].reshape(8, n)[0], equal_nan=True)
+
+
+_FRESH = r"""
+import json, sys
+import numpy as np
+from dataclasses import replace
+sys.path.insert(0, sys.argv[1])
+import adiabatic_raytracer_amd as A
+p = A.Params(theta_m=0.2, mass_a=1e-5, flat=True)
+n = 2000
+s = A.sample_conversion_points(p, n, seed=1769)
+out = {}
+for species in (1, 0):
+    q, k, mc = (p, s["k_init"], -1) if species == 1 else (replace(p, B0=-p.B0), -s["k_init"], 100000)
+    r = A.propagate_batch(q, s["x"], k, s["erg"], -np.ones(n), np.full(n, -30.0), np.full(n, species, np.int8),
+                          max_crossings=mc, capacity=8)
+    out[species] = [int(r["n_accept"].sum()), int(r["n_cross"].sum()), r["stats"]["grid"]]
+print(json.dumps(out))
+"""
+
+
+@pytest.mark.gpu
+def test_small_batch_w1_first_launch_in_fresh_process():
+    """Round 2's reproducer (tools/exp_axn_case.py flat 1 2000 8): a fresh process samples 2000
+    flat roots and runs them, first as photons then as backtrace axions, with crossing capacity
+    8 on the 1-wave/SIMD build. Both launches succeed, on the 1-wave grid (one block per CU)."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", _FRESH, root], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    for species, (acc, ncross, grid) in out.items():
+        assert acc > 0 and grid == 8, (species, acc, ncross, grid)  # 2000 rays: 8 blocks of 256

@@ -53,3 +53,48 @@ def test_tail_donation_rejects_bad_lane_counts():
     for bad in (-1, 64):
         with pytest.raises(A.ArtError):
             eng.set_tail_donation(bad)
+
+
+def _host_run(p, args, lanes, **kw):
+    import adiabatic_raytracer_amd as A
+    lib = A._lib.load()
+    A._lib.check(lib.art_set_tail_donation(lanes))
+    try:
+        return A.propagate_batch(p, *args, **kw)
+    finally:
+        A._lib.check(lib.art_set_tail_donation(0))
+
+
+@pytest.mark.parametrize("cfg", ["flat", "gr"])
+@pytest.mark.parametrize("mode", ["backtrace", "saveat"])
+def test_tail_donation_round_trips_crossings_and_saved_points(cfg, mode):
+    """The donation record carries the post-event state (condition memory, sign, the
+    just-evented flag), the crossing count and the next saveat index. Round trips through it
+    with several crossings per ray -- the all-crossings axion backtrace (max_crossings 100000,
+    capacity 8, -k and -B0 as MainRunner.jl:581-591) -- and with saved points (ntimes 3 and 7,
+    RayTracer.jl:176,383) leave every output bit-identical (host entry points, which honour the
+    device's donation setting like every launch)."""
+    from dataclasses import replace
+    import adiabatic_raytracer_amd as A
+    p = A.Params(**CONFIGS[cfg])
+    n = 4000
+    s = A.sample_conversion_points(p, n, seed=1769)
+    if mode == "backtrace":
+        q = replace(p, B0=-p.B0)
+        args = (s["x"], -s["k_init"], s["erg"], -np.ones(n), np.full(n, -30.0), np.zeros(n, np.int8))
+        kws = [dict(max_crossings=100000, capacity=8)]
+    else:
+        q = p
+        args = (s["x"], s["k_init"], s["erg"], -np.ones(n), np.full(n, -30.0), np.ones(n, np.int8))
+        kws = [dict(max_crossings=-1, capacity=1, ntimes=3), dict(max_crossings=-1, capacity=1, ntimes=7)]
+    for kw in kws:
+        ref = _host_run(q, args, 0, **kw)
+        if mode == "backtrace":
+            assert (ref["n_cross"] > 1).any()
+        for lanes in (16, 63):
+            got = _host_run(q, args, lanes, **kw)
+            for k, v in ref.items():
+                if isinstance(v, np.ndarray):
+                    assert np.array_equal(v, got[k], equal_nan=True), (cfg, mode, kw, lanes, k)
+            for k in ("attempts", "accepted", "root_steps", "scan_evals", "rays", "cert_steps"):
+                assert ref["stats"][k] == got["stats"][k], (cfg, mode, lanes, k)
