@@ -7,12 +7,17 @@
 
 #include <dlfcn.h>
 
+#include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <cmath>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/art.h"
@@ -49,6 +54,11 @@ struct DeviceCtx {
   int32_t donate = 0;            // tail donation (art_set_tail_donation): lanes per wave, 0 = off
   std::vector<std::pair<void*, size_t>> pool;  // host-entry staging buffers (grow-only, used under g_mu by the
                                                // synchronous *_host calls only)
+  // the chunked host pipeline of art_propagate_host (propagate_host_chunked): its extra
+  // streams, and per pipeline slot a pinned input and output staging buffer (grow-only)
+  std::vector<hipStream_t> pstreams;
+  std::vector<std::pair<void*, size_t>> pinned;
+  std::vector<hipEvent_t> pdone;
 };
 std::vector<DeviceCtx> g_ctx;
 
@@ -118,6 +128,101 @@ int pool_get(DeviceCtx* c, size_t slot, size_t bytes, void** p) {
   return ART_OK;
 }
 
+int pinned_get(DeviceCtx* c, size_t slot, size_t bytes, void** p) {
+  if (c->pinned.size() <= slot) c->pinned.resize(slot + 1, {nullptr, 0});
+  auto& e = c->pinned[slot];
+  if (e.second < bytes) {
+    if (e.first) HIP_OK(hipHostFree(e.first));
+    e.first = nullptr;
+    e.second = 0;
+    if (hipHostMalloc(&e.first, bytes, hipHostMallocDefault) != hipSuccess)
+      return fail(ART_E_NOMEM, "hipHostMalloc of %s bytes failed", std::to_string(bytes).c_str());
+    e.second = bytes;
+  }
+  *p = e.first;
+  return ART_OK;
+}
+
+// Host-side copies of the chunked host pipeline (caller arrays <-> pinned staging): a few
+// persistent worker threads share each batch of row segments, so gathering one chunk's inputs
+// and scattering another's outputs runs at the host's memory bandwidth, not one core's.
+class CopyPool {
+ public:
+  struct Seg {
+    void* dst;
+    const void* src;
+    size_t bytes;
+  };
+  explicit CopyPool(int nthreads) {
+    for (int i = 0; i < nthreads; ++i) th_.emplace_back([this] { loop(); });
+  }
+  ~CopyPool() {
+    {
+      std::lock_guard<std::mutex> lk(m_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : th_) t.join();
+  }
+  // copies every segment; pieces of at most 1 MiB are shared by the workers and the caller
+  void run(const std::vector<Seg>& segs) {
+    pieces_.clear();
+    for (const Seg& g : segs)
+      for (size_t o = 0; o < g.bytes; o += PIECE)
+        pieces_.push_back({(char*)g.dst + o, (const char*)g.src + o, std::min(PIECE, g.bytes - o)});
+    if (pieces_.empty()) return;
+    next_.store(0);
+    {
+      std::lock_guard<std::mutex> lk(m_);
+      busy_ = (int)th_.size();
+      ++gen_;
+    }
+    cv_.notify_all();
+    work();
+    std::unique_lock<std::mutex> lk(m_);
+    done_.wait(lk, [this] { return busy_ == 0; });
+  }
+
+ private:
+  static constexpr size_t PIECE = size_t(1) << 20;
+  void work() {
+    for (size_t i; (i = next_.fetch_add(1)) < pieces_.size();) std::memcpy(pieces_[i].dst, pieces_[i].src, pieces_[i].bytes);
+  }
+  void loop() {
+    unsigned long long seen = 0;
+    for (;;) {
+      {
+        std::unique_lock<std::mutex> lk(m_);
+        cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+        if (stop_) return;
+        seen = gen_;
+      }
+      work();
+      std::lock_guard<std::mutex> lk(m_);
+      if (--busy_ == 0) done_.notify_all();
+    }
+  }
+  std::vector<std::thread> th_;
+  std::vector<Seg> pieces_;
+  std::atomic<size_t> next_{0};
+  std::mutex m_;
+  std::condition_variable cv_, done_;
+  unsigned long long gen_ = 0;
+  int busy_ = 0;
+  bool stop_ = false;
+};
+
+int env_int(const char* name, int dflt) {
+  const char* e = std::getenv(name);
+  return (e && *e) ? std::atoi(e) : dflt;
+}
+
+CopyPool& copy_pool() {
+  // ART_HOST_THREADS: worker threads besides the caller (default 7)
+  static CopyPool pool(std::max(0, env_int("ART_HOST_THREADS", 7)));
+  return pool;
+}
+
 // Device scratch of ONE launch, allocated and freed in the order of its stream (hipMallocAsync /
 // hipFreeAsync), so concurrent launches never share a work-queue word or a state buffer.
 int scratch_alloc(hipStream_t s, size_t bytes, void** p) {
@@ -184,7 +289,8 @@ int check_segment_args(const art_params* p, int64_t n, const double* x0, const d
 
 int propagate_device_impl(const art_params* p, int64_t n, const double* x0, const double* k0, const double* erg,
                           const double* dw, const double* ln_t0, const int8_t* species, int32_t max_crossings,
-                          art_segment_out* out, art_crossing_buf* xc, void* stream, const TrajArgs& tr = TrajArgs()) {
+                          art_segment_out* out, art_crossing_buf* xc, void* stream, const TrajArgs& tr = TrajArgs(),
+                          int donate_override = -1) {
   bool empty = false;
   int rc = check_segment_args(p, n, x0, k0, erg, dw, ln_t0, species, out, xc, tr, &empty);
   if (rc || empty) return rc;
@@ -201,10 +307,11 @@ int propagate_device_impl(const art_params* p, int64_t n, const double* x0, cons
   const size_t xrb = (size_t)cap * nd * art::X_REC * sizeof(double);
   // tail donation: at most (resident waves) x donate records of CONT_REC doubles
   size_t ncont = 0;
-  if (c->donate > 0) {
+  const int32_t donate = donate_override >= 0 ? donate_override : c->donate;
+  if (donate > 0) {
     int ncu = 0;
     HIP_OK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device));
-    ncont = std::min(nd, (size_t)ncu * 32 * (size_t)c->donate);
+    ncont = std::min(nd, (size_t)ncu * 32 * (size_t)donate);
   }
   const size_t contb = ncont * art::CONT_REC * sizeof(double);
   LaunchRec* L;
@@ -234,7 +341,7 @@ int propagate_device_impl(const art_params* p, int64_t n, const double* x0, cons
     so.cont = (double*)((char*)blk + head + u0b + recb + xrb);
     so.cont_count = words + 16;  // head words 16 and 17 (zeroed with the head)
     so.cont_queue = words + 17;
-    so.donate = c->donate;
+    so.donate = donate;
   }
   HIP_OK(hipMemsetAsync(words, 0, head, s));
   HIP_OK(art::launch_propagate(K, n, in, so, max_crossings, words, words + 1, s, &L->grid, L->ev0, L->ev1));
@@ -258,6 +365,27 @@ int finish_timing(DeviceCtx* c) {
   g_last_ms = ms;
   g_last_grid = L.grid;
   for (int i = 0; i < art::N_STATS; ++i) g_last_stats[i] = L.host_stats[i];
+  return ART_OK;
+}
+
+// Latch several propagate launches (the chunks of one host call) as one: their integrator
+// kernels' summed durations and summed statistics.
+int finish_timing_sum(DeviceCtx* c, const std::vector<int>& slots) {
+  double ms_sum = 0.0;
+  unsigned long long st[art::N_STATS] = {0};
+  int grid = 0;
+  for (int i : slots) {
+    LaunchRec& L = c->ring[i];
+    HIP_OK(hipEventSynchronize(L.done));
+    float ms = 0.f;
+    HIP_OK(hipEventElapsedTime(&ms, L.ev0, L.ev1));
+    ms_sum += ms;
+    for (int k = 0; k < art::N_STATS; ++k) st[k] += L.host_stats[k];
+    grid = std::max(grid, L.grid);
+  }
+  g_last_ms = ms_sum;
+  g_last_grid = grid;
+  for (int k = 0; k < art::N_STATS; ++k) g_last_stats[k] = st[k];
   return ART_OK;
 }
 
@@ -395,6 +523,141 @@ int art_propagate_traj_device(const art_params* p, int64_t n, const double* x0, 
 }  // extern "C"
 
 namespace {
+// art_propagate_host for large batches: a pipeline of chunks (the reference call
+// site MainRunner.jl:179-190 hands over host arrays). Chunk k's inputs are gathered from the
+// caller's arrays into pinned staging by the copy pool, copied to HBM, propagated (with tail
+// donation: up to `slots` chunks run concurrently on their own streams, so one chunk's drain
+// tail is filled by the next), and its outputs come back to pinned staging and are scattered
+// into the caller's arrays -- while the chunks after it compute. Per-ray results do not
+// depend on the batch split (tests/test_edges.py), so the outputs equal the single launch's
+// bit for bit. The statistics and kernel time of the call are the sums over its chunks.
+int propagate_host_chunked(DeviceCtx* c, const art_params* p, int64_t n, const double* x0, const double* k0,
+                           const double* erg, const double* dw, const double* ln_t0, const int8_t* species,
+                           int32_t max_crossings, art_segment_out* out, art_crossing_buf* xc, int nchunks,
+                           int nslots) {
+  const int cap = (xc && xc->count) ? xc->capacity : 0;
+  const int64_t K = nchunks;
+  const int64_t m_max = (n + K - 1) / K;
+  auto up = [](size_t b) { return (b + 255) & ~size_t(255); };
+  // blob layouts of a chunk of m rays (identical in pinned staging and in HBM)
+  auto in_bytes = [&](int64_t m) { return up((size_t)m * 9 * sizeof(double)) + up((size_t)m); };
+  auto cnt_off = [&](int64_t m) { return up((size_t)m * 8 * sizeof(double) + (size_t)m * 3 * sizeof(int32_t)); };
+  auto xd_off = [&](int64_t m) { return cnt_off(m) + up((size_t)m * sizeof(int32_t)); };
+  auto out_bytes = [&](int64_t m) { return cap ? xd_off(m) + (size_t)cap * m * 9 * sizeof(double) : cnt_off(m); };
+  while ((int)c->pstreams.size() < nslots) {
+    hipStream_t st = c->stream;
+    if (!c->pstreams.empty()) HIP_OK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    c->pstreams.push_back(st);
+    hipEvent_t ev;
+    HIP_OK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    c->pdone.push_back(ev);
+  }
+  std::vector<char*> pin_in(nslots), pin_out(nslots), dev_in(nslots), dev_out(nslots);
+  int rc;
+  for (int s = 0; s < nslots; ++s) {
+    void *a, *b, *d1, *d2;
+    if ((rc = pinned_get(c, 2 * s, in_bytes(m_max), &a)) || (rc = pinned_get(c, 2 * s + 1, out_bytes(m_max), &b)) ||
+        (rc = pool_get(c, 16 + 2 * s, in_bytes(m_max), &d1)) || (rc = pool_get(c, 17 + 2 * s, out_bytes(m_max), &d2)))
+      return rc;
+    pin_in[s] = (char*)a; pin_out[s] = (char*)b; dev_in[s] = (char*)d1; dev_out[s] = (char*)d2;
+  }
+  using Seg = CopyPool::Seg;
+  std::vector<int64_t> slot_lo(nslots, -1), slot_m(nslots, 0);
+  std::vector<int> rings;
+  // ART_HOST_TRACE=1: the host side of every chunk to stderr (waits, gathers, scatters)
+  const bool trace = env_int("ART_HOST_TRACE", 0) != 0;
+  auto clk = [] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
+  const double t_start = clk();
+  // the outputs of the chunk in slot s: pinned staging -> the caller's arrays
+  auto drain = [&](int s) -> int {
+    if (slot_lo[s] < 0) return ART_OK;
+    const double tw0 = clk();
+    HIP_OK(hipEventSynchronize(c->pdone[s]));
+    const double tw1 = clk();
+    const int64_t lo = slot_lo[s], m = slot_m[s];
+    const double* d = (const double*)pin_out[s];
+    const int32_t* i32 = (const int32_t*)(d + 8 * m);
+    std::vector<Seg> g;
+    for (int q = 0; q < 3; ++q) {
+      g.push_back({out->x_end + q * n + lo, d + q * m, m * sizeof(double)});
+      g.push_back({out->k_end + q * n + lo, d + (3 + q) * m, m * sizeof(double)});
+    }
+    g.push_back({out->u7_end + lo, d + 6 * m, m * sizeof(double)});
+    g.push_back({out->tau_end + lo, d + 7 * m, m * sizeof(double)});
+    g.push_back({out->status + lo, i32, m * sizeof(int32_t)});
+    g.push_back({out->n_accept + lo, i32 + m, m * sizeof(int32_t)});
+    g.push_back({out->n_reject + lo, i32 + 2 * m, m * sizeof(int32_t)});
+    if (cap) {
+      g.push_back({xc->count + lo, pin_out[s] + cnt_off(m), m * sizeof(int32_t)});
+      const double* x = (const double*)(pin_out[s] + xd_off(m));
+      // rows of [(comp * cap + j) * n + ray]: 3 cap rows of pos, of k, cap rows of t, dw, P
+      for (int r = 0; r < 3 * cap; ++r) {
+        g.push_back({xc->pos + r * n + lo, x + r * m, m * sizeof(double)});
+        g.push_back({xc->k + r * n + lo, x + (3 * cap + r) * m, m * sizeof(double)});
+      }
+      for (int r = 0; r < cap; ++r) {
+        g.push_back({xc->t + r * n + lo, x + (6 * cap + r) * m, m * sizeof(double)});
+        g.push_back({xc->dw + r * n + lo, x + (7 * cap + r) * m, m * sizeof(double)});
+        g.push_back({xc->p_nonad + r * n + lo, x + (8 * cap + r) * m, m * sizeof(double)});
+      }
+    }
+    copy_pool().run(g);
+    if (trace)
+      std::fprintf(stderr, "[art-host] t=%.2f drain lo=%lld wait %.2f ms scatter %.2f ms\n", tw0 - t_start,
+                   (long long)lo, tw1 - tw0, clk() - tw1);
+    slot_lo[s] = -1;
+    return ART_OK;
+  };
+  const int32_t donate = nslots > 1 ? 16 : 0;
+  for (int64_t k = 0; k < K; ++k) {
+    const int s = (int)(k % nslots);
+    hipStream_t st = c->pstreams[s];
+    if ((rc = drain(s))) return rc;  // chunk k - nslots, the slot's previous occupant
+    const int64_t lo = k * n / K, hi = (k + 1) * n / K, m = hi - lo;
+    double* d = (double*)pin_in[s];
+    std::vector<Seg> g;
+    for (int q = 0; q < 3; ++q) {
+      g.push_back({d + q * m, x0 + q * n + lo, m * sizeof(double)});
+      g.push_back({d + (3 + q) * m, k0 + q * n + lo, m * sizeof(double)});
+    }
+    g.push_back({d + 6 * m, erg + lo, m * sizeof(double)});
+    g.push_back({d + 7 * m, dw + lo, m * sizeof(double)});
+    g.push_back({d + 8 * m, ln_t0 + lo, m * sizeof(double)});
+    g.push_back({pin_in[s] + up((size_t)m * 9 * sizeof(double)), species + lo, (size_t)m});
+    const double tg0 = clk();
+    copy_pool().run(g);
+    if (trace) std::fprintf(stderr, "[art-host] t=%.2f gather lo=%lld %.2f ms\n", tg0 - t_start, (long long)lo, clk() - tg0);
+    HIP_OK(hipMemcpyAsync(dev_in[s], pin_in[s], in_bytes(m), hipMemcpyHostToDevice, st));
+    const double* di = (const double*)dev_in[s];
+    double* dd = (double*)dev_out[s];
+    int32_t* di32 = (int32_t*)(dd + 8 * m);
+    art_segment_out dso{dd, dd + 3 * m, dd + 6 * m, dd + 7 * m, di32, di32 + m, di32 + 2 * m};
+    art_crossing_buf dxb{};
+    art_crossing_buf* dxbp = nullptr;
+    if (cap) {
+      int32_t* cnt = (int32_t*)(dev_out[s] + cnt_off(m));
+      double* x = (double*)(dev_out[s] + xd_off(m));
+      // slots without a crossing come back as NaN (as the single-launch host path)
+      HIP_OK(hipMemsetD32Async((hipDeviceptr_t)x, 0x7FF80000, (size_t)cap * m * 9 * 2, st));
+      dxb = art_crossing_buf{cap, cnt, x, x + 3 * cap * m, x + 6 * cap * m, x + 7 * cap * m, x + 8 * cap * m};
+      dxbp = &dxb;
+    }
+    if ((rc = propagate_device_impl(p, m, di, di + 3 * m, di + 6 * m, di + 7 * m, di + 8 * m,
+                                    (const int8_t*)(dev_in[s] + up((size_t)m * 9 * sizeof(double))), max_crossings,
+                                    &dso, dxbp, st, TrajArgs(), donate)))
+      return rc;
+    rings.push_back(c->last);
+    HIP_OK(hipMemcpyAsync(pin_out[s], dev_out[s], out_bytes(m), hipMemcpyDeviceToHost, st));
+    HIP_OK(hipEventRecord(c->pdone[s], st));
+    slot_lo[s] = lo;
+    slot_m[s] = m;
+  }
+  for (int64_t k = K; k < K + nslots; ++k)
+    if ((rc = drain((int)(k % nslots)))) return rc;
+  if (trace) std::fprintf(stderr, "[art-host] total %.2f ms\n", clk() - t_start);
+  return finish_timing_sum(c, rings);
+}
+
 int propagate_host_impl(const art_params* p, int64_t n, const double* x0, const double* k0, const double* erg,
                         const double* dw, const double* ln_t0, const int8_t* species, int32_t max_crossings,
                         art_segment_out* out, art_crossing_buf* xc, const TrajArgs& htr) {
@@ -403,6 +666,12 @@ int propagate_host_impl(const art_params* p, int64_t n, const double* x0, const 
   if (rc || empty) return rc;
   DeviceCtx* c;
   if ((rc = current_ctx(&c))) return rc;
+  // large batches: the chunked pipeline (copies overlap the kernels); ART_HOST_CHUNKS=1 or a
+  // batch below ART_HOST_CHUNK_MIN rays (default 2^21) takes the single launch below
+  const int nchunks = env_int("ART_HOST_CHUNKS", 8);
+  if (htr.ntimes == 0 && nchunks > 1 && n >= env_int("ART_HOST_CHUNK_MIN", 1 << 21))
+    return propagate_host_chunked(c, p, n, x0, k0, erg, dw, ln_t0, species, max_crossings, out, xc, nchunks,
+                                  std::max(1, env_int("ART_HOST_SLOTS", 3)));
   const int cap = (xc && xc->count) ? xc->capacity : 0;
   const size_t nd = (size_t)n;
   // staging layout: inputs 3n+3n+n+n+n doubles + n int8; outputs 3n+3n+n+n doubles + 3n int32 (+ crossings)

@@ -218,3 +218,32 @@ def test_small_batch_w1_first_launch_in_fresh_process():
     out = json.loads(r.stdout.strip().splitlines()[-1])
     for species, (acc, ncross, grid) in out.items():
         assert acc > 0 and grid == 8, (species, acc, ncross, grid)  # 2000 rays: 8 blocks of 256
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg,species,cap,chunks,slots", [("flat", 1, 1, 5, 3), ("flat", 0, 3, 7, 2), ("gr", 1, 2, 4, 3)])
+def test_chunked_host_pipeline_is_bit_exact(cfg, species, cap, chunks, slots, monkeypatch):
+    """art_propagate_host above ART_HOST_CHUNK_MIN rays runs as a pipeline of chunks (pinned
+    staging, copies overlapping the kernels, several chunks in flight with tail donation).
+    An odd batch size split into uneven chunks returns exactly the single launch's outputs,
+    every crossing slot included (NaN where a ray has no crossing), and the call's statistics
+    are the sums over its chunks."""
+    from dataclasses import replace
+    import adiabatic_raytracer_amd as A
+    p = A.Params(**CONFIGS[cfg])
+    n = 20011
+    s = A.sample_conversion_points(p, n, seed=1769)
+    q, k, mc = (p, s["k_init"], -1) if species == 1 else (replace(p, B0=-p.B0), -s["k_init"], 100000)
+    args = (s["x"], k, s["erg"], -np.ones(n), np.full(n, -30.0), np.full(n, species, np.int8))
+    monkeypatch.setenv("ART_HOST_CHUNKS", "1")
+    ref = A.propagate_batch(q, *args, max_crossings=mc, capacity=cap)
+    monkeypatch.setenv("ART_HOST_CHUNKS", str(chunks))
+    monkeypatch.setenv("ART_HOST_SLOTS", str(slots))
+    monkeypatch.setenv("ART_HOST_CHUNK_MIN", "1000")
+    got = A.propagate_batch(q, *args, max_crossings=mc, capacity=cap)
+    for key, v in ref.items():
+        if isinstance(v, np.ndarray):
+            assert np.array_equal(v, got[key], equal_nan=True), (cfg, key)
+    assert np.isnan(got["xc_t"].reshape(cap, n)[:, got["n_cross"] == 0]).all()
+    for key in ("attempts", "accepted", "root_steps", "scan_evals", "rays", "cert_steps"):
+        assert ref["stats"][key] == got["stats"][key], key
