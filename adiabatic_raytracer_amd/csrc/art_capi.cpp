@@ -54,8 +54,8 @@ struct DeviceCtx {
   int32_t donate = 0;            // tail donation (art_set_tail_donation): lanes per wave, 0 = off
   std::vector<std::pair<void*, size_t>> pool;  // host-entry staging buffers (grow-only, used under g_mu by the
                                                // synchronous *_host calls only)
-  // the chunked host pipeline of art_propagate_host (propagate_host_chunked): its extra
-  // streams, and per pipeline slot a pinned input and output staging buffer (grow-only)
+  // the chunked host pipeline of art_propagate_host (propagate_host_chunked): its streams,
+  // its pinned input and output staging (grow-only) and one completion event per chunk
   std::vector<hipStream_t> pstreams;
   std::vector<std::pair<void*, size_t>> pinned;
   std::vector<hipEvent_t> pdone;
@@ -524,136 +524,140 @@ int art_propagate_traj_device(const art_params* p, int64_t n, const double* x0, 
 
 namespace {
 // art_propagate_host for large batches: a pipeline of chunks (the reference call
-// site MainRunner.jl:179-190 hands over host arrays). Chunk k's inputs are gathered from the
-// caller's arrays into pinned staging by the copy pool, copied to HBM, propagated (with tail
-// donation: up to `slots` chunks run concurrently on their own streams, so one chunk's drain
-// tail is filled by the next), and its outputs come back to pinned staging and are scattered
-// into the caller's arrays -- while the chunks after it compute. Per-ray results do not
-// depend on the batch split (tests/test_edges.py), so the outputs equal the single launch's
-// bit for bit. The statistics and kernel time of the call are the sums over its chunks.
+// site MainRunner.jl:179-190 hands over host arrays). Every chunk's inputs are gathered from the
+// caller's arrays into pinned staging by the copy pool and its whole sequence -- H2D, the
+// propagate launch, D2H of its outputs -- is enqueued at once on stream k % slots, so the GPU
+// always holds `slots` chunks in flight (tail donation: one chunk's drain tail is filled by the
+// next) and never waits for the host. The host then waits for the chunks in order and
+// scatters each one's outputs into the caller's arrays while the later ones still compute.
+// (A first version reused `slots` staging buffers and could enqueue chunk k only after chunk
+// k - slots was drained; the concurrent chunks finished together and the GPU idled while the
+// host caught up: 132 ms per 1e7 rays against 128 for the single launch,
+// profiles/r03d_host_path.jsonl.) Per-ray results do not depend on the batch split
+// (tests/test_edges.py), so the outputs equal the single launch's bit for bit. The statistics
+// and kernel time of the call are the sums over its chunks.
 int propagate_host_chunked(DeviceCtx* c, const art_params* p, int64_t n, const double* x0, const double* k0,
                            const double* erg, const double* dw, const double* ln_t0, const int8_t* species,
                            int32_t max_crossings, art_segment_out* out, art_crossing_buf* xc, int nchunks,
                            int nslots) {
   const int cap = (xc && xc->count) ? xc->capacity : 0;
   const int64_t K = nchunks;
-  const int64_t m_max = (n + K - 1) / K;
   auto up = [](size_t b) { return (b + 255) & ~size_t(255); };
   // blob layouts of a chunk of m rays (identical in pinned staging and in HBM)
   auto in_bytes = [&](int64_t m) { return up((size_t)m * 9 * sizeof(double)) + up((size_t)m); };
   auto cnt_off = [&](int64_t m) { return up((size_t)m * 8 * sizeof(double) + (size_t)m * 3 * sizeof(int32_t)); };
   auto xd_off = [&](int64_t m) { return cnt_off(m) + up((size_t)m * sizeof(int32_t)); };
   auto out_bytes = [&](int64_t m) { return cap ? xd_off(m) + (size_t)cap * m * 9 * sizeof(double) : cnt_off(m); };
+  std::vector<int64_t> lo(K + 1);
+  std::vector<size_t> ioff(K + 1, 0), ooff(K + 1, 0);
+  for (int64_t k = 0; k <= K; ++k) lo[k] = k * n / K;
+  for (int64_t k = 0; k < K; ++k) {
+    ioff[k + 1] = ioff[k] + in_bytes(lo[k + 1] - lo[k]);
+    ooff[k + 1] = ooff[k] + out_bytes(lo[k + 1] - lo[k]);
+  }
   while ((int)c->pstreams.size() < nslots) {
     hipStream_t st = c->stream;
     if (!c->pstreams.empty()) HIP_OK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
     c->pstreams.push_back(st);
+  }
+  while ((int64_t)c->pdone.size() < K) {
     hipEvent_t ev;
     HIP_OK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
     c->pdone.push_back(ev);
   }
-  std::vector<char*> pin_in(nslots), pin_out(nslots), dev_in(nslots), dev_out(nslots);
   int rc;
-  for (int s = 0; s < nslots; ++s) {
-    void *a, *b, *d1, *d2;
-    if ((rc = pinned_get(c, 2 * s, in_bytes(m_max), &a)) || (rc = pinned_get(c, 2 * s + 1, out_bytes(m_max), &b)) ||
-        (rc = pool_get(c, 16 + 2 * s, in_bytes(m_max), &d1)) || (rc = pool_get(c, 17 + 2 * s, out_bytes(m_max), &d2)))
-      return rc;
-    pin_in[s] = (char*)a; pin_out[s] = (char*)b; dev_in[s] = (char*)d1; dev_out[s] = (char*)d2;
-  }
+  void *pi, *po, *di_, *do_;
+  if ((rc = pinned_get(c, 0, ioff[K], &pi)) || (rc = pinned_get(c, 1, ooff[K], &po)) ||
+      (rc = pool_get(c, 16, ioff[K], &di_)) || (rc = pool_get(c, 17, ooff[K], &do_)))
+    return rc;
+  char *pin_in = (char*)pi, *pin_out = (char*)po, *dev_in = (char*)di_, *dev_out = (char*)do_;
   using Seg = CopyPool::Seg;
-  std::vector<int64_t> slot_lo(nslots, -1), slot_m(nslots, 0);
   std::vector<int> rings;
-  // ART_HOST_TRACE=1: the host side of every chunk to stderr (waits, gathers, scatters)
+  // ART_HOST_TRACE=1: the host side of every chunk to stderr (gathers, waits, scatters)
   const bool trace = env_int("ART_HOST_TRACE", 0) != 0;
   auto clk = [] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
   const double t_start = clk();
-  // the outputs of the chunk in slot s: pinned staging -> the caller's arrays
-  auto drain = [&](int s) -> int {
-    if (slot_lo[s] < 0) return ART_OK;
-    const double tw0 = clk();
-    HIP_OK(hipEventSynchronize(c->pdone[s]));
-    const double tw1 = clk();
-    const int64_t lo = slot_lo[s], m = slot_m[s];
-    const double* d = (const double*)pin_out[s];
-    const int32_t* i32 = (const int32_t*)(d + 8 * m);
-    std::vector<Seg> g;
-    for (int q = 0; q < 3; ++q) {
-      g.push_back({out->x_end + q * n + lo, d + q * m, m * sizeof(double)});
-      g.push_back({out->k_end + q * n + lo, d + (3 + q) * m, m * sizeof(double)});
-    }
-    g.push_back({out->u7_end + lo, d + 6 * m, m * sizeof(double)});
-    g.push_back({out->tau_end + lo, d + 7 * m, m * sizeof(double)});
-    g.push_back({out->status + lo, i32, m * sizeof(int32_t)});
-    g.push_back({out->n_accept + lo, i32 + m, m * sizeof(int32_t)});
-    g.push_back({out->n_reject + lo, i32 + 2 * m, m * sizeof(int32_t)});
-    if (cap) {
-      g.push_back({xc->count + lo, pin_out[s] + cnt_off(m), m * sizeof(int32_t)});
-      const double* x = (const double*)(pin_out[s] + xd_off(m));
-      // rows of [(comp * cap + j) * n + ray]: 3 cap rows of pos, of k, cap rows of t, dw, P
-      for (int r = 0; r < 3 * cap; ++r) {
-        g.push_back({xc->pos + r * n + lo, x + r * m, m * sizeof(double)});
-        g.push_back({xc->k + r * n + lo, x + (3 * cap + r) * m, m * sizeof(double)});
-      }
-      for (int r = 0; r < cap; ++r) {
-        g.push_back({xc->t + r * n + lo, x + (6 * cap + r) * m, m * sizeof(double)});
-        g.push_back({xc->dw + r * n + lo, x + (7 * cap + r) * m, m * sizeof(double)});
-        g.push_back({xc->p_nonad + r * n + lo, x + (8 * cap + r) * m, m * sizeof(double)});
-      }
-    }
-    copy_pool().run(g);
-    if (trace)
-      std::fprintf(stderr, "[art-host] t=%.2f drain lo=%lld wait %.2f ms scatter %.2f ms\n", tw0 - t_start,
-                   (long long)lo, tw1 - tw0, clk() - tw1);
-    slot_lo[s] = -1;
-    return ART_OK;
-  };
   const int32_t donate = nslots > 1 ? 16 : 0;
   for (int64_t k = 0; k < K; ++k) {
-    const int s = (int)(k % nslots);
-    hipStream_t st = c->pstreams[s];
-    if ((rc = drain(s))) return rc;  // chunk k - nslots, the slot's previous occupant
-    const int64_t lo = k * n / K, hi = (k + 1) * n / K, m = hi - lo;
-    double* d = (double*)pin_in[s];
+    hipStream_t st = c->pstreams[k % nslots];
+    const int64_t l0 = lo[k], m = lo[k + 1] - lo[k];
+    char* bi = pin_in + ioff[k];
+    double* d = (double*)bi;
     std::vector<Seg> g;
     for (int q = 0; q < 3; ++q) {
-      g.push_back({d + q * m, x0 + q * n + lo, m * sizeof(double)});
-      g.push_back({d + (3 + q) * m, k0 + q * n + lo, m * sizeof(double)});
+      g.push_back({d + q * m, x0 + q * n + l0, m * sizeof(double)});
+      g.push_back({d + (3 + q) * m, k0 + q * n + l0, m * sizeof(double)});
     }
-    g.push_back({d + 6 * m, erg + lo, m * sizeof(double)});
-    g.push_back({d + 7 * m, dw + lo, m * sizeof(double)});
-    g.push_back({d + 8 * m, ln_t0 + lo, m * sizeof(double)});
-    g.push_back({pin_in[s] + up((size_t)m * 9 * sizeof(double)), species + lo, (size_t)m});
+    g.push_back({d + 6 * m, erg + l0, m * sizeof(double)});
+    g.push_back({d + 7 * m, dw + l0, m * sizeof(double)});
+    g.push_back({d + 8 * m, ln_t0 + l0, m * sizeof(double)});
+    g.push_back({bi + up((size_t)m * 9 * sizeof(double)), species + l0, (size_t)m});
     const double tg0 = clk();
     copy_pool().run(g);
-    if (trace) std::fprintf(stderr, "[art-host] t=%.2f gather lo=%lld %.2f ms\n", tg0 - t_start, (long long)lo, clk() - tg0);
-    HIP_OK(hipMemcpyAsync(dev_in[s], pin_in[s], in_bytes(m), hipMemcpyHostToDevice, st));
-    const double* di = (const double*)dev_in[s];
-    double* dd = (double*)dev_out[s];
+    if (trace) std::fprintf(stderr, "[art-host] t=%.2f gather lo=%lld %.2f ms\n", tg0 - t_start, (long long)l0, clk() - tg0);
+    char* dbi = dev_in + ioff[k];
+    char* dbo = dev_out + ooff[k];
+    HIP_OK(hipMemcpyAsync(dbi, bi, in_bytes(m), hipMemcpyHostToDevice, st));
+    const double* di = (const double*)dbi;
+    double* dd = (double*)dbo;
     int32_t* di32 = (int32_t*)(dd + 8 * m);
     art_segment_out dso{dd, dd + 3 * m, dd + 6 * m, dd + 7 * m, di32, di32 + m, di32 + 2 * m};
     art_crossing_buf dxb{};
     art_crossing_buf* dxbp = nullptr;
     if (cap) {
-      int32_t* cnt = (int32_t*)(dev_out[s] + cnt_off(m));
-      double* x = (double*)(dev_out[s] + xd_off(m));
+      int32_t* cnt = (int32_t*)(dbo + cnt_off(m));
+      double* x = (double*)(dbo + xd_off(m));
       // slots without a crossing come back as NaN (as the single-launch host path)
       HIP_OK(hipMemsetD32Async((hipDeviceptr_t)x, 0x7FF80000, (size_t)cap * m * 9 * 2, st));
       dxb = art_crossing_buf{cap, cnt, x, x + 3 * cap * m, x + 6 * cap * m, x + 7 * cap * m, x + 8 * cap * m};
       dxbp = &dxb;
     }
     if ((rc = propagate_device_impl(p, m, di, di + 3 * m, di + 6 * m, di + 7 * m, di + 8 * m,
-                                    (const int8_t*)(dev_in[s] + up((size_t)m * 9 * sizeof(double))), max_crossings,
-                                    &dso, dxbp, st, TrajArgs(), donate)))
+                                    (const int8_t*)(dbi + up((size_t)m * 9 * sizeof(double))), max_crossings, &dso,
+                                    dxbp, st, TrajArgs(), donate)))
       return rc;
     rings.push_back(c->last);
-    HIP_OK(hipMemcpyAsync(pin_out[s], dev_out[s], out_bytes(m), hipMemcpyDeviceToHost, st));
-    HIP_OK(hipEventRecord(c->pdone[s], st));
-    slot_lo[s] = lo;
-    slot_m[s] = m;
+    HIP_OK(hipMemcpyAsync(pin_out + ooff[k], dbo, out_bytes(m), hipMemcpyDeviceToHost, st));
+    HIP_OK(hipEventRecord(c->pdone[k], st));
   }
-  for (int64_t k = K; k < K + nslots; ++k)
-    if ((rc = drain((int)(k % nslots)))) return rc;
+  // the chunks' outputs, in order: pinned staging -> the caller's arrays
+  for (int64_t k = 0; k < K; ++k) {
+    const double tw0 = clk();
+    HIP_OK(hipEventSynchronize(c->pdone[k]));
+    const double tw1 = clk();
+    const int64_t l0 = lo[k], m = lo[k + 1] - lo[k];
+    const char* bo = pin_out + ooff[k];
+    const double* d = (const double*)bo;
+    const int32_t* i32 = (const int32_t*)(d + 8 * m);
+    std::vector<Seg> g;
+    for (int q = 0; q < 3; ++q) {
+      g.push_back({out->x_end + q * n + l0, d + q * m, m * sizeof(double)});
+      g.push_back({out->k_end + q * n + l0, d + (3 + q) * m, m * sizeof(double)});
+    }
+    g.push_back({out->u7_end + l0, d + 6 * m, m * sizeof(double)});
+    g.push_back({out->tau_end + l0, d + 7 * m, m * sizeof(double)});
+    g.push_back({out->status + l0, i32, m * sizeof(int32_t)});
+    g.push_back({out->n_accept + l0, i32 + m, m * sizeof(int32_t)});
+    g.push_back({out->n_reject + l0, i32 + 2 * m, m * sizeof(int32_t)});
+    if (cap) {
+      g.push_back({xc->count + l0, bo + cnt_off(m), m * sizeof(int32_t)});
+      const double* x = (const double*)(bo + xd_off(m));
+      // rows of [(comp * cap + j) * n + ray]: 3 cap rows of pos, of k, cap rows of t, dw, P
+      for (int r = 0; r < 3 * cap; ++r) {
+        g.push_back({xc->pos + r * n + l0, x + r * m, m * sizeof(double)});
+        g.push_back({xc->k + r * n + l0, x + (3 * cap + r) * m, m * sizeof(double)});
+      }
+      for (int r = 0; r < cap; ++r) {
+        g.push_back({xc->t + r * n + l0, x + (6 * cap + r) * m, m * sizeof(double)});
+        g.push_back({xc->dw + r * n + l0, x + (7 * cap + r) * m, m * sizeof(double)});
+        g.push_back({xc->p_nonad + r * n + l0, x + (8 * cap + r) * m, m * sizeof(double)});
+      }
+    }
+    copy_pool().run(g);
+    if (trace)
+      std::fprintf(stderr, "[art-host] t=%.2f drain lo=%lld wait %.2f ms scatter %.2f ms\n", tw0 - t_start,
+                   (long long)l0, tw1 - tw0, clk() - tw1);
+  }
   if (trace) std::fprintf(stderr, "[art-host] total %.2f ms\n", clk() - t_start);
   return finish_timing_sum(c, rings);
 }

@@ -467,17 +467,36 @@ __host__ __device__ inline void rhs_photon(const KParams& P, const T* u, const T
 // numbers). In flat space (rs_eff == 0, compile-time in the GEOM_FLAT kernel) the metric
 // terms drop out; in Schwarzschild
 //   H_r += ½ ∂g^tt E² + ½ ∂g^rr k_r² - ½ ωp² ∂g^rr Q/g^rr - w ∂g^rr/√g^rr k_r a1.
+// ψ = φ - ω (time0 + t), time0 = 0 (MainRunner.jl:177): the argument of rhs_photon_gj's second sincos
+template <class T>
+__host__ __device__ inline T psi_of(const KParams& P, const T& phi, const T& t) {
+  return phi - P.omega * t;
+}
+
+// rhs_photon_gj from its transcendental inputs: t = e^τ, (sin, cos) of θ = u[1] and of ψ = psi_of(u[2], t).
+// The one-ray-per-wave tail kernel evaluates the two sincos on two lanes at once and every
+// stage's e^τ ahead of the stage; the values and the arithmetic here are the same.
+template <class T>
+__host__ __device__ inline void rhs_photon_gj_tr(const KParams& P, const T* u, const T& t, const T& st, const T& ct,
+                                                 const T& sp, const T& cp, double erg, T* du, T* aux = nullptr);
+
 template <class T>
 __host__ __device__ inline void rhs_photon_gj(const KParams& P, const T* u, const T& tau, double erg, T* du,
                                               T* aux = nullptr) {
-  const bool flat = P.rs_eff == 0.0;
   const T t = fexp(tau);
+  T st, ct, sp, cp;
+  msincos(u[1], st, ct);
+  msincos(psi_of(P, u[2], t), sp, cp);
+  rhs_photon_gj_tr(P, u, t, st, ct, sp, cp, erg, du, aux);
+}
+
+template <class T>
+__host__ __device__ inline void rhs_photon_gj_tr(const KParams& P, const T* u, const T& t, const T& st, const T& ct,
+                                                 const T& sp, const T& cp, double erg, T* du, T* aux) {
+  const bool flat = P.rs_eff == 0.0;
   const T r = u[0];
   const T E = -u[6];
   const T rc = rclamp(r, P.rNS);  // max(r, rNS) in one instruction
-  T st, ct, sp, cp;
-  msincos(u[1], st, ct);
-  msincos(u[2] - P.omega * t, sp, cp);
   const T ast = mabs(st);
   const T sgn_st = msign(st);
   const T kr = u[3] * erg, kt = u[4] * erg, kp = u[5] * erg;

@@ -1277,6 +1277,565 @@ __global__ __launch_bounds__(BLOCK, WPS) void propagate_kernel(const KParams P_i
 #endif
 }
 
+// ---------------------------------------------------------------------------
+// tail_kernel: the long rays that set a launch's drain time, ONE WAVE PER RAY.
+//
+// A persistent pass ends with a drain: once its queue is empty, its last long rays run alone
+// in their waves, and a lone lane issues every instruction of its wave (configs[3]'s ray
+// 717277 alone takes ~0.3 s of the 1e6-ray GR batch). With tail donation (SegOut::donate) such
+// rays leave the bulk kernel with their complete state; when few remain, this kernel resumes
+// each of them on a wave of its own and spreads the attempt's independent work across lanes:
+//   * the e^τ of all eight stages of an attempt in one pass on lanes 0..7 (stage times are
+//     known at the attempt's start), instead of one exp per stage on the critical path;
+//   * sin/cos of θ and of ψ = φ - ωt in ONE sincos on lanes 0 and 1 (same code, two arguments);
+//   * the 49 grid points of an uncertified step's resonance scan on lanes 0..48 at once, their
+//     sign codes gathered with two ballots;
+//   * all the stage vectors in registers (one wave per SIMD: 512 VGPRs), the Vern6 stages fully
+//     unrolled with compile-time coefficients, the ray's control state wave-uniform.
+// Everything else is the bulk kernel's arithmetic on the same operands in the same order, so a
+// donated ray's result is bit-identical to its never-donated one (tests/test_gpu_tail_donation.py).
+// Vern6 without saveat only (the other launches keep the packed continuation).
+__constant__ double c_tail_ct[8] = {Vern6::c2, Vern6::c3, Vern6::c4, Vern6::c5, Vern6::c6, Vern6::c7, 1.0, 1.0};
+
+// a wave-uniform double from lane l (two v_readlane_b32)
+__device__ inline double rdlane(double v, int l) {
+  const unsigned long long b = __builtin_bit_cast(unsigned long long, v);
+  const unsigned lo = __builtin_amdgcn_readlane((unsigned)b, l), hi = __builtin_amdgcn_readlane((unsigned)(b >> 32), l);
+  return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
+
+// the 16 bits b[15:0] spread to the even bit positions of 32
+__device__ inline unsigned spread16(unsigned x) {
+  x &= 0xffffu;
+  x = (x | (x << 8)) & 0x00ff00ffu;
+  x = (x | (x << 4)) & 0x0f0f0f0fu;
+  x = (x | (x << 2)) & 0x33333333u;
+  x = (x | (x << 1)) & 0x55555555u;
+  return x;
+}
+
+// scan_nd_lds on register arrays (the same arithmetic)
+__device__ inline void scan_nd_regs(const KParams& P, const double* u0, const double* f0, const double* u1,
+                                    const double* f1, double h, double tau, double th, double& N, double& D) {
+  double ui[7];
+  hermite7(u0, f0, u1, f1, h, th, ui);
+#pragma unroll
+  for (int i = 0; i < 7; ++i) ui[i] = (th == 1.0) ? u1[i] : ui[i];
+  condition_nd(P, ui, fexp(tau + th * h), N, D);
+}
+
+__device__ inline double scan_point_regs(const KParams& P, const double* u0, const double* f0, const double* u1,
+                                         const double* f1, double h, double tau, double th) {
+  double N, D;
+  scan_nd_regs(P, u0, f0, u1, f1, h, tau, th, N, D);
+  return 0.5 * N / D;
+}
+
+// The photon RHS at stage point y, t = e^(τ_s) given: θ's and ψ's sincos on lanes 0 and 1.
+template <int GEOM>
+__device__ inline void tail_rhs(const KParams& P, int lane, const double* y, double ty, double t, double erg,
+                                double* kk, double* aux) {
+  if constexpr (GEOM != GEOM_ANY) {
+    const double arg = (lane == 1) ? psi_of(P, y[2], t) : y[1];
+    double sn, cs;
+    msincos(arg, sn, cs);
+    const double st = rdlane(sn, 0), ct = rdlane(cs, 0), sp = rdlane(sn, 1), cp = rdlane(cs, 1);
+    rhs_photon_gj_tr(P, y, t, st, ct, sp, cp, erg, kk, aux);
+  } else {
+    rhs_photon(P, y, ty, erg, kk, aux);
+  }
+}
+
+template <int GEOM>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void tail_kernel(
+    const KParams P_in, const int64_t n, const SegIn in, const SegOut out, const int32_t max_crossings,
+    const int32_t max_rays, unsigned long long* __restrict__ stats) {
+  const KParams P = specialize<GEOM>(P_in);
+  using V = Vern6;
+  const int lane = threadIdx.x;
+  const int64_t nq = (int64_t)*out.cont_count;
+  if (nq > max_rays) return;  // too many rays for one wave each: the packed continuation takes them
+  __builtin_amdgcn_s_setprio(3);  // the rays that set the launch's end
+  const bool cbs = max_crossings != ART_NO_CALLBACKS;
+  const double tend = P.ln_t_end;
+  const int npts = P.interp_points;
+  const int nper = npts - 1;
+  const double my_ct = c_tail_ct[lane & 7];
+  const double my_th = double(lane + 1) / double(npts - 1);  // grid point lane + 1 (Julia's range(0, 1, length = npts))
+  unsigned s_att = 0, s_acc = 0, s_root = 0, s_scan = 0, s_interp = 0, s_cert = 0;
+  while (true) {
+    unsigned long long ix = 0;
+    if (lane == 0) ix = atomicAdd(out.cont_queue, 1ull);
+    const int64_t rec = (int64_t)__builtin_amdgcn_readfirstlane((unsigned)ix) |
+                        ((int64_t)__builtin_amdgcn_readfirstlane((unsigned)(ix >> 32)) << 32);
+    if (rec >= nq) break;
+    // ---- the donated ray's complete state (the bulk kernel's CONT_REC) ----
+    double u[7], f[7];
+    double tau, dt, qpow, cprev, bstart, erg;
+    int ray, n_acc, n_rej, ncross, iter, sprev;
+    bool photon, cprev_ok, just_evented;
+    {
+      const double2* rq = reinterpret_cast<const double2*>(out.cont + rec * CONT_REC);
+      double v[20];
+#pragma unroll
+      for (int i = 0; i < 10; ++i) {
+        const double2 q = rq[i];
+        v[2 * i] = q.x;
+        v[2 * i + 1] = q.y;
+      }
+#pragma unroll
+      for (int i = 0; i < 7; ++i) {
+        u[i] = v[i];
+        f[i] = v[7 + i];
+      }
+      tau = v[14]; dt = v[15]; qpow = v[16]; cprev = v[17]; bstart = v[18]; erg = v[19];
+      const int4 i0 = reinterpret_cast<const int4*>(rq + 10)[0], i1 = reinterpret_cast<const int4*>(rq + 10)[1];
+      ray = i0.x; n_acc = i0.y; n_rej = i0.z; ncross = i0.w;
+      iter = i1.x; sprev = i1.y;
+      photon = i1.z & 1; cprev_ok = (i1.z >> 1) & 1; just_evented = (i1.z >> 2) & 1;
+    }
+    int mode = M_STEP;
+    double hroot = 0.0, r_tha = 0.0, r_ca = 0.0, r_thb = 0.0, r_cb = 0.0, r_t = 0.0, r_slope = 1.0, post_c = 0.0;
+    int post_s = 0, r_side = 0, r_it = 0;
+    int finish = -1;
+    while (finish < 0) {
+      // ---- this attempt's step size (the bulk kernel's rules) ----
+      bool last = false, forced = false;
+      double hs;
+      if (mode == M_ROOT) {
+        hs = r_t * hroot;
+      } else {
+        hs = dt;
+        if (tau + hs >= tend) { hs = tend - tau; last = true; }
+        else if (hs < P.dtmin) { hs = P.dtmin; forced = true; }
+      }
+      // ---- e^τ of the eight stages at once (lane s: stage s) ----
+      const double tl = fexp(tau + my_ct * hs);
+      // ---- the Vern6 stages, unrolled (c_vern6's rows with their coefficients folded) ----
+      double kA[7], L0[7], L1[7], L2[7], L3[7], L4[7], y[7], kk[7], aux[2] = {0.0, 0.0};
+      auto stage = [&](int s, double ct) {
+        const double ty = tau + ct * hs;
+        const double t = rdlane(tl, s);
+        tail_rhs<GEOM>(P, lane, y, ty, t, erg, kk, aux);
+        if (!photon) {
+          double ka[7];
+          rhs_axion(P, y, ty, erg, ka);
+#pragma unroll
+          for (int i = 0; i < 7; ++i) kk[i] = ka[i];
+        }
+      };
+#pragma unroll
+      for (int i = 0; i < 7; ++i) y[i] = u[i] + hs * (V::a21 * f[i]);
+      stage(0, V::c2);
+#pragma unroll
+      for (int i = 0; i < 7; ++i) kA[i] = kk[i];
+#pragma unroll
+      for (int i = 0; i < 7; ++i) y[i] = u[i] + hs * fma(V::a31, f[i], V::a32 * kA[i]);
+      stage(1, V::c3);
+#pragma unroll
+      for (int i = 0; i < 7; ++i) L0[i] = kk[i];
+#pragma unroll
+      for (int i = 0; i < 7; ++i) {
+        double acc = V::a41 * f[i];
+        acc += V::a43 * L0[i];
+        y[i] = u[i] + hs * acc;
+      }
+      stage(2, V::c4);
+#pragma unroll
+      for (int i = 0; i < 7; ++i) L1[i] = kk[i];
+#pragma unroll
+      for (int i = 0; i < 7; ++i) {
+        double acc = V::a51 * f[i];
+        acc += V::a53 * L0[i];
+        acc += V::a54 * L1[i];
+        y[i] = u[i] + hs * acc;
+      }
+      stage(3, V::c5);
+#pragma unroll
+      for (int i = 0; i < 7; ++i) L2[i] = kk[i];
+#pragma unroll
+      for (int i = 0; i < 7; ++i) {
+        double acc = V::a61 * f[i];
+        acc += V::a63 * L0[i];
+        acc += V::a64 * L1[i];
+        acc += V::a65 * L2[i];
+        y[i] = u[i] + hs * acc;
+      }
+      stage(4, V::c6);
+#pragma unroll
+      for (int i = 0; i < 7; ++i) L3[i] = kk[i];
+#pragma unroll
+      for (int i = 0; i < 7; ++i) {
+        double acc = V::a71 * f[i];
+        acc += V::a73 * L0[i];
+        acc += V::a74 * L1[i];
+        acc += V::a75 * L2[i];
+        acc += V::a76 * L3[i];
+        y[i] = u[i] + hs * acc;
+      }
+      stage(5, V::c7);
+#pragma unroll
+      for (int i = 0; i < 7; ++i) L4[i] = kk[i];
+#pragma unroll
+      for (int i = 0; i < 7; ++i) {
+        double acc = V::a81 * f[i];
+        acc += V::a83 * L0[i];
+        acc += V::a84 * L1[i];
+        acc += V::a85 * L2[i];
+        acc += V::a86 * L3[i];
+        acc += V::a87 * L4[i];
+        y[i] = u[i] + hs * acc;
+      }
+      stage(6, 1.0);
+#pragma unroll
+      for (int i = 0; i < 7; ++i) kA[i] = kk[i];  // k8
+#pragma unroll
+      for (int i = 0; i < 7; ++i) {
+        double acc = fma(V::a91, f[i], V::a98 * kA[i]);
+        acc += V::a94 * L1[i];
+        acc += V::a95 * L2[i];
+        acc += V::a96 * L3[i];
+        acc += V::a97 * L4[i];
+        y[i] = u[i] + hs * acc;
+      }
+      stage(7, 1.0);
+      const double bend = aux[0], tlast = aux[1];
+      // ---- error estimate (y = u_{n+1}, kk = f(u_{n+1})) ----
+      if (photon && y[0] < P.rNS) y[0] = P.rNS;  // clamp on the FSAL stage (:531)
+      double EEst2;
+      {
+        double acc = 0.0;
+#pragma unroll
+        for (int i = 0; i < 7; ++i) {
+          double e = V::e1 * f[i] + V::e8 * kA[i] + V::e9 * kk[i];
+          e += V::e4 * L1[i];
+          e += V::e5 * L2[i];
+          e += V::e6 * L3[i];
+          e += V::e7 * L4[i];
+          e *= hs;
+          const double q = e * frcp(P.abstol + fmax_abs(u[i], y[i]) * P.reltol);
+          acc += q * q;
+        }
+        EEst2 = acc * (1.0 / 7.0);
+      }
+      // ---- controller (STEP) ----
+      bool scan = false;
+      double dtnext = dt;
+      if (mode == M_STEP) {
+        s_att += 1;
+        ++iter;
+        bool finite = !isnan(EEst2) && !isinf(EEst2);
+#pragma unroll
+        for (int i = 0; i < 7; ++i) finite = finite && !isnan(y[i]) && !isinf(y[i]);
+        if (!finite) {
+          finish = ART_STATUS_NONFINITE;
+        } else {
+          double q = 1.0, q11 = 1.0, y60 = 0.0;
+          if (EEst2 == 0.0) {
+            q = 0.1;
+          } else {
+            y60 = fexp(flog(EEst2) * (1.0 / 120.0));
+            const double y2 = y60 * y60;
+            q11 = (y2 * y2) * (y2 * y60);
+            q = q11 * frcp(qpow);
+            q = fmax(0.1, fmin(5.0, q * (1.0 / 0.9)));
+          }
+          const bool accept = (EEst2 <= 1.0) || forced;
+          if (!accept) {
+            dt = hs * frcp(fmin(5.0, q11 * (1.0 / 0.9)));
+            ++n_rej;
+            if (iter >= P.maxiters) finish = ART_STATUS_MAXITERS;
+          } else {
+            ++n_acc;
+            s_acc += 1;
+            const double ym = fmax(y60, 0.8576958985908941);  // (1e-4)^(1/60)
+            qpow = (ym * ym) * (ym * ym);
+            dtnext = hs * frcp(q);
+            scan = true;
+          }
+        }
+      }
+      if (finish >= 0) break;
+      // ---- resonance scan of an accepted step: certificate, else the 49 grid points at once ----
+      const int ccode = !scan ? 0 : (cbs ? scan_certified_code(P, u, f, y, kk, hs, bend, tlast, bstart) : 3);
+      const bool cert = ccode != 0;
+      s_cert += cert ? 1u : 0u;
+      const bool grid = scan && !cert;
+      double gN = 0.0, gD = 1.0;  // lane l: N, D at grid point l + 1
+      unsigned cw[SCAN_WORDS] = {0u, 0u, 0u, 0u};
+      double lastv = 0.0;  // value at the last grid point
+      if (grid) {
+        if (lane < nper) scan_nd_regs(P, u, f, y, kk, hs, tau, my_th, gN, gD);
+        const double cv = 0.5 * gN / gD;
+        const unsigned code = (lane == nper - 1) ? sign_code(cv) : sign_code_nd(gN, gD);
+        const unsigned long long b0 = __ballot(lane < nper && (code & 1u)), b1 = __ballot(lane < nper && (code & 2u));
+#pragma unroll
+        for (int w = 0; w < SCAN_WORDS; ++w)
+          cw[w] = spread16((unsigned)(b0 >> (16 * w))) | (spread16((unsigned)(b1 >> (16 * w))) << 1);
+        lastv = rdlane(cv, nper - 1);
+        s_scan += (unsigned)nper;
+      } else if (ccode != 0) {
+#pragma unroll
+        for (int w = 0; w < SCAN_WORDS; ++w) cw[w] = 0x55555555u * (unsigned)ccode;
+      }
+      auto gval = [&](int j) {  // the condition at grid point j of this step (from the grid pass when it ran)
+        if (grid && j >= 1) return 0.5 * rdlane(gN, j - 1) / rdlane(gD, j - 1);
+        s_interp += 1;
+        return scan_point_regs(P, u, f, y, kk, hs, tau, double(j) / double(npts - 1));
+      };
+      // ---- the sign walk, brackets and root polish: the bulk kernel's per-lane logic ----
+      int ph = scan ? 2 : 0;
+      int ip = 1, last_j = 0;
+      int last_s = sprev;
+      double last_c = cprev;
+      bool lc_ok = cprev_ok;
+      if (ph == 2) {
+        const unsigned s0 = cw[0] & 3u;
+        if (s0 == 1u || s0 == 2u) {
+          bool same = (last_s == 0) || (last_s == (s0 == 1u ? 1 : -1));
+#pragma unroll
+          for (int w = 0; w < SCAN_WORDS; ++w) {
+            const int nw = nper - 16 * w;
+            if (nw <= 0) break;
+            const unsigned m = nw >= 16 ? 0xffffffffu : ((1u << (2 * nw)) - 1u);
+            same = same && ((cw[w] & m) == ((s0 * 0x55555555u) & m));
+          }
+          if (same) {
+            last_s = (s0 == 1u) ? 1 : -1;
+            last_j = nper;
+            if (!cert) last_c = lastv;
+            lc_ok = !cert;
+            ph = 0;
+          }
+        } else if (s0 == 3u) {
+          bool all = true;
+#pragma unroll
+          for (int w = 0; w < SCAN_WORDS; ++w) {
+            const int nw = nper - 16 * w;
+            if (nw <= 0) break;
+            const unsigned m = nw >= 16 ? 0xffffffffu : ((1u << (2 * nw)) - 1u);
+            all = all && ((cw[w] & m) == m);
+          }
+          if (all) {
+            last_s = 0;
+            lc_ok = false;
+            ph = 0;
+          }
+        }
+      }
+      double i_tha = 0.0, i_ca = 0.0, i_thb = 0.0, i_cb = 0.0, i_tr = 0.0, i_cg = 0.0;
+      int i_side = 0, i_it = 0;
+      bool hit = false, root_done = false;
+      auto thg = [&](int j) { return double(j) / double(npts - 1); };
+      auto open_root = [&](double t_int) {
+        const double tg = thg(ip), lth = thg(last_j);
+        hit = true;
+        hroot = hs;
+        r_tha = lth; r_ca = last_c; r_thb = tg; r_cb = i_cg;
+        r_slope = (i_cg - last_c) / (tg - lth);
+        r_t = (t_int > lth && t_int < tg) ? t_int : 0.5 * (lth + tg);
+        r_side = 0;
+        r_it = 0;
+        post_c = i_cg;
+        post_s = sgn(i_cg);
+        dt = dtnext;
+      };
+      auto open_bracket = [&]() {
+        lc_ok = true;
+        i_tha = thg(last_j);
+        i_ca = last_c;
+        i_thb = thg(ip);
+        i_cb = i_cg;
+        i_tr = i_tha - i_ca * (i_thb - i_tha) / (i_cb - i_ca);
+        i_side = 0;
+        i_it = 0;
+        if (just_evented && i_tha < 0.01) {
+          ph = 3;
+        } else {
+          open_root(i_tr);
+          ph = 0;
+        }
+      };
+      auto walk = [&]() {
+        WalkState ws{ip, last_s, last_j, lc_ok};
+        bool found = false;
+        if (!walk_codes_bits(cw, nper, ws, found)) walk_codes_loop(cw, nper, ws, found);
+        ip = ws.ip;
+        last_s = ws.last_s;
+        last_j = ws.last_j;
+        lc_ok = ws.lc_ok;
+        if (found) {
+          ph = 5;
+        } else if (!lc_ok && last_j == nper) {
+          if (!cert) {
+            last_c = lastv;
+            lc_ok = true;
+          }
+          ph = 0;
+        } else if (!lc_ok && last_s != 0) {
+          ph = 7;
+        } else {
+          ph = 0;
+        }
+      };
+      auto polish = [&](double ci) {
+        ++r_it;
+        bool done = !(fabs(ci) > 1e-12);
+        if (!done) {
+          if (sgn(ci) == sgn(r_ca)) { r_tha = r_t; r_ca = ci; if (r_side == -1) r_cb *= 0.5; r_side = -1; }
+          else { r_thb = r_t; r_cb = ci; if (r_side == 1) r_ca *= 0.5; r_side = 1; }
+          done = (r_thb - r_tha) * hroot < 1e-13 || r_it >= 9;
+          if (!done) {
+            double tn = (r_it == 1) ? r_t - ci / r_slope : r_tha - r_ca * (r_thb - r_tha) / (r_cb - r_ca);
+            if (!(tn > r_tha && tn < r_thb)) tn = 0.5 * (r_tha + r_thb);
+            r_t = tn;
+          }
+        }
+        root_done = done;
+        ph = 0;
+      };
+      if (mode == M_ROOT) {  // the re-stepped end's value (th = 1 of this step)
+        s_root += 1;
+        polish(scan_point_regs(P, u, f, y, kk, hs, tau, 1.0));
+      }
+      if (ph == 2) walk();
+#pragma unroll 1
+      while (ph != 0) {
+        if (ph == 2) {
+          walk();
+          if (ph == 0) break;
+        }
+        if (ph == 5) {  // the values at the change point and, when unknown, at the bracket start
+          i_cg = gval(ip);
+          if (!lc_ok) last_c = gval(last_j);
+          open_bracket();
+        } else if (ph == 7) {
+          last_c = gval(last_j);
+          lc_ok = true;
+          ph = 0;
+        } else {  // ph 3: Illinois on the interpolant inside (i_tha, i_thb] (repeat_nudge)
+          s_interp += 1;
+          const double ci = scan_point_regs(P, u, f, y, kk, hs, tau, i_tr);
+          bool stop = ci == 0.0 || isnan(ci) || (i_thb - i_tha) < 1e-12;
+          bool below = false;
+          if (!stop) {
+            if (sgn(ci) == sgn(i_ca)) { i_tha = i_tr; i_ca = ci; if (i_side == -1) i_cb *= 0.5; i_side = -1; }
+            else { i_thb = i_tr; i_cb = ci; if (i_side == 1) i_ca *= 0.5; i_side = 1; }
+            below = just_evented && i_thb < 0.01;
+            if (below) {
+              stop = true;
+            } else {
+              const double tn = i_tha - i_ca * (i_thb - i_tha) / (i_cb - i_ca);
+              if (tn == i_tr) stop = true;
+              else i_tr = tn;
+              if (++i_it >= 40) stop = true;
+            }
+          }
+          if (stop) {
+            const double t_int = i_tr;
+            if (!below && !(just_evented && t_int < 0.01)) {
+              open_root(t_int);
+              ph = 0;
+            } else {
+              last_s = sgn(i_cg);
+              last_c = i_cg;
+              last_j = ip;
+              lc_ok = true;
+              ++ip;
+              ph = 2;
+            }
+          }
+        }
+      }
+      // ---- the state the ray continues from (the bulk kernel's reload and event logic) ----
+      if (root_done || (scan && !hit)) {
+#pragma unroll
+        for (int i = 0; i < 7; ++i) {
+          u[i] = y[i];
+          f[i] = kk[i];
+        }
+        bstart = bend;
+      }
+      if (hit) mode = M_ROOT;
+      if (root_done) {
+        const double tau_r = tau + hs;
+        int a = 0;
+        {  // affect! (RayTracer.jl:301-350) as the bulk kernel's affect(), stored by lane 0
+          double st, ct, sp, cp;
+          msincos(u[1], st, ct);
+          msincos(u[2], sp, cp);
+          bool skip = false;
+          if (ncross == 0) {
+            const double sc = 1.0001;
+            const double pos[3] = {st * cp * u[0], st * sp * u[0], ct * u[0]};
+            bool all_lt = true, all_gt = true;
+#pragma unroll
+            for (int i = 0; i < 3; ++i) {
+              const double x0i = fabs(in.x0[i * n + ray]);
+              all_lt = all_lt && (fabs(pos[i]) < x0i * sc);
+              all_gt = all_gt && (fabs(pos[i]) > x0i / sc);
+            }
+            skip = all_lt && all_gt;
+          }
+          if (!skip) {
+            double x[3], k[3];
+            sph_to_cart(u, erg, P.rs_eff, x, k);
+            if (!(sqrt(x[0] * x[0] + x[1] * x[1] + x[2] * x[2]) < P.rNS101)) {
+              const int j = ncross;
+              if (lane == 0 && out.xcount && j < out.cap) {
+                double2* rq = reinterpret_cast<double2*>(out.xrec + ((int64_t)ray * out.cap + j) * X_REC);
+                rq[0] = make_double2(x[0], x[1]);
+                rq[1] = make_double2(x[2], k[0]);
+                rq[2] = make_double2(k[1], k[2]);
+                rq[3] = make_double2(exp(tau_r), u[6] / erg);
+              }
+              ncross = j + 1;
+              const int maxc = max_crossings <= 0 ? -1 : max_crossings;
+              a = (ncross >= maxc) ? 2 : 1;
+            }
+          }
+        }
+        tau = tau_r;
+        cprev = post_c;
+        cprev_ok = true;
+        sprev = post_s;
+        just_evented = true;
+        mode = M_STEP;
+        if (a == 2) finish = ART_STATUS_CROSSING;
+        else if (photon && u[0] < P.rNS101) finish = ART_STATUS_HIT_NS;
+        else if (iter >= P.maxiters) finish = ART_STATUS_MAXITERS;
+      }
+      if (scan && !hit) {
+        tau = last ? tend : tau + hs;
+        cprev = last_c;
+        cprev_ok = lc_ok;
+        sprev = last_s;
+        just_evented = false;
+        dt = dtnext;
+        if (cbs && photon && u[0] < P.rNS101) finish = ART_STATUS_HIT_NS;
+        else if (last) finish = ART_STATUS_SUCCESS;
+        else if (iter >= P.maxiters) finish = ART_STATUS_MAXITERS;
+      }
+    }
+    if (lane == 0) {  // the raw end record; finalize_kernel back-transforms it
+      double2* rq = reinterpret_cast<double2*>(out.rec + (int64_t)ray * END_REC);
+      rq[0] = make_double2(u[0], u[1]);
+      rq[1] = make_double2(u[2], u[3]);
+      rq[2] = make_double2(u[4], u[5]);
+      rq[3] = make_double2(u[6], tau);
+      int4* ri = reinterpret_cast<int4*>(rq + 4);
+      ri[0] = make_int4(finish, n_acc, n_rej, ncross);
+    }
+  }
+  if (lane == 0) {
+    const unsigned v[6] = {s_att, s_acc, s_root, s_scan, s_interp, s_cert};
+    const int slot[6] = {ST_ATTEMPTS, ST_ACCEPTED, ST_ROOT_STEPS, ST_SCAN_EVALS, ST_INTERP_EVALS, ST_CERT};
+#pragma unroll
+    for (int k = 0; k < 6; ++k)
+      if (v[k]) atomicAdd(&stats[slot[k]], (unsigned long long)v[k]);
+  }
+}
+
 // Fresh state of every segment, one thread per ray: u0 (RayTracer.jl:179-216: k_norm_Cart
 // onto the axion shell, Cartesian -> (r, θ, φ), covariant celerity), f(u0) with the
 // hamiltonian's in-place clamp (:531), the initial dt (ode_determine_initdt, order 6, with
@@ -1924,6 +2483,13 @@ static KFn pick_propagate(bool save, bool rk4, bool flat, bool sch) {
                             : propagate_kernel<ART_VERN6, GEOM_ANY, false, DON>));
 }
 
+// The one-wave-per-ray tail kernel for donated rays: ART_TAIL=0 off, ART_TAIL=k at most k rays
+// (default 1: one per SIMD of the device).
+static int tail_rays() {
+  const char* e = std::getenv("ART_TAIL");  // read per launch (tests switch it)
+  return (e && *e) ? std::atoi(e) : 1;
+}
+
 // The 1-wave/SIMD instantiations (small batches, GR continuations) are on unless ART_W1=0.
 static bool w1_builds() {
   static const bool on = [] {
@@ -1991,6 +2557,22 @@ hipError_t launch_propagate(const KParams& P, int64_t n, const SegIn& in, const 
     // configs[3] bench line: 3.21e8 -> 3.35e8 ray-steps/s, bit-identical
     // (profiles/r02h_continuation_w1_ab.txt); flat stays at 2 (measured -3.5% at 1).
     const KFn cfn = (w1_builds() && sch && !rk4 && out.ntimes < 2) ? propagate_kernel<ART_VERN6, GEOM_GR, false, true, 1> : fn;
+    // few donated rays: one wave each (tail_kernel, up to one per SIMD; ART_TAIL=0 off); it
+    // leaves the work queue drained for the packed continuation below, or returns at once and
+    // leaves every record to it
+    if (tail_rays() > 0 && !rk4 && out.ntimes < 2) {
+      int dev = 0, ncu = 0;
+      (void)hipGetDevice(&dev);
+      (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+      const int max_rays = tail_rays() == 1 ? ncu * 4 : tail_rays();
+      const int tgrid = (int)(maxc < max_rays ? maxc : max_rays);
+      using TFn = void (*)(const KParams, const int64_t, const SegIn, const SegOut, const int32_t, const int32_t,
+                           unsigned long long*);
+      const TFn tfn = flat ? tail_kernel<GEOM_FLAT> : (sch ? tail_kernel<GEOM_GR> : tail_kernel<GEOM_ANY>);
+      hipLaunchKernelGGL(tfn, dim3(tgrid), dim3(64), 0, s, P, n, in, oc, max_crossings, max_rays, stats);
+      ART_DBG("tail_kernel")
+      if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
     hipLaunchKernelGGL(cfn, dim3(cgrid), dim3(BLOCK), 0, s, P, n, in, oc, max_crossings, queue, stats);
     ART_DBG("continuation")
     if ((e = hipGetLastError()) != hipSuccess) return e;

@@ -27,8 +27,13 @@ def _run(eng, inp, lanes):
     return {k: v.cpu().numpy() for k, v in out.items() if hasattr(v, "cpu")}, st
 
 
-@pytest.mark.parametrize("cfg", ["flat", "gr"])
-def test_tail_donation_is_bit_exact(cfg):
+@pytest.mark.parametrize("cfg", ["flat", "gr", "gr_oblique"])
+@pytest.mark.parametrize("tail", ["0", "100000"], ids=["packed", "tail_kernel"])
+def test_tail_donation_is_bit_exact(cfg, tail, monkeypatch):
+    """ART_TAIL=0: the donated rays resume packed into full waves (the bulk kernel's own
+    continuation); ART_TAIL=100000: every donated ray resumes on a wave of its own (tail_kernel,
+    which spreads the attempt's independent work over the lanes)."""
+    monkeypatch.setenv("ART_TAIL", tail)
     import adiabatic_raytracer_amd as A
     from adiabatic_raytracer_amd import Engine
     eng = Engine(A.Params(**CONFIGS[cfg]))
@@ -67,7 +72,8 @@ def _host_run(p, args, lanes, **kw):
 
 @pytest.mark.parametrize("cfg", ["flat", "gr"])
 @pytest.mark.parametrize("mode", ["backtrace", "saveat"])
-def test_tail_donation_round_trips_crossings_and_saved_points(cfg, mode):
+@pytest.mark.parametrize("tail", ["0", "100000"], ids=["packed", "tail_kernel"])
+def test_tail_donation_round_trips_crossings_and_saved_points(cfg, mode, tail, monkeypatch):
     """The donation record carries the post-event state (condition memory, sign, the
     just-evented flag), the crossing count and the next saveat index. Round trips through it
     with several crossings per ray -- the all-crossings axion backtrace (max_crossings 100000,
@@ -76,6 +82,7 @@ def test_tail_donation_round_trips_crossings_and_saved_points(cfg, mode):
     device's donation setting like every launch)."""
     from dataclasses import replace
     import adiabatic_raytracer_amd as A
+    monkeypatch.setenv("ART_TAIL", tail)
     p = A.Params(**CONFIGS[cfg])
     n = 4000
     s = A.sample_conversion_points(p, n, seed=1769)

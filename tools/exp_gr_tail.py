@@ -15,6 +15,7 @@ from adiabatic_raytracer_amd import Engine  # noqa: E402
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 1_000_000
 KW = json.loads(os.environ.get("TAIL_KW", '{"theta_m": 0.0, "mass_a": 1e-6, "flat": false}'))
 eng = Engine(A.Params(**KW))
+DONATE = int(os.environ.get("TAIL_DONATE", "0"))  # > 0: the ray goes to the one-wave-per-ray tail kernel
 sect = any(k in os.environ.get("ART_LIB", "") for k in ("sect", "slot"))
 if len(sys.argv) > 2:
     ray = int(sys.argv[2])
@@ -27,13 +28,15 @@ else:
                       "top_rays": top.indices.tolist(), "mean_attempts": float(att.double().mean())}), flush=True)
     ray = int(top.indices[0])
 inp1 = eng.forward_roots(1, seed=1769, ray_offset=ray)
+eng.set_tail_donation(DONATE)
 for _ in range(2):
     out1 = eng.propagate(inp1)
 ms = eng.kernel_ms()
 st = A.raytracer.last_stats()
 a = int(out1["n_accept"][0] + out1["n_reject"][0])
 line = {"ray": ray, "kernel_ms": ms, "attempts": a, "us_per_attempt": ms * 1e3 / a,
-        "status": int(out1["status"][0])}
+        "status": int(out1["status"][0]), "donate": DONATE, "tail": os.environ.get("ART_TAIL", "1"),
+        "x_end": out1["x_end"].cpu().tolist(), "n_accept": int(out1["n_accept"][0])}
 if sect:
     NAMES = ["refill etc", "stage slots", "norm/controller/cert/park", "grid pass", "fast paths", "walk", "coop pass",
              "fallback"]
