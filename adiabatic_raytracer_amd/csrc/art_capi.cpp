@@ -313,7 +313,10 @@ int propagate_device_impl(const art_params* p, int64_t n, const double* x0, cons
     HIP_OK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device));
     ncont = std::min(nd, (size_t)ncu * 32 * (size_t)donate);
   }
-  const size_t contb = ncont * art::CONT_REC * sizeof(double);
+  // the second level (the packed continuation's own donations, resumed by the tail kernel):
+  // at most (continuation waves) x 63 records, never more than the first level's
+  const size_t ncont2 = ncont;
+  const size_t contb = (ncont + ncont2) * art::CONT_REC * sizeof(double);
   LaunchRec* L;
   if ((rc = take_slot(c, &L))) return rc;
   void* blk = nullptr;
@@ -339,8 +342,11 @@ int propagate_device_impl(const art_params* p, int64_t n, const double* x0, cons
   so.rec = rec;
   if (ncont) {
     so.cont = (double*)((char*)blk + head + u0b + recb + xrb);
-    so.cont_count = words + 16;  // head words 16 and 17 (zeroed with the head)
+    so.cont_count = words + 16;  // head words 16 .. 19 (zeroed with the head)
     so.cont_queue = words + 17;
+    so.cont2 = so.cont + ncont * art::CONT_REC;
+    so.cont2_count = words + 18;
+    so.cont2_queue = words + 19;
     so.donate = donate;
   }
   HIP_OK(hipMemsetAsync(words, 0, head, s));

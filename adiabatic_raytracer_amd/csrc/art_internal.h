@@ -43,6 +43,13 @@ struct SegOut {
   unsigned long long* cont_count;
   unsigned long long* cont_queue;
   int32_t donate, cont_mode;
+  // the continuation launch (cont_mode = 1) reads the records from cont_src (count
+  // *cont_src_count) and may itself donate its own drained waves' last rays into cont /
+  // cont_count: the second level, which tail_kernel resumes one ray per wave
+  const double* cont_src;
+  const unsigned long long* cont_src_count;
+  double* cont2;  // the second-level records (set on the launch's SegOut; read by launch_propagate)
+  unsigned long long *cont2_count, *cont2_queue;
 };
 constexpr int END_REC = 16;
 constexpr int X_REC = 8;

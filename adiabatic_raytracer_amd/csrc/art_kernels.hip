@@ -412,7 +412,7 @@ __global__ __launch_bounds__(BLOCK, WPS) void propagate_kernel(const KParams P_i
   constexpr bool RK4 = (INTEG == ART_RK4);
   // the work queue: fresh rays [0, n), or in a continuation launch the donated records
   const bool cont = DON && out.cont_mode;
-  const int64_t nq = cont ? (int64_t)*out.cont_count : n;
+  const int64_t nq = cont ? (int64_t)*out.cont_src_count : n;
   unsigned long long* const rqueue = cont ? out.cont_queue : queue;
   // the callbacks (RayTracer.jl:357-368) are installed only when make_tree (:361-377)
   const bool cbs = max_crossings != ART_NO_CALLBACKS;
@@ -519,7 +519,7 @@ __global__ __launch_bounds__(BLOCK, WPS) void propagate_kernel(const KParams P_i
         if (mode == M_IDLE && rank < take && cont) {
           // a donated ray: its complete state from the tail-donation record
           mode = M_STEP;
-          const double2* rq = reinterpret_cast<const double2*>(out.cont + (int64_t)(wnext + rank) * CONT_REC);
+          const double2* rq = reinterpret_cast<const double2*>(out.cont_src + (int64_t)(wnext + rank) * CONT_REC);
           double v[20];
 #pragma unroll
           for (int i = 0; i < 10; ++i) {
@@ -1354,7 +1354,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
   using V = Vern6;
   const int lane = threadIdx.x;
   const int64_t nq = (int64_t)*out.cont_count;
-  if (nq > max_rays) return;  // too many rays for one wave each: the packed continuation takes them
+  (void)max_rays;
   __builtin_amdgcn_s_setprio(3);  // the rays that set the launch's end
   const bool cbs = max_crossings != ART_NO_CALLBACKS;
   const double tend = P.ln_t_end;
@@ -2490,6 +2490,13 @@ static int tail_rays() {
   return (e && *e) ? std::atoi(e) : 1;
 }
 
+// lanes a drained wave of the packed continuation hands to the tail kernel (ART_TAIL_DONATE)
+static int tail_donate() {
+  const char* e = std::getenv("ART_TAIL_DONATE");
+  const int v = (e && *e) ? std::atoi(e) : 4;
+  return v < 1 ? 1 : (v > 63 ? 63 : v);
+}
+
 // The 1-wave/SIMD instantiations (small batches, GR continuations) are on unless ART_W1=0.
 static bool w1_builds() {
   static const bool on = [] {
@@ -2548,34 +2555,46 @@ hipError_t launch_propagate(const KParams& P, int64_t n, const SegIn& in, const 
   ART_DBG("propagate_kernel")
   if ((e = hipGetLastError()) != hipSuccess) return e;
   if (out.donate > 0) {  // the donated tail rays, packed into full waves (at most waves x donate of them)
+    // with the tail kernel (ART_TAIL != 0, Vern6 without saveat) the packed continuation donates
+    // in its turn: its drained waves' last rays (at most ART_TAIL_DONATE each, default 4) go to
+    // the second-level records, and tail_kernel resumes each of those on a wave of its own
+    const bool tail = tail_rays() != 0 && !rk4 && out.ntimes < 2 && out.cont2;
     SegOut oc = out;
     oc.cont_mode = 1;
-    oc.donate = 0;
+    oc.cont_src = out.cont;
+    oc.cont_src_count = out.cont_count;
+    oc.donate = tail ? tail_donate() : 0;
+    oc.cont = out.cont2;
+    oc.cont_count = out.cont2_count;
     const int64_t maxc = (int64_t)grid * (BLOCK / 64) * out.donate;
     const int cgrid = (int)((maxc + BLOCK - 1) / BLOCK);
     // GR continuations at 1 wave/SIMD: no spills (68 VGPRs spill to scratch at 2). A/B on the
     // configs[3] bench line: 3.21e8 -> 3.35e8 ray-steps/s, bit-identical
     // (profiles/r02h_continuation_w1_ab.txt); flat stays at 2 (measured -3.5% at 1).
     const KFn cfn = (w1_builds() && sch && !rk4 && out.ntimes < 2) ? propagate_kernel<ART_VERN6, GEOM_GR, false, true, 1> : fn;
-    // few donated rays: one wave each (tail_kernel, up to one per SIMD; ART_TAIL=0 off); it
-    // leaves the work queue drained for the packed continuation below, or returns at once and
-    // leaves every record to it
-    if (tail_rays() > 0 && !rk4 && out.ntimes < 2) {
-      int dev = 0, ncu = 0;
-      (void)hipGetDevice(&dev);
-      (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-      const int max_rays = tail_rays() == 1 ? ncu * 4 : tail_rays();
-      const int tgrid = (int)(maxc < max_rays ? maxc : max_rays);
-      using TFn = void (*)(const KParams, const int64_t, const SegIn, const SegOut, const int32_t, const int32_t,
-                           unsigned long long*);
-      const TFn tfn = flat ? tail_kernel<GEOM_FLAT> : (sch ? tail_kernel<GEOM_GR> : tail_kernel<GEOM_ANY>);
-      hipLaunchKernelGGL(tfn, dim3(tgrid), dim3(64), 0, s, P, n, in, oc, max_crossings, max_rays, stats);
-      ART_DBG("tail_kernel")
-      if ((e = hipGetLastError()) != hipSuccess) return e;
-    }
     hipLaunchKernelGGL(cfn, dim3(cgrid), dim3(BLOCK), 0, s, P, n, in, oc, max_crossings, queue, stats);
     ART_DBG("continuation")
     if ((e = hipGetLastError()) != hipSuccess) return e;
+    if (tail) {
+      int dev = 0, ncu = 0;
+      (void)hipGetDevice(&dev);
+      (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+      // one wave per ray, at most one per SIMD of the device (ART_TAIL=k: k waves); more
+      // second-level rays queue behind them
+      const int64_t maxc2 = (int64_t)cgrid * (BLOCK / 64) * oc.donate;
+      const int waves = tail_rays() == 1 ? ncu * 4 : tail_rays();
+      const int tgrid = (int)(maxc2 < waves ? maxc2 : waves);
+      SegOut ot = out;
+      ot.cont = out.cont2;
+      ot.cont_count = out.cont2_count;
+      ot.cont_queue = out.cont2_queue;
+      using TFn = void (*)(const KParams, const int64_t, const SegIn, const SegOut, const int32_t, const int32_t,
+                           unsigned long long*);
+      const TFn tfn = flat ? tail_kernel<GEOM_FLAT> : (sch ? tail_kernel<GEOM_GR> : tail_kernel<GEOM_ANY>);
+      if (tgrid > 0) hipLaunchKernelGGL(tfn, dim3(tgrid), dim3(64), 0, s, P, n, in, ot, max_crossings, waves, stats);
+      ART_DBG("tail_kernel")
+      if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
   }
   if (ev1 && (e = hipEventRecord(ev1, s)) != hipSuccess) return e;
   hipLaunchKernelGGL(finalize_kernel, dim3(g1), dim3(256), 0, s, P, n, in, out);
