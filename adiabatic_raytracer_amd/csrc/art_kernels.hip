@@ -29,6 +29,23 @@ enum { ST_ATTEMPTS = 0, ST_ACCEPTED, ST_ROOT_STEPS, ST_SCAN_EVALS, ST_INTERP_EVA
 
 constexpr int CHUNK = 64;
 
+#ifdef ART_TRACE
+// dev build: per-attempt state of ONE ray (g_trace_ray) from whichever kernel integrates it:
+// [kernel (0 bulk, 1 tail), mode, hs, tau, EEst2, y (7), kk (7)] per attempt
+__device__ int g_trace_ray = -1;
+__device__ unsigned g_trace_n = 0;
+constexpr int TRACE_REC = 21, TRACE_MAX = 4096;
+__device__ double g_trace[TRACE_MAX * TRACE_REC];
+__device__ inline void trace_attempt(int kern, int mode, double hs, double tau, double e2, const double* y,
+                                     const double* kk) {
+  const unsigned k = atomicAdd(&g_trace_n, 1u);
+  if (k >= TRACE_MAX) return;
+  double* r = g_trace + (size_t)k * TRACE_REC;
+  r[0] = kern; r[1] = mode; r[2] = hs; r[3] = tau; r[4] = e2;
+  for (int i = 0; i < 7; ++i) { r[5 + i] = y[i]; r[12 + i] = kk[i]; }
+}
+#endif
+
 // ---------------------------------------------------------------------------
 // One Verner 6(5) attempt from (u, k1 = f(u)) over h: writes u_{n+1}, its FSAL derivative
 // k9 and returns the RMS error norm of OrdinaryDiffEq (abstol + max(|u|,|u_new|) reltol).
@@ -671,14 +688,20 @@ __global__ __launch_bounds__(BLOCK, WPS) void propagate_kernel(const KParams P_i
         double acc = 0.0;
 #pragma unroll
         for (int i = 0; i < 7; ++i) {
-          double e = T.e_f * f[i] + T.e_A * kA[i] + T.e_k * kk[i];
+          // explicit FMAs: the contraction of a sum of three products is the compiler's choice
+          // (it prefers the product with fewer uses), so written out it could round differently
+          // in the tail kernel's straight-line code (tests/test_gpu_tail_donation.py)
+          double e = fma(T.e_k, kk[i], fma(T.e_A, kA[i], T.e_f * f[i]));
 #pragma unroll
-          for (int q = 1; q < LDS_SLOTS; ++q) e += T.e_L[q] * L[(q * 7 + i) * BLOCK];
+          for (int q = 1; q < LDS_SLOTS; ++q) e = fma(T.e_L[q], L[(q * 7 + i) * BLOCK], e);
           e *= hs;
           const double q = e * frcp(P.abstol + fmax_abs(u[i], y[i]) * P.reltol);
           acc += q * q;
         }
         EEst2 = acc * (1.0 / 7.0);
+#ifdef ART_TRACE
+        if (ray == g_trace_ray) trace_attempt(0, mode, hs, tau, EEst2, y, kk);
+#endif
       }
     }
 
@@ -904,6 +927,12 @@ __global__ __launch_bounds__(BLOCK, WPS) void propagate_kernel(const KParams P_i
     ART_LBOOL2 hit = false, root_done = false;
     // a crossing in (θ_last, θ_ip]: polish it on the true trajectory (mode ROOT), from t_int
     auto open_root = [&](double t_int) {
+#ifdef ART_TRACE
+      if (ray == g_trace_ray) {
+        const double v[7] = {double(ip), double(last_j), last_c, i_cg, t_int, double(lc_ok), thgrid[ip]};
+        trace_attempt(10, mode, hs, tau, 0.0, v, v);
+      }
+#endif
       const double thg = thgrid[ip];
       const double last_th = thgrid[last_j];
       hit = true;
@@ -1335,6 +1364,13 @@ __device__ inline double scan_point_regs(const KParams& P, const double* u0, con
 template <int GEOM>
 __device__ inline void tail_rhs(const KParams& P, int lane, const double* y, double ty, double t, double erg,
                                 double* kk, double* aux) {
+#if defined(ART_TAIL_PLAIN_RHS)
+  rhs(P, true, y, ty, erg, kk);  // dev A/B: the bulk kernel's RHS call
+  if (GEOM != GEOM_ANY) rhs_photon_gj(P, y, ty, erg, kk, aux); else rhs_photon(P, y, ty, erg, kk, aux);
+  return;
+#elif defined(ART_TAIL_PLAIN_T)
+  t = fexp(ty);
+#endif
   if constexpr (GEOM != GEOM_ANY) {
     const double arg = (lane == 1) ? psi_of(P, y[2], t) : y[1];
     double sn, cs;
@@ -1412,6 +1448,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
       // ---- e^τ of the eight stages at once (lane s: stage s) ----
       const double tl = fexp(tau + my_ct * hs);
       // ---- the Vern6 stages, unrolled (c_vern6's rows with their coefficients folded) ----
+      // The bulk kernel forms each stage point in the order acc = cf f (rounded), then
+      // acc = fma(c_q, L_q, acc) per parked stage, y = fma(h, acc, u): its product cf f and the
+      // stage loop's additions sit in different basic blocks, so they are never contracted into
+      // one FMA. Written straight-line, `cf * f + c * L` would be (fma(cf, f, c L)); the explicit
+      // fma calls below keep the bulk kernel's roundings, bit for bit.
       double kA[7], L0[7], L1[7], L2[7], L3[7], L4[7], y[7], kk[7], aux[2] = {0.0, 0.0};
       auto stage = [&](int s, double ct) {
         const double ty = tau + ct * hs;
@@ -1437,7 +1478,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
 #pragma unroll
       for (int i = 0; i < 7; ++i) {
         double acc = V::a41 * f[i];
-        acc += V::a43 * L0[i];
+        acc = fma(V::a43, L0[i], acc);
         y[i] = u[i] + hs * acc;
       }
       stage(2, V::c4);
@@ -1446,8 +1487,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
 #pragma unroll
       for (int i = 0; i < 7; ++i) {
         double acc = V::a51 * f[i];
-        acc += V::a53 * L0[i];
-        acc += V::a54 * L1[i];
+        acc = fma(V::a53, L0[i], acc);
+        acc = fma(V::a54, L1[i], acc);
         y[i] = u[i] + hs * acc;
       }
       stage(3, V::c5);
@@ -1456,9 +1497,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
 #pragma unroll
       for (int i = 0; i < 7; ++i) {
         double acc = V::a61 * f[i];
-        acc += V::a63 * L0[i];
-        acc += V::a64 * L1[i];
-        acc += V::a65 * L2[i];
+        acc = fma(V::a63, L0[i], acc);
+        acc = fma(V::a64, L1[i], acc);
+        acc = fma(V::a65, L2[i], acc);
         y[i] = u[i] + hs * acc;
       }
       stage(4, V::c6);
@@ -1467,10 +1508,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
 #pragma unroll
       for (int i = 0; i < 7; ++i) {
         double acc = V::a71 * f[i];
-        acc += V::a73 * L0[i];
-        acc += V::a74 * L1[i];
-        acc += V::a75 * L2[i];
-        acc += V::a76 * L3[i];
+        acc = fma(V::a73, L0[i], acc);
+        acc = fma(V::a74, L1[i], acc);
+        acc = fma(V::a75, L2[i], acc);
+        acc = fma(V::a76, L3[i], acc);
         y[i] = u[i] + hs * acc;
       }
       stage(5, V::c7);
@@ -1479,11 +1520,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
 #pragma unroll
       for (int i = 0; i < 7; ++i) {
         double acc = V::a81 * f[i];
-        acc += V::a83 * L0[i];
-        acc += V::a84 * L1[i];
-        acc += V::a85 * L2[i];
-        acc += V::a86 * L3[i];
-        acc += V::a87 * L4[i];
+        acc = fma(V::a83, L0[i], acc);
+        acc = fma(V::a84, L1[i], acc);
+        acc = fma(V::a85, L2[i], acc);
+        acc = fma(V::a86, L3[i], acc);
+        acc = fma(V::a87, L4[i], acc);
         y[i] = u[i] + hs * acc;
       }
       stage(6, 1.0);
@@ -1492,10 +1533,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
 #pragma unroll
       for (int i = 0; i < 7; ++i) {
         double acc = fma(V::a91, f[i], V::a98 * kA[i]);
-        acc += V::a94 * L1[i];
-        acc += V::a95 * L2[i];
-        acc += V::a96 * L3[i];
-        acc += V::a97 * L4[i];
+        acc = fma(V::a94, L1[i], acc);
+        acc = fma(V::a95, L2[i], acc);
+        acc = fma(V::a96, L3[i], acc);
+        acc = fma(V::a97, L4[i], acc);
         y[i] = u[i] + hs * acc;
       }
       stage(7, 1.0);
@@ -1507,16 +1548,19 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
         double acc = 0.0;
 #pragma unroll
         for (int i = 0; i < 7; ++i) {
-          double e = V::e1 * f[i] + V::e8 * kA[i] + V::e9 * kk[i];
-          e += V::e4 * L1[i];
-          e += V::e5 * L2[i];
-          e += V::e6 * L3[i];
-          e += V::e7 * L4[i];
+          double e = fma(V::e9, kk[i], fma(V::e8, kA[i], V::e1 * f[i]));  // as the bulk kernel
+          e = fma(V::e4, L1[i], e);
+          e = fma(V::e5, L2[i], e);
+          e = fma(V::e6, L3[i], e);
+          e = fma(V::e7, L4[i], e);
           e *= hs;
           const double q = e * frcp(P.abstol + fmax_abs(u[i], y[i]) * P.reltol);
           acc += q * q;
         }
         EEst2 = acc * (1.0 / 7.0);
+#ifdef ART_TRACE
+        if (lane == 0 && ray == g_trace_ray) trace_attempt(1, mode, hs, tau, EEst2, y, kk);
+#endif
       }
       // ---- controller (STEP) ----
       bool scan = false;
@@ -1628,6 +1672,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
       bool hit = false, root_done = false;
       auto thg = [&](int j) { return double(j) / double(npts - 1); };
       auto open_root = [&](double t_int) {
+#ifdef ART_TRACE
+        if (lane == 0 && ray == g_trace_ray) {
+          const double v[7] = {double(ip), double(last_j), last_c, i_cg, t_int, double(lc_ok), thg(ip)};
+          trace_attempt(11, mode, hs, tau, 0.0, v, v);
+        }
+#endif
         const double tg = thg(ip), lth = thg(last_j);
         hit = true;
         hroot = hs;
@@ -2169,26 +2219,23 @@ __global__ __launch_bounds__(256) void sample_kernel(const KParams P, const doub
         }
       }
       const bool unc = active && !cert;
-      const unsigned long long mU = __ballot(unc), mC = __ballot(active && cert);
-      const int nU = __popcll(mU), nC = __popcll(mC);
+      const unsigned long long mU = __ballot(unc);
+      const int nU = __popcll(mU);
       if (unc) ssrc[wb + __popcll(mU & lt)] = (unsigned char)lane;
-      if (active && cert) ssrc[256 + wb + __popcll(mC & lt)] = (unsigned char)lane;
       ssb[threadIdx.x] = signbit(c_prev) ? 1u : 0u;
       snz[threadIdx.x] = (c_prev != 0.0) ? 1u : 0u;
       wave_lds_sync();
-      // items: (uncertified lane, point 1..nper) point-major, then (certified lane, point nper)
-      const int totU = nU * nper, tot = totU + nC;
+      // items: (uncertified lane, point 1..nper) point-major. A certified step needs no point at
+      // all: its last point -- the next step's bracket start -- has the certified sign, and
+      // c_prev is only ever read for its sign (the next certificate, the bit-0 sign and
+      // nonzero-ness of the next scan), so it keeps the value it had (round 3: until then
+      // every certified lane evaluated its last point, 1 item per lane per step)
+      const int totU = nU * nper, tot = totU;
       for (int w0 = 0; w0 < tot; w0 += 64) {
         const int t = w0 + lane;
         if (t < tot) {
-          int src, j;
-          if (t < totU) {
-            j = t / nU + 1;
-            src = ssrc[wb + t % nU];
-          } else {
-            j = nper;
-            src = ssrc[256 + wb + (t - totU)];
-          }
+          const int j = t / nU + 1;
+          const int src = ssrc[wb + t % nU];
           const double* S = sline + wb + src;
           const double sc = s0 + (s1 - s0) * double(j) / double(np - 1);
           double xl[3];
@@ -2209,8 +2256,8 @@ __global__ __launch_bounds__(256) void sample_kernel(const KParams P, const doub
         if (unc) {
           const unsigned sb = ssb[threadIdx.x], nz = snz[threadIdx.x];
           br = (sb ^ (sb << 1)) & nz & (nz << 1) & (((1u << np) - 1u) & ~1u);
+          c_prev = slast[threadIdx.x];
         }
-        c_prev = slast[threadIdx.x];
         s_prev = s0 + (s1 - s0) * double(nper) / double(np - 1);
       }
       // queue the brackets, each lane's in its order along the line
@@ -2666,3 +2713,21 @@ hipError_t launch_eval_condition(const KParams& P, int64_t n, const double* u, c
 }
 
 }  // namespace art
+
+#ifdef ART_TRACE
+// dev build only: trace one ray (-1: off); read back its per-attempt records (TRACE_REC doubles)
+extern "C" int art_debug_trace_set(int ray) {
+  const unsigned zero = 0;
+  if (hipMemcpyToSymbol(HIP_SYMBOL(art::g_trace_ray), &ray, sizeof ray) != hipSuccess) return -2;
+  return hipMemcpyToSymbol(HIP_SYMBOL(art::g_trace_n), &zero, sizeof zero) == hipSuccess ? 0 : -2;
+}
+extern "C" int art_debug_trace_get(double* out, int max_records, int* count) {
+  unsigned n = 0;
+  if (hipDeviceSynchronize() != hipSuccess) return -2;
+  if (hipMemcpyFromSymbol(&n, HIP_SYMBOL(art::g_trace_n), sizeof n) != hipSuccess) return -2;
+  n = n < (unsigned)art::TRACE_MAX ? n : (unsigned)art::TRACE_MAX;
+  n = n < (unsigned)max_records ? n : (unsigned)max_records;
+  *count = (int)n;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(art::g_trace), (size_t)n * art::TRACE_REC * sizeof(double)) == hipSuccess ? 0 : -2;
+}
+#endif
