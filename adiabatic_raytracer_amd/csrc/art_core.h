@@ -17,6 +17,20 @@
 
 #include "../../include/art.h"
 
+// FMA contraction. libart.so is compiled with -ffp-contract=on: a multiply and an add are
+// fused only inside one source expression, so a shared function rounds the same in every
+// kernel it is inlined into (the bulk integrator and the one-wave-per-ray tail kernel must
+// agree bit for bit; with the backend's cross-statement fusion ("fast") the choice depends on
+// how many uses each product has at the inlined site, and it differed between the two in the
+// scan and the back-transform). The ray equations' right-hand side keeps "fast" contraction
+// (ART_FP_FAST at the top of its functions): it is 2% of the headline kernel's time faster
+// that way, and its roundings were checked equal between the kernels (tools/exp_tail_trace*.py).
+#if defined(__clang__)
+#define ART_FP_FAST _Pragma("clang fp contract(fast)")
+#else
+#define ART_FP_FAST
+#endif
+
 namespace art {
 
 // Constants.jl:3-5
@@ -35,6 +49,7 @@ __host__ __device__ inline double msign(double x) { return copysign(1.0, x); }  
 // angles θ and ψ = φ - ωt stay small, so the large-argument (Payne-Hanek) path that
 // ocml's sincos carries -- ~200 instructions of code per call site -- is never needed.
 __host__ __device__ inline void msincos(double x, double& s, double& c) {
+  ART_FP_FAST
   const double n = rint(x * 0.63661977236758134308);
   double r = fma(-n, 1.5707963267948966, x);
   r = fma(-n, 6.123233995736766e-17, r);
@@ -119,6 +134,7 @@ __host__ __device__ inline double frcp(double x) {
 // (tests/test_corecheck.py); no overflow/underflow/NaN special-casing beyond what the
 // arithmetic propagates (the integrator's arguments are moderate ln t and ln EEst values).
 __host__ __device__ inline double exp_fma(double x) {
+  ART_FP_FAST
   const double k = rint(x * 1.4426950408889634);
   double r = fma(-k, 0.6931471805599453, x);
   r = fma(-k, 2.3190468138462996e-17, r);
@@ -271,6 +287,7 @@ inline KParams make_kparams(const art_params& p) {
 // on r <= 10 km, the keyword default that hot-path callers never override (:455).
 template <class T>
 __host__ __device__ inline void metric_tr(const T& r, double rs, T& gtt, T& grr) {
+  ART_FP_FAST
   if (rs == 0.0) {  // flat space: exactly what both branches below give for rs = 0
     grr = 1.0;
     gtt = -1.0;
@@ -287,6 +304,7 @@ __host__ __device__ inline void metric_tr(const T& r, double rs, T& gtt, T& grr)
 
 template <class T>
 __host__ __device__ inline void metric_tr_d(const T& r, double rs, T& gtt, T& grr, T& dgtt, T& dgrr) {
+  ART_FP_FAST
   if (rs == 0.0) {  // flat space (wave-uniform branch): no divisions
     grr = 1.0;
     gtt = -1.0;
@@ -329,6 +347,7 @@ struct DipoleAng {
 template <class T>
 __host__ __device__ inline DipoleAng<T> dipole_ang(const KParams& P, const T& st, const T& ct, const T& sp,
                                                    const T& cp) {
+  ART_FP_FAST
   DipoleAng<T> d;
   d.a1 = P.cm * ct + P.sm * st * cp;
   d.a2 = P.cm * st - P.sm * ct * cp;
@@ -346,6 +365,7 @@ __host__ __device__ inline DipoleAng<T> dipole_ang(const KParams& P, const T& st
 // Boundary-layer increment of ωp (RayTracer.jl:1158-1161), r >= rNS.
 template <class T>
 __host__ __device__ inline T layer_wp(const KParams& P, const T& r, double rmax) {
+  ART_FP_FAST
   const T x = P.rNS / r;
   return P.pole_val * x * msqrt(x) * mexp(-(r - rmax * P.bndry_lyr) / (0.1 * rmax));
 }
@@ -363,6 +383,7 @@ __host__ __device__ inline T layer_wp(const KParams& P, const T& r, double rmax)
 template <class T>
 __host__ __device__ inline void rhs_photon(const KParams& P, const T* u, const T& tau, double erg, T* du,
                                            T* aux = nullptr) {
+  ART_FP_FAST
   const T t = fexp(tau);
   const T r = u[0];
   const T E = -u[6];
@@ -470,6 +491,7 @@ __host__ __device__ inline void rhs_photon(const KParams& P, const T* u, const T
 // ψ = φ - ω (time0 + t), time0 = 0 (MainRunner.jl:177): the argument of rhs_photon_gj's second sincos
 template <class T>
 __host__ __device__ inline T psi_of(const KParams& P, const T& phi, const T& t) {
+  ART_FP_FAST
   return phi - P.omega * t;
 }
 
@@ -483,6 +505,7 @@ __host__ __device__ inline void rhs_photon_gj_tr(const KParams& P, const T* u, c
 template <class T>
 __host__ __device__ inline void rhs_photon_gj(const KParams& P, const T* u, const T& tau, double erg, T* du,
                                               T* aux = nullptr) {
+  ART_FP_FAST
   const T t = fexp(tau);
   T st, ct, sp, cp;
   msincos(u[1], st, ct);
@@ -493,6 +516,7 @@ __host__ __device__ inline void rhs_photon_gj(const KParams& P, const T* u, cons
 template <class T>
 __host__ __device__ inline void rhs_photon_gj_tr(const KParams& P, const T* u, const T& t, const T& st, const T& ct,
                                                  const T& sp, const T& cp, double erg, T* du, T* aux) {
+  ART_FP_FAST
   const bool flat = P.rs_eff == 0.0;
   const T r = u[0];
   const T E = -u[6];
@@ -585,6 +609,7 @@ __host__ __device__ inline void rhs_photon_gj_tr(const KParams& P, const T* u, c
 // energy erg, no clamp, no NS cut, du[7] = 0.
 template <class T>
 __host__ __device__ inline void rhs_axion(const KParams& P, const T* u, const T& tau, double erg, T* du) {
+  ART_FP_FAST
   const T t = fexp(tau);
   const T r = u[0];
   T st, ct;

@@ -172,7 +172,7 @@ def dispatch(items, launch, streams, poll_s=2e-4):
     return order
 
 
-def run_scan(rays: int, n_points: int | None = None, seed: int = 1769, run=None, streams: int = 8):
+def run_scan(rays: int, n_points: int | None = None, seed: int = 1769, run=None, streams: int = 8, donate: int = 0):
     """This rank's share of the grid (run_points, or `run` point by point); with
     WORLD_SIZE > 1 the records are gathered on every rank (all_gather_object) and returned in
     grid order."""
@@ -183,7 +183,7 @@ def run_scan(rays: int, n_points: int | None = None, seed: int = 1769, run=None,
     grid = scan_grid()[:n_points]
     idx = points_of_rank(len(grid), rank, world)
     if run is None:
-        recs, _ = run_points([grid[i] for i in idx], rays, seed, device=local, streams=streams)
+        recs, _ = run_points([grid[i] for i in idx], rays, seed, device=local, streams=streams, donate=donate)
         mine = [dict(r, point=i) for r, i in zip(recs, idx)]
     else:
         mine = [dict(run(grid[i], rays, seed, device=local), point=i) for i in idx]
@@ -201,6 +201,9 @@ def main():
     ap.add_argument("--seed", type=int, default=1769)
     ap.add_argument("--out", default=None)
     ap.add_argument("--streams", type=int, default=8)
+    ap.add_argument("--donate", type=int, default=16,
+                    help="tail donation lanes (art_set_tail_donation): the drained tails resume packed, then one "
+                         "wave per ray (tail kernel)")
     args = ap.parse_args()
     # concurrent kernels need hardware queues: one per stream in flight (read at HIP init)
     want = min(16, max(4, args.streams))
@@ -213,7 +216,7 @@ def main():
         local = int(os.environ.get("LOCAL_RANK", "0"))
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    recs = run_scan(args.rays, args.points, args.seed, streams=args.streams)
+    recs = run_scan(args.rays, args.points, args.seed, streams=args.streams, donate=args.donate)
     if int(os.environ.get("RANK", "0")) == 0:
         lines = "\n".join(json.dumps(r) for r in recs)
         if args.out:
