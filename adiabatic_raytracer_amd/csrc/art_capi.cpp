@@ -54,11 +54,14 @@ struct DeviceCtx {
   int32_t donate = 0;            // tail donation (art_set_tail_donation): lanes per wave, 0 = off
   std::vector<std::pair<void*, size_t>> pool;  // host-entry staging buffers (grow-only, used under g_mu by the
                                                // synchronous *_host calls only)
-  // the chunked host pipeline of art_propagate_host (propagate_host_chunked): its streams,
-  // its pinned input and output staging (grow-only) and one completion event per chunk
+  // the chunked host pipeline of art_propagate_host (propagate_host_chunked): its compute
+  // streams, one stream for the uploads and one for the downloads, its pinned input and
+  // output staging (grow-only) and three events per chunk (inputs in HBM, computed, outputs
+  // in pinned memory)
   std::vector<hipStream_t> pstreams;
+  hipStream_t h2d = nullptr, d2h = nullptr;
   std::vector<std::pair<void*, size_t>> pinned;
-  std::vector<hipEvent_t> pdone;
+  std::vector<hipEvent_t> pev;
 };
 std::vector<DeviceCtx> g_ctx;
 
@@ -530,33 +533,43 @@ int art_propagate_traj_device(const art_params* p, int64_t n, const double* x0, 
 
 namespace {
 // art_propagate_host for large batches: a pipeline of chunks (the reference call
-// site MainRunner.jl:179-190 hands over host arrays). Every chunk's inputs are gathered from the
-// caller's arrays into pinned staging by the copy pool and its whole sequence -- H2D, the
-// propagate launch, D2H of its outputs -- is enqueued at once on stream k % slots, so the GPU
-// always holds `slots` chunks in flight (tail donation: one chunk's drain tail is filled by the
-// next) and never waits for the host. The host then waits for the chunks in order and
-// scatters each one's outputs into the caller's arrays while the later ones still compute.
-// (A first version reused `slots` staging buffers and could enqueue chunk k only after chunk
-// k - slots was drained; the concurrent chunks finished together and the GPU idled while the
-// host caught up: 132 ms per 1e7 rays against 128 for the single launch,
-// profiles/r03d_host_path.jsonl.) Per-ray results do not depend on the batch split
-// (tests/test_edges.py), so the outputs equal the single launch's bit for bit. The statistics
-// and kernel time of the call are the sums over its chunks.
+// site MainRunner.jl:179-190 hands over host arrays). Three kinds of streams:
+//   * uploads (one stream): chunk k's inputs, gathered from the caller's arrays into pinned
+//     staging by the copy pool, go to HBM one chunk after another, all enqueued up front;
+//   * compute (`slots` streams, chunk k on stream k % slots): each chunk's launch waits for its
+//     own upload only, so two chunks in flight fill each other's drain tails (with tail
+//     donation) and the GPU never waits behind a download;
+//   * downloads (one stream): chunk k's outputs leave as soon as chunk k is computed.
+// The host then scatters the chunks' outputs into the caller's arrays in order while the later
+// ones still compute. Only the first chunk's upload and the last chunk's download and scatter
+// are not hidden behind compute, so those two chunks are a quarter of the others.
+// (Version 2 ran each chunk's copies on its compute stream: a chunk's upload then waited for
+// the download of the chunk before it on that stream, and the GPU idled 6-8 ms between chunks,
+// profiles/r03o_host_timeline.txt. Version 1 reused `slots` staging buffers and enqueued
+// chunk k only after chunk k - slots was drained.) Per-ray results do not depend on the batch
+// split (tests/test_edges.py), so the outputs equal the single launch's bit for bit. The
+// statistics and kernel time of the call are the sums over its chunks.
 int propagate_host_chunked(DeviceCtx* c, const art_params* p, int64_t n, const double* x0, const double* k0,
                            const double* erg, const double* dw, const double* ln_t0, const int8_t* species,
                            int32_t max_crossings, art_segment_out* out, art_crossing_buf* xc, int nchunks,
                            int nslots) {
   const int cap = (xc && xc->count) ? xc->capacity : 0;
-  const int64_t K = nchunks;
+  const int64_t K = std::max(2, nchunks);
   auto up = [](size_t b) { return (b + 255) & ~size_t(255); };
   // blob layouts of a chunk of m rays (identical in pinned staging and in HBM)
   auto in_bytes = [&](int64_t m) { return up((size_t)m * 9 * sizeof(double)) + up((size_t)m); };
   auto cnt_off = [&](int64_t m) { return up((size_t)m * 8 * sizeof(double) + (size_t)m * 3 * sizeof(int32_t)); };
   auto xd_off = [&](int64_t m) { return cnt_off(m) + up((size_t)m * sizeof(int32_t)); };
   auto out_bytes = [&](int64_t m) { return cap ? xd_off(m) + (size_t)cap * m * 9 * sizeof(double) : cnt_off(m); };
+  // chunk boundaries: weights 1/4, 1, ..., 1, 1/4
   std::vector<int64_t> lo(K + 1);
+  const double wsum = 0.5 + double(K - 2);
+  for (int64_t k = 0; k <= K; ++k) {
+    const double wk = k == 0 ? 0.0 : (k == K ? wsum : 0.25 + double(k - 1));
+    lo[k] = (int64_t)((double)n * (wk / wsum));
+  }
+  lo[K] = n;
   std::vector<size_t> ioff(K + 1, 0), ooff(K + 1, 0);
-  for (int64_t k = 0; k <= K; ++k) lo[k] = k * n / K;
   for (int64_t k = 0; k < K; ++k) {
     ioff[k + 1] = ioff[k] + in_bytes(lo[k + 1] - lo[k]);
     ooff[k + 1] = ooff[k] + out_bytes(lo[k + 1] - lo[k]);
@@ -566,17 +579,24 @@ int propagate_host_chunked(DeviceCtx* c, const art_params* p, int64_t n, const d
     if (!c->pstreams.empty()) HIP_OK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
     c->pstreams.push_back(st);
   }
-  while ((int64_t)c->pdone.size() < K) {
+  if (!c->h2d) HIP_OK(hipStreamCreateWithFlags(&c->h2d, hipStreamNonBlocking));
+  if (!c->d2h) HIP_OK(hipStreamCreateWithFlags(&c->d2h, hipStreamNonBlocking));
+  while ((int64_t)c->pev.size() < 3 * K) {
     hipEvent_t ev;
     HIP_OK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-    c->pdone.push_back(ev);
+    c->pev.push_back(ev);
   }
+  hipEvent_t *ev_in = c->pev.data(), *ev_done = ev_in + K, *ev_out = ev_in + 2 * K;
   int rc;
   void *pi, *po, *di_, *do_;
   if ((rc = pinned_get(c, 0, ioff[K], &pi)) || (rc = pinned_get(c, 1, ooff[K], &po)) ||
       (rc = pool_get(c, 16, ioff[K], &di_)) || (rc = pool_get(c, 17, ooff[K], &do_)))
     return rc;
   char *pin_in = (char*)pi, *pin_out = (char*)po, *dev_in = (char*)di_, *dev_out = (char*)do_;
+  // the staging buffers may still be read by the previous call's streams only if it failed
+  // half-way; a completed call has drained all three kinds
+  HIP_OK(hipStreamSynchronize(c->h2d));
+  HIP_OK(hipStreamSynchronize(c->d2h));
   using Seg = CopyPool::Seg;
   std::vector<int> rings;
   // ART_HOST_TRACE=1: the host side of every chunk to stderr (gathers, waits, scatters)
@@ -584,8 +604,12 @@ int propagate_host_chunked(DeviceCtx* c, const art_params* p, int64_t n, const d
   auto clk = [] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
   const double t_start = clk();
   const int32_t donate = nslots > 1 ? 16 : 0;
-  for (int64_t k = 0; k < K; ++k) {
-    hipStream_t st = c->pstreams[k % nslots];
+  // Submission order matters: the runtime keeps the copies of all streams in the order they
+  // were submitted, so a download submitted before an upload holds the upload back until the
+  // download's chunk is computed (a first version interleaved them per chunk and the chunks ran
+  // one at a time, profiles/r03p_host_timeline.txt). So: upload 0, compute 0, the other uploads,
+  // the other computes, then the downloads.
+  auto upload = [&](int64_t k) -> int {
     const int64_t l0 = lo[k], m = lo[k + 1] - lo[k];
     char* bi = pin_in + ioff[k];
     double* d = (double*)bi;
@@ -600,10 +624,21 @@ int propagate_host_chunked(DeviceCtx* c, const art_params* p, int64_t n, const d
     g.push_back({bi + up((size_t)m * 9 * sizeof(double)), species + l0, (size_t)m});
     const double tg0 = clk();
     copy_pool().run(g);
-    if (trace) std::fprintf(stderr, "[art-host] t=%.2f gather lo=%lld %.2f ms\n", tg0 - t_start, (long long)l0, clk() - tg0);
+    const double tg1 = clk();
+    HIP_OK(hipMemcpyAsync(dev_in + ioff[k], bi, in_bytes(m), hipMemcpyHostToDevice, c->h2d));
+    HIP_OK(hipEventRecord(ev_in[k], c->h2d));
+    if (trace)
+      std::fprintf(stderr, "[art-host] t=%.2f upload lo=%lld m=%lld gather %.2f ms submit %.2f ms\n", tg0 - t_start,
+                   (long long)l0, (long long)m, tg1 - tg0, clk() - tg1);
+    return ART_OK;
+  };
+  auto compute = [&](int64_t k) -> int {
+    const double t0 = clk();
+    hipStream_t st = c->pstreams[k % nslots];
+    const int64_t m = lo[k + 1] - lo[k];
     char* dbi = dev_in + ioff[k];
     char* dbo = dev_out + ooff[k];
-    HIP_OK(hipMemcpyAsync(dbi, bi, in_bytes(m), hipMemcpyHostToDevice, st));
+    HIP_OK(hipStreamWaitEvent(st, ev_in[k], 0));
     const double* di = (const double*)dbi;
     double* dd = (double*)dbo;
     int32_t* di32 = (int32_t*)(dd + 8 * m);
@@ -618,18 +653,35 @@ int propagate_host_chunked(DeviceCtx* c, const art_params* p, int64_t n, const d
       dxb = art_crossing_buf{cap, cnt, x, x + 3 * cap * m, x + 6 * cap * m, x + 7 * cap * m, x + 8 * cap * m};
       dxbp = &dxb;
     }
-    if ((rc = propagate_device_impl(p, m, di, di + 3 * m, di + 6 * m, di + 7 * m, di + 8 * m,
+    int rc2 = propagate_device_impl(p, m, di, di + 3 * m, di + 6 * m, di + 7 * m, di + 8 * m,
                                     (const int8_t*)(dbi + up((size_t)m * 9 * sizeof(double))), max_crossings, &dso,
-                                    dxbp, st, TrajArgs(), donate)))
-      return rc;
+                                    dxbp, st, TrajArgs(), donate);
+    if (rc2) return rc2;
     rings.push_back(c->last);
-    HIP_OK(hipMemcpyAsync(pin_out + ooff[k], dbo, out_bytes(m), hipMemcpyDeviceToHost, st));
-    HIP_OK(hipEventRecord(c->pdone[k], st));
-  }
+    HIP_OK(hipEventRecord(ev_done[k], st));
+    if (trace) std::fprintf(stderr, "[art-host] t=%.2f compute k=%lld submit %.2f ms\n", t0 - t_start, (long long)k, clk() - t0);
+    return ART_OK;
+  };
+  auto download = [&](int64_t k) -> int {
+    const double t0 = clk();
+    HIP_OK(hipStreamWaitEvent(c->d2h, ev_done[k], 0));
+    HIP_OK(hipMemcpyAsync(pin_out + ooff[k], dev_out + ooff[k], out_bytes(lo[k + 1] - lo[k]), hipMemcpyDeviceToHost,
+                          c->d2h));
+    HIP_OK(hipEventRecord(ev_out[k], c->d2h));
+    if (trace) std::fprintf(stderr, "[art-host] t=%.2f download k=%lld submit %.2f ms\n", t0 - t_start, (long long)k, clk() - t0);
+    return ART_OK;
+  };
+  if ((rc = upload(0)) || (rc = compute(0))) return rc;
+  for (int64_t k = 1; k < K; ++k)
+    if ((rc = upload(k))) return rc;
+  for (int64_t k = 1; k < K; ++k)
+    if ((rc = compute(k))) return rc;
+  for (int64_t k = 0; k < K; ++k)
+    if ((rc = download(k))) return rc;
   // the chunks' outputs, in order: pinned staging -> the caller's arrays
   for (int64_t k = 0; k < K; ++k) {
     const double tw0 = clk();
-    HIP_OK(hipEventSynchronize(c->pdone[k]));
+    HIP_OK(hipEventSynchronize(ev_out[k]));
     const double tw1 = clk();
     const int64_t l0 = lo[k], m = lo[k + 1] - lo[k];
     const char* bo = pin_out + ooff[k];

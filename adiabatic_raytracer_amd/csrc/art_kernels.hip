@@ -2030,13 +2030,18 @@ __device__ inline double line_rmin2(const double* x0, const double* va, double s
   return xm[0] * xm[0] + xm[1] * xm[1] + xm[2] * xm[2];
 }
 
-__global__ __launch_bounds__(256) void sample_kernel(const KParams P, const double maxR, const uint64_t seed,
+#ifndef ART_SAMPLER_WPS
+#define ART_SAMPLER_WPS 2  // waves per SIMD the sampler is compiled for (LDS allows 3)
+#endif
+__global__ __launch_bounds__(256, ART_SAMPLER_WPS) void sample_kernel(const KParams P, const double maxR, const uint64_t seed,
                                                      const int64_t ray_offset, const int64_t n, double* __restrict__ xo,
                                                      double* __restrict__ ko, double* __restrict__ ergo,
                                                      double* __restrict__ vifo, int32_t* __restrict__ wo,
                                                      int32_t* __restrict__ ao, unsigned long long* __restrict__ queue) {
-  // line data of every lane [component][lane]: x0 (3), va (3), vl (3), E, 1/E²
-  __shared__ double sline[11 * 256];
+  // line data of every lane [component][lane]: x0 (3), va (3), vl (3), E, 1/E², vIfty (3).
+  // A lane reads its own line from here too (its registers hold none of it across the step
+  // loop: the kernel fits 2 waves/SIMD without spills)
+  __shared__ double sline[14 * 256];
   __shared__ double slast[256];           // value at the step's last point
   __shared__ unsigned ssb[256], snz[256];  // bit j: signbit / nonzero of point j (bit 0: the step start)
   __shared__ unsigned char ssrc[2 * 256];  // compact lists: uncertified lanes, certified lanes
@@ -2057,6 +2062,8 @@ __global__ __launch_bounds__(256) void sample_kernel(const KParams P, const doub
   // certified-negative scan steps: GJ plasma without a boundary layer only (ART_SCAN_CERT=0: off)
   const bool cert_ok = !(P.bndry_lyr > 0.0) && P.mass_a > 0.0 && P.cert_fac < 1e300;
   const double cert_lhs = 2.0 * P.wp2n, cert_rhs = P.mass_a2 * (1.0 - 1e-6);
+  // r_win³ = 2 wp2n / (m_a² (1 - 1e-6)) with a margin: ωp² < m_a² (1 - 1e-6) beyond it
+  const double r_win2 = cert_ok ? pow(cert_lhs / cert_rhs, 2.0 / 3.0) * (1.0 + 3e-6) : 0.0;
   const unsigned long long lt = (1ull << lane) - 1ull;
   while (true) {
     if (!exhausted) {
@@ -2120,14 +2127,32 @@ __global__ __launch_bounds__(256) void sample_kernel(const KParams P, const doub
     }
     Lx[9 * 256] = E;
     Lx[10 * 256] = iE2;
-    double s_prev = 0.0;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) Lx[(11 + i) * 256] = vI[i];
     double c_prev = sampler_condition_e(P, x0, vl, E, iE2);
     int qn = 0;  // queued brackets (wave-uniform)
+    // This line's window: its chord through the sphere r <= r_win, outside which
+    // ωp² <= 2 wp2n / r³ < m_a² (1 - 1e-6) on every point (|b| <= 2), so every step there is
+    // certified negative once the point before is negative -- the certificate below would say
+    // so too, step by step; here it costs one comparison, and a wave whose lanes are all
+    // outside their windows jumps to the next window (the big-maxR scan points walk ~650
+    // steps per line, ~99% of them certified).
+    double w_in = 1e300, w_out = -1e300;
+    if (active && cert_ok) {
+      const double sc = -(x0[0] * va[0] + x0[1] * va[1] + x0[2] * va[2]);
+      const double h2 = r_win2 - ((x0[0] * x0[0] + x0[1] * x0[1] + x0[2] * x0[2]) - sc * sc);
+      if (h2 > 0.0) {
+        const double h = sqrt(h2);
+        w_in = sc - h - 1e-6;
+        w_out = sc + h + 1e-6;
+      }
+    }
 
     // resolve the queued brackets: Illinois on the exact line (the lane that found one owns
     // it), then each owner counts its valid crossings in queue order and keeps the randInx-th
     auto flush = [&]() {
       wave_lds_sync();
+      #pragma unroll 1
       for (int t = lane; t < qn; t += 64) {
         const int src = sqsrc[wq + t];
         const double* S = sline + wb + src;
@@ -2143,6 +2168,7 @@ __global__ __launch_bounds__(256) void sample_kernel(const KParams P, const doub
         for (int i = 0; i < 3; ++i) xr[i] = X0[i] + VA[i] * b;
         double fb = sampler_condition_e(P, xr, VL, Es, iEs);
         int side = 0;
+        #pragma unroll 1
         for (int it = 0; it < 100; ++it) {  // Illinois on the exact line
           root = a - fa * (b - a) / (fb - fa);
 #pragma unroll
@@ -2168,7 +2194,7 @@ __global__ __launch_bounds__(256) void sample_kernel(const KParams P, const doub
           if (count == randInx) {
             const double r = sqa[wq + t];
 #pragma unroll
-            for (int i = 0; i < 3; ++i) xsel[i] = x0[i] + va[i] * r;
+            for (int i = 0; i < 3; ++i) xsel[i] = Lx[i * 256] + Lx[(3 + i) * 256] * r;
           }
         }
       }
@@ -2179,6 +2205,16 @@ __global__ __launch_bounds__(256) void sample_kernel(const KParams P, const doub
     for (int st = 0; st < nsteps; ++st) {
       const double s0 = st * 0.5;
       const double s1 = fmin(s0 + 0.5, send);
+      const bool quiet = !active || (cert_ok && c_prev < 0.0 && (s1 < w_in || s0 > w_out));
+      if (__ballot(!quiet) == 0ull) {
+        // every lane is certified outside its window: jump to one step before the earliest
+        // next window start (certified steps change nothing but the step counter)
+        int nxt = (active && s1 < w_in && w_in < send) ? (int)floor(w_in * 2.0) - 1 : nsteps;
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) nxt = min(nxt, __shfl_xor(nxt, o));
+        if (nxt > st + 1) st = nxt - 1;
+        continue;
+      }
       // Certified-negative step: with the axion shell imposed (w normalised), the condition
       // is ½(-m_a² + ωp² (1 - g^rr k∥²/E²))/E² with 0 <= g^rr k∥² <= E² (Cauchy-Schwarz, the
       // factor is at most 1), and ωp² = wp2n |b| / r³ <= 2 wp2n / r³ (|b| <= √(4a1² + a2²)
@@ -2187,32 +2223,40 @@ __global__ __launch_bounds__(256) void sample_kernel(const KParams P, const doub
       // point before is negative too, no sign change can occur: only the last point is
       // evaluated, for the value a bracket opening at the next step's first point starts from.
       //
-      // Both bounds use b = Bz/B_n at the step's start point, b = cosθm (3z² - r²)/r² +
-      // 3 sinθm x z / r² (ψ = φ at t = 0), and its Lipschitz bound on the unit sphere,
-      // |∇b| <= |∂θ b| + |∂φ b|/sinθ <= 3 + 3|sinθm|, over the step's angular extent <= L/r_min
-      // (the radial projection shrinks lengths by 1/|x|): so |b| <= min(2, |b_a| + db) along the
-      // step, and |b| >= |b_a| - db.
+      // Both bounds use b = Bz/B_n at the step's two end points, b = cosθm (3z² - r²)/r² +
+      // 3 sinθm x z / r² (ψ = φ at t = 0): a quadratic form n̂ᵀ M n̂ of the direction n̂, M with
+      // eigenvalues -cosθm and (cosθm ± 3)/2, so λmax - λmin = 3. The step projects onto a
+      // great-circle arc of angle α <= L/r_min (the radial projection shrinks lengths by 1/|x|),
+      // along which b(φ) = C + A cos 2φ + B sin 2φ with √(A² + B²) <= (λmax - λmin)/2, so
+      // |b''| <= 6 and b stays within 6 α²/8 of the chord between its end values:
+      // |b| <= min(2, max(|b_a|, |b_b|) + 0.75 α²), and where b_a, b_b share a sign,
+      // |b| >= min(|b_a|, |b_b|) - 0.75 α². (Until round 3 the bound was the first-order
+      // |b_a| ± (3 + 3|sinθm|) α, about 100x wider at 0.5 km steps: the uncertified steps
+      // drop by a third, tools/sampler_steps.cpp.)
       //  * negative: ωp² <= wp2n |b|max / r_min³ < m_a² (see above);
       //  * positive (the point before positive too): outside g_schwartz's interior patch
       //    (r > 10 km), g^rr g^tt = -1, so Cauchy-Schwarz on k∥ with w on the axion shell gives
       //    1 - g^rr k∥²/E² >= g^rr m_a²/E² and the condition >= ½ m_a² (ωp² g^rr/E² - 1)/E² > 0
       //    when wp2n |b|min g^rr(r_min) > E² r_max³ (r_max: at an end of the step).
-      bool cert = false;
-      if (active && cert_ok && c_prev != 0.0 && !isnan(c_prev)) {
-        const double rm2 = line_rmin2(x0, va, s0, s1);
+      bool cert = active && quiet;
+      if (active && !quiet && cert_ok && c_prev != 0.0 && !isnan(c_prev)) {
+        const double X0[3] = {Lx[0], Lx[256], Lx[2 * 256]}, VA[3] = {Lx[3 * 256], Lx[4 * 256], Lx[5 * 256]};
+        const double rm2 = line_rmin2(X0, VA, s0, s1);
         const double rmin = sqrt(rm2);
         double xa[3], xb[3];
 #pragma unroll
-        for (int i = 0; i < 3; ++i) { xa[i] = x0[i] + va[i] * s0; xb[i] = x0[i] + va[i] * s1; }
+        for (int i = 0; i < 3; ++i) { xa[i] = X0[i] + VA[i] * s0; xb[i] = X0[i] + VA[i] * s1; }
         const double ra2 = xa[0] * xa[0] + xa[1] * xa[1] + xa[2] * xa[2];
         const double rb2 = xb[0] * xb[0] + xb[1] * xb[1] + xb[2] * xb[2];
         const double ba = (P.cm * (3.0 * xa[2] * xa[2] - ra2) + 3.0 * P.sm * xa[0] * xa[2]) / ra2;
-        const double db = (3.0 + 3.0 * fabs(P.sm)) * (s1 - s0) / rmin * (1.0 + 1e-9) + 1e-9;
+        const double bb = (P.cm * (3.0 * xb[2] * xb[2] - rb2) + 3.0 * P.sm * xb[0] * xb[2]) / rb2;
+        const double al = (s1 - s0) / rmin;
+        const double db = 0.75 * al * al * (1.0 + 1e-9) + 1e-12;
         if (c_prev < 0.0) {
-          const double bmax = fmin(2.0, fabs(ba) + db);
+          const double bmax = fmin(2.0, fmax(fabs(ba), fabs(bb)) + db);
           cert = cert_lhs * 0.5 * bmax < cert_rhs * (rm2 * rmin);
         } else if (rmin > 10.0) {
-          const double bmin = fabs(ba) - db;
+          const double bmin = (ba * bb > 0.0) ? fmin(fabs(ba), fabs(bb)) - db : -1.0;
           const double rmax2 = fmax(ra2, rb2);
           const double grr = 1.0 - P.rs_gr / rmin;
           cert = bmin > 0.0 && P.wp2n * bmin * grr > E * E * (1.0 + 1e-6) * (rmax2 * sqrt(rmax2));
@@ -2221,6 +2265,7 @@ __global__ __launch_bounds__(256) void sample_kernel(const KParams P, const doub
       const bool unc = active && !cert;
       const unsigned long long mU = __ballot(unc);
       const int nU = __popcll(mU);
+      if (nU == 0) continue;  // all certified: no point, no bracket, c_prev unchanged
       if (unc) ssrc[wb + __popcll(mU & lt)] = (unsigned char)lane;
       ssb[threadIdx.x] = signbit(c_prev) ? 1u : 0u;
       snz[threadIdx.x] = (c_prev != 0.0) ? 1u : 0u;
@@ -2231,6 +2276,7 @@ __global__ __launch_bounds__(256) void sample_kernel(const KParams P, const doub
       // nonzero-ness of the next scan), so it keeps the value it had (round 3: until then
       // every certified lane evaluated its last point, 1 item per lane per step)
       const int totU = nU * nper, tot = totU;
+      #pragma unroll 1
       for (int w0 = 0; w0 < tot; w0 += 64) {
         const int t = w0 + lane;
         if (t < tot) {
@@ -2251,15 +2297,14 @@ __global__ __launch_bounds__(256) void sample_kernel(const KParams P, const doub
       wave_lds_sync();
       // this lane's sign changes in (point j-1, point j]: signbits differ, both values nonzero
       unsigned br = 0u;
-      const double s_start = s_prev;
-      if (active) {
-        if (unc) {
-          const unsigned sb = ssb[threadIdx.x], nz = snz[threadIdx.x];
-          br = (sb ^ (sb << 1)) & nz & (nz << 1) & (((1u << np) - 1u) & ~1u);
-          c_prev = slast[threadIdx.x];
-        }
-        s_prev = s0 + (s1 - s0) * double(nper) / double(np - 1);
+      if (unc) {
+        const unsigned sb = ssb[threadIdx.x], nz = snz[threadIdx.x];
+        br = (sb ^ (sb << 1)) & nz & (nz << 1) & (((1u << np) - 1u) & ~1u);
+        c_prev = slast[threadIdx.x];
       }
+      // the previous step's last grid point, where a bracket at point 1 opens
+      const double ps0 = (st - 1) * 0.5;
+      const double s_start = st == 0 ? 0.0 : ps0 + (fmin(ps0 + 0.5, send) - ps0) * double(nper) / double(np - 1);
       // queue the brackets, each lane's in its order along the line
       unsigned long long bm = __ballot(br != 0u);
       while (bm != 0ull) {
@@ -2283,10 +2328,12 @@ __global__ __launch_bounds__(256) void sample_kernel(const KParams P, const doub
       if (count >= randInx || give_up) {
         if (count < randInx) { xsel[0] = xsel[1] = xsel[2] = NAN; count = 0; }
         const double rmag = sqrt(xsel[0] * xsel[0] + xsel[1] * xsel[1] + xsel[2] * xsel[2]);
-        const double vml = sqrt(vmag * vmag + 2.0 * P.GM_c2 * C_KM * C_KM / rmag) / C_KM;  // :1644
+        const double vIl[3] = {Lx[11 * 256], Lx[12 * 256], Lx[13 * 256]};
+        const double vmagl = sqrt(vIl[0] * vIl[0] + vIl[1] * vIl[1] + vIl[2] * vIl[2]);  // = vmag
+        const double vml = sqrt(vmagl * vmagl + 2.0 * P.GM_c2 * C_KM * C_KM / rmag) / C_KM;  // :1644
         double vel[3], vc[3];
 #pragma unroll
-        for (int i = 0; i < 3; ++i) { vel[i] = vl[i] * vml; vc[i] = vI[i] / C_KM; }
+        for (int i = 0; i < 3; ++i) { vel[i] = Lx[(6 + i) * 256] * vml; vc[i] = vIl[i] / C_KM; }
         // MainRunner.jl:514-529: erg_inf_ini from vIfty/c, k_init = k_norm_Cart(ax_fix = true)
         const double vm = sqrt(vc[0] * vc[0] + vc[1] * vc[1] + vc[2] * vc[2]);
         const double gA = 1.0 / sqrt(1.0 - vm * vm);

@@ -143,6 +143,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pcie", action="store_true")
     args = ap.parse_args()
+    # concurrent passes need a hardware queue each (read at HIP init; the image's default is 4)
+    if args.streams > 3 and int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < args.streams + 1:
+        os.environ["GPU_MAX_HW_QUEUES"] = str(min(16, args.streams + 1))
 
     import torch
     import torch.distributed as dist
