@@ -55,12 +55,17 @@ struct DeviceCtx {
   std::vector<std::pair<void*, size_t>> pool;  // host-entry staging buffers (grow-only, used under g_mu by the
                                                // synchronous *_host calls only)
   // the chunked host pipeline of art_propagate_host (propagate_host_chunked): its compute
-  // streams, one stream for the uploads and one for the downloads, its pinned input and
-  // output staging (grow-only) and three events per chunk (inputs in HBM, computed, outputs
-  // in pinned memory)
+  // streams, one stream for the uploads and one for the chunks' finalize kernels, its pinned
+  // input and output staging (grow-only) and two events per chunk (inputs in HBM, outputs in
+  // pinned memory)
   std::vector<hipStream_t> pstreams;
-  hipStream_t h2d = nullptr, d2h = nullptr;
-  std::vector<std::pair<void*, size_t>> pinned;
+  hipStream_t h2d = nullptr, fin = nullptr;
+  struct Pinned {
+    void* p = nullptr;
+    size_t bytes = 0;
+    unsigned flags = 0;
+  };
+  std::vector<Pinned> pinned;
   std::vector<hipEvent_t> pev;
 };
 std::vector<DeviceCtx> g_ctx;
@@ -131,18 +136,19 @@ int pool_get(DeviceCtx* c, size_t slot, size_t bytes, void** p) {
   return ART_OK;
 }
 
-int pinned_get(DeviceCtx* c, size_t slot, size_t bytes, void** p) {
-  if (c->pinned.size() <= slot) c->pinned.resize(slot + 1, {nullptr, 0});
+int pinned_get(DeviceCtx* c, size_t slot, size_t bytes, void** p, unsigned flags = hipHostMallocDefault) {
+  if (c->pinned.size() <= slot) c->pinned.resize(slot + 1);
   auto& e = c->pinned[slot];
-  if (e.second < bytes) {
-    if (e.first) HIP_OK(hipHostFree(e.first));
-    e.first = nullptr;
-    e.second = 0;
-    if (hipHostMalloc(&e.first, bytes, hipHostMallocDefault) != hipSuccess)
+  if (e.bytes < bytes || e.flags != flags) {
+    if (e.p) HIP_OK(hipHostFree(e.p));
+    e.p = nullptr;
+    e.bytes = 0;
+    e.flags = flags;
+    if (hipHostMalloc(&e.p, bytes, flags) != hipSuccess)
       return fail(ART_E_NOMEM, "hipHostMalloc of %s bytes failed", std::to_string(bytes).c_str());
-    e.second = bytes;
+    e.bytes = bytes;
   }
-  *p = e.first;
+  *p = e.p;
   return ART_OK;
 }
 
@@ -290,10 +296,48 @@ int check_segment_args(const art_params* p, int64_t n, const double* x0, const d
   return ART_OK;
 }
 
+// Options of one propagate launch beyond the entry points' arguments (the host paths' own
+// use): the tail-donation lanes (-1: the device's setting), caller-provided scratch of
+// propagate_scratch_bytes() bytes (null: from the stream-ordered pool), and NaN in the
+// crossing slots without a crossing (finalize_kernel writes them, the *_host contract).
+struct LaunchOpts {
+  int donate = -1;
+  void* scratch = nullptr;
+  bool nan_fill = false;
+  hipStream_t finalize_stream = nullptr;  // finalize_kernel on this stream (after the integrator)
+};
+
+int launch_donate(DeviceCtx* c, const LaunchOpts& o) { return o.donate >= 0 ? o.donate : c->donate; }
+
+// this launch's scratch: [queue head + statistics (256 B) | u0: 16n doubles of fresh state
+// (init_kernel -> the integrator) | END_REC n doubles of end records | X_REC cap n doubles of
+// crossing records (the integrator -> finalize_kernel) | donation records of two levels]
+struct ScratchLayout {
+  size_t head = 256, u0b = 0, recb = 0, xrb = 0, ncont = 0, contb = 0;
+  size_t total() const { return head + u0b + recb + xrb + contb; }
+};
+int scratch_layout(DeviceCtx* c, int64_t n, int cap, int32_t donate, ScratchLayout* L) {
+  const size_t nd = (size_t)n;
+  L->u0b = nd * 16 * sizeof(double);
+  L->recb = nd * art::END_REC * sizeof(double);
+  L->xrb = (size_t)cap * nd * art::X_REC * sizeof(double);
+  // tail donation: at most (resident waves) x donate records of CONT_REC doubles
+  L->ncont = 0;
+  if (donate > 0) {
+    int ncu = 0;
+    HIP_OK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device));
+    L->ncont = std::min(nd, (size_t)ncu * 32 * (size_t)donate);
+  }
+  // the second level (the packed continuation's own donations, resumed by the tail kernel):
+  // never more than the first level's
+  L->contb = 2 * L->ncont * art::CONT_REC * sizeof(double);
+  return ART_OK;
+}
+
 int propagate_device_impl(const art_params* p, int64_t n, const double* x0, const double* k0, const double* erg,
                           const double* dw, const double* ln_t0, const int8_t* species, int32_t max_crossings,
                           art_segment_out* out, art_crossing_buf* xc, void* stream, const TrajArgs& tr = TrajArgs(),
-                          int donate_override = -1) {
+                          const LaunchOpts& opt = LaunchOpts()) {
   bool empty = false;
   int rc = check_segment_args(p, n, x0, k0, erg, dw, ln_t0, species, out, xc, tr, &empty);
   if (rc || empty) return rc;
@@ -302,28 +346,14 @@ int propagate_device_impl(const art_params* p, int64_t n, const double* x0, cons
   hipStream_t s = pick(c, stream);
   const art::KParams K = kparams(*p);
   const int cap = (xc && xc->count) ? xc->capacity : 0;
-  // this launch's scratch: [queue head + statistics (256 B) | u0: 16n doubles of fresh state
-  // (init_kernel -> the integrator) | END_REC n doubles of end records | X_REC cap n doubles of
-  // crossing records (the integrator -> finalize_kernel)]
-  const size_t nd = (size_t)n;
-  const size_t head = 256, u0b = nd * 16 * sizeof(double), recb = nd * art::END_REC * sizeof(double);
-  const size_t xrb = (size_t)cap * nd * art::X_REC * sizeof(double);
-  // tail donation: at most (resident waves) x donate records of CONT_REC doubles
-  size_t ncont = 0;
-  const int32_t donate = donate_override >= 0 ? donate_override : c->donate;
-  if (donate > 0) {
-    int ncu = 0;
-    HIP_OK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device));
-    ncont = std::min(nd, (size_t)ncu * 32 * (size_t)donate);
-  }
-  // the second level (the packed continuation's own donations, resumed by the tail kernel):
-  // at most (continuation waves) x 63 records, never more than the first level's
-  const size_t ncont2 = ncont;
-  const size_t contb = (ncont + ncont2) * art::CONT_REC * sizeof(double);
+  const int32_t donate = launch_donate(c, opt);
+  ScratchLayout SL;
+  if ((rc = scratch_layout(c, n, cap, donate, &SL))) return rc;
+  const size_t head = SL.head, u0b = SL.u0b, recb = SL.recb, xrb = SL.xrb, ncont = SL.ncont;
   LaunchRec* L;
   if ((rc = take_slot(c, &L))) return rc;
-  void* blk = nullptr;
-  if ((rc = scratch_alloc(s, head + u0b + recb + xrb + contb, &blk))) return rc;
+  void* blk = opt.scratch;
+  if (!blk && (rc = scratch_alloc(s, SL.total(), &blk))) return rc;
   unsigned long long* words = (unsigned long long*)blk;
   double* u0 = (double*)((char*)blk + head);
   double* rec = (double*)((char*)blk + head + u0b);
@@ -335,6 +365,7 @@ int propagate_device_impl(const art_params* p, int64_t n, const double* x0, cons
     so.xcount = xc->count;
     so.xpos = xc->pos; so.xk = xc->k; so.xt = xc->t; so.xdw = xc->dw; so.xp = xc->p_nonad;
     so.xrec = (double*)((char*)blk + head + u0b + recb);
+    so.nan_fill = opt.nan_fill ? 1 : 0;
   }
   if (tr.ntimes != 0) {
     so.ntimes = tr.ntimes;
@@ -353,10 +384,11 @@ int propagate_device_impl(const art_params* p, int64_t n, const double* x0, cons
     so.donate = donate;
   }
   HIP_OK(hipMemsetAsync(words, 0, head, s));
-  HIP_OK(art::launch_propagate(K, n, in, so, max_crossings, words, words + 1, s, &L->grid, L->ev0, L->ev1));
+  HIP_OK(art::launch_propagate(K, n, in, so, max_crossings, words, words + 1, s, &L->grid, L->ev0, L->ev1,
+                               opt.finalize_stream));
   HIP_OK(hipMemcpyAsync(L->host_stats, words + 1, sizeof(unsigned long long) * art::N_STATS, hipMemcpyDeviceToHost, s));
   HIP_OK(hipEventRecord(L->done, s));
-  HIP_OK(hipFreeAsync(blk, s));
+  if (!opt.scratch) HIP_OK(hipFreeAsync(blk, s));
   L->pending = true;
   c->last = c->next;
   c->next = (c->next + 1) % RING;
@@ -532,23 +564,37 @@ int art_propagate_traj_device(const art_params* p, int64_t n, const double* x0, 
 }  // extern "C"
 
 namespace {
+// The chunked pipeline's output staging: coarse-grained (non-coherent) mapped host memory
+// lets the L2 combine finalize_kernel's 8-byte stores into full-line PCIe writes; the stream
+// event the host waits on makes them visible. ART_HOST_COHERENT=1: fine-grained memory (A/B).
+unsigned out_coherence() {
+  return env_int("ART_HOST_COHERENT", 0) ? hipHostMallocCoherent : hipHostMallocNonCoherent;
+}
+
 // art_propagate_host for large batches: a pipeline of chunks (the reference call
-// site MainRunner.jl:179-190 hands over host arrays). Three kinds of streams:
-//   * uploads (one stream): chunk k's inputs, gathered from the caller's arrays into pinned
-//     staging by the copy pool, go to HBM one chunk after another, all enqueued up front;
-//   * compute (`slots` streams, chunk k on stream k % slots): each chunk's launch waits for its
-//     own upload only, so two chunks in flight fill each other's drain tails (with tail
-//     donation) and the GPU never waits behind a download;
-//   * downloads (one stream): chunk k's outputs leave as soon as chunk k is computed.
-// The host then scatters the chunks' outputs into the caller's arrays in order while the later
-// ones still compute. Only the first chunk's upload and the last chunk's download and scatter
-// are not hidden behind compute, so those two chunks are a quarter of the others.
-// (Version 2 ran each chunk's copies on its compute stream: a chunk's upload then waited for
-// the download of the chunk before it on that stream, and the GPU idled 6-8 ms between chunks,
-// profiles/r03o_host_timeline.txt. Version 1 reused `slots` staging buffers and enqueued
-// chunk k only after chunk k - slots was drained.) Per-ray results do not depend on the batch
-// split (tests/test_edges.py), so the outputs equal the single launch's bit for bit. The
-// statistics and kernel time of the call are the sums over its chunks.
+// site MainRunner.jl:179-190 hands over host arrays).
+//   * uploads: chunk k's inputs, gathered from the caller's arrays into pinned staging by the
+//     copy pool, go to HBM on one stream, all submitted up front;
+//   * compute: `slots` streams, chunk k on stream k % slots, each launch waiting for its own
+//     upload only, so two chunks in flight fill each other's drain tails (tail donation);
+//   * downloads: none. Each chunk's finalize_kernel writes its outputs straight into mapped
+//     pinned memory over PCIe (coalesced 8-byte-per-lane stores), on a stream of its own
+//     after the chunk's integrator kernels, so the outputs leave while the compute stream
+//     goes on with its next chunk, and no copy waits behind a kernel.
+// The host scatters the chunks' outputs into the caller's arrays in order while the later
+// ones still compute. Only the first chunk's upload and the last chunk's finalize and
+// scatter are not hidden behind compute, so those two chunks are a quarter of the others.
+// Each chunk's scratch is carved from one preallocated buffer (a stream-ordered allocation
+// per chunk blocked the submitting thread once several chunks were in flight).
+// Earlier versions and why they lost (profiles/r03o_host_timeline.txt,
+// profiles/r03p_host_timeline.txt, profiles/r03q_host_timeline.txt): copies on the compute
+// streams (an upload waited behind the previous chunk's download on its stream), then on
+// their own streams but submitted per chunk (the runtime keeps copies in submission order, so
+// a download held the next uploads back until its chunk was computed), then downloads as
+// copies after all uploads (the downloads ran as blit kernels competing with the compute for
+// CUs, 4-15 ms per chunk). Per-ray results do not depend on the batch split
+// (tests/test_edges.py), so the outputs equal the single launch's bit for bit. The statistics
+// and kernel time of the call are the sums over its chunks.
 int propagate_host_chunked(DeviceCtx* c, const art_params* p, int64_t n, const double* x0, const double* k0,
                            const double* erg, const double* dw, const double* ln_t0, const int8_t* species,
                            int32_t max_crossings, art_segment_out* out, art_crossing_buf* xc, int nchunks,
@@ -556,7 +602,7 @@ int propagate_host_chunked(DeviceCtx* c, const art_params* p, int64_t n, const d
   const int cap = (xc && xc->count) ? xc->capacity : 0;
   const int64_t K = std::max(2, nchunks);
   auto up = [](size_t b) { return (b + 255) & ~size_t(255); };
-  // blob layouts of a chunk of m rays (identical in pinned staging and in HBM)
+  // blob layouts of a chunk of m rays (inputs: pinned staging and HBM; outputs: pinned)
   auto in_bytes = [&](int64_t m) { return up((size_t)m * 9 * sizeof(double)) + up((size_t)m); };
   auto cnt_off = [&](int64_t m) { return up((size_t)m * 8 * sizeof(double) + (size_t)m * 3 * sizeof(int32_t)); };
   auto xd_off = [&](int64_t m) { return cnt_off(m) + up((size_t)m * sizeof(int32_t)); };
@@ -569,10 +615,16 @@ int propagate_host_chunked(DeviceCtx* c, const art_params* p, int64_t n, const d
     lo[k] = (int64_t)((double)n * (wk / wsum));
   }
   lo[K] = n;
-  std::vector<size_t> ioff(K + 1, 0), ooff(K + 1, 0);
+  const int32_t donate = nslots > 1 ? 16 : 0;
+  std::vector<size_t> ioff(K + 1, 0), ooff(K + 1, 0), soff(K + 1, 0);
   for (int64_t k = 0; k < K; ++k) {
-    ioff[k + 1] = ioff[k] + in_bytes(lo[k + 1] - lo[k]);
-    ooff[k + 1] = ooff[k] + out_bytes(lo[k + 1] - lo[k]);
+    const int64_t m = lo[k + 1] - lo[k];
+    ScratchLayout SL;
+    int rc0 = scratch_layout(c, m, cap, donate, &SL);
+    if (rc0) return rc0;
+    ioff[k + 1] = ioff[k] + in_bytes(m);
+    ooff[k + 1] = ooff[k] + out_bytes(m);
+    soff[k + 1] = soff[k] + up(SL.total());
   }
   while ((int)c->pstreams.size() < nslots) {
     hipStream_t st = c->stream;
@@ -580,35 +632,30 @@ int propagate_host_chunked(DeviceCtx* c, const art_params* p, int64_t n, const d
     c->pstreams.push_back(st);
   }
   if (!c->h2d) HIP_OK(hipStreamCreateWithFlags(&c->h2d, hipStreamNonBlocking));
-  if (!c->d2h) HIP_OK(hipStreamCreateWithFlags(&c->d2h, hipStreamNonBlocking));
-  while ((int64_t)c->pev.size() < 3 * K) {
+  if (!c->fin) HIP_OK(hipStreamCreateWithFlags(&c->fin, hipStreamNonBlocking));
+  while ((int64_t)c->pev.size() < 2 * K) {
     hipEvent_t ev;
     HIP_OK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
     c->pev.push_back(ev);
   }
-  hipEvent_t *ev_in = c->pev.data(), *ev_done = ev_in + K, *ev_out = ev_in + 2 * K;
+  hipEvent_t *ev_in = c->pev.data(), *ev_done = ev_in + K;
   int rc;
-  void *pi, *po, *di_, *do_;
-  if ((rc = pinned_get(c, 0, ioff[K], &pi)) || (rc = pinned_get(c, 1, ooff[K], &po)) ||
-      (rc = pool_get(c, 16, ioff[K], &di_)) || (rc = pool_get(c, 17, ooff[K], &do_)))
+  void *pi, *po, *di_, *sc_;
+  if ((rc = pinned_get(c, 0, ioff[K], &pi)) ||
+      (rc = pinned_get(c, 1, ooff[K], &po, hipHostMallocMapped | out_coherence())) ||
+      (rc = pool_get(c, 16, ioff[K], &di_)) || (rc = pool_get(c, 17, soff[K], &sc_)))
     return rc;
-  char *pin_in = (char*)pi, *pin_out = (char*)po, *dev_in = (char*)di_, *dev_out = (char*)do_;
-  // the staging buffers may still be read by the previous call's streams only if it failed
-  // half-way; a completed call has drained all three kinds
-  HIP_OK(hipStreamSynchronize(c->h2d));
-  HIP_OK(hipStreamSynchronize(c->d2h));
+  void* po_dev = nullptr;
+  HIP_OK(hipHostGetDevicePointer(&po_dev, po, 0));
+  char *pin_in = (char*)pi, *pin_out = (char*)po, *out_dev = (char*)po_dev, *dev_in = (char*)di_, *scratch = (char*)sc_;
   using Seg = CopyPool::Seg;
   std::vector<int> rings;
-  // ART_HOST_TRACE=1: the host side of every chunk to stderr (gathers, waits, scatters)
+  // ART_HOST_TRACE=1: the host side of every chunk to stderr (gathers, submits, waits, scatters)
   const bool trace = env_int("ART_HOST_TRACE", 0) != 0;
   auto clk = [] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
   const double t_start = clk();
-  const int32_t donate = nslots > 1 ? 16 : 0;
-  // Submission order matters: the runtime keeps the copies of all streams in the order they
-  // were submitted, so a download submitted before an upload holds the upload back until the
-  // download's chunk is computed (a first version interleaved them per chunk and the chunks ran
-  // one at a time, profiles/r03p_host_timeline.txt). So: upload 0, compute 0, the other uploads,
-  // the other computes, then the downloads.
+  // Submission order: upload 0, compute 0, the other uploads, the other computes (the
+  // runtime keeps copies in submission order, so no upload waits behind anything).
   auto upload = [&](int64_t k) -> int {
     const int64_t l0 = lo[k], m = lo[k + 1] - lo[k];
     char* bi = pin_in + ioff[k];
@@ -636,10 +683,9 @@ int propagate_host_chunked(DeviceCtx* c, const art_params* p, int64_t n, const d
     const double t0 = clk();
     hipStream_t st = c->pstreams[k % nslots];
     const int64_t m = lo[k + 1] - lo[k];
-    char* dbi = dev_in + ioff[k];
-    char* dbo = dev_out + ooff[k];
+    const double* di = (const double*)(dev_in + ioff[k]);
+    char* dbo = out_dev + ooff[k];  // device view of the chunk's pinned outputs
     HIP_OK(hipStreamWaitEvent(st, ev_in[k], 0));
-    const double* di = (const double*)dbi;
     double* dd = (double*)dbo;
     int32_t* di32 = (int32_t*)(dd + 8 * m);
     art_segment_out dso{dd, dd + 3 * m, dd + 6 * m, dd + 7 * m, di32, di32 + m, di32 + 2 * m};
@@ -648,27 +694,21 @@ int propagate_host_chunked(DeviceCtx* c, const art_params* p, int64_t n, const d
     if (cap) {
       int32_t* cnt = (int32_t*)(dbo + cnt_off(m));
       double* x = (double*)(dbo + xd_off(m));
-      // slots without a crossing come back as NaN (as the single-launch host path)
-      HIP_OK(hipMemsetD32Async((hipDeviceptr_t)x, 0x7FF80000, (size_t)cap * m * 9 * 2, st));
       dxb = art_crossing_buf{cap, cnt, x, x + 3 * cap * m, x + 6 * cap * m, x + 7 * cap * m, x + 8 * cap * m};
       dxbp = &dxb;
     }
+    LaunchOpts lo_;
+    lo_.donate = donate;
+    lo_.scratch = scratch + soff[k];
+    lo_.nan_fill = true;
+    lo_.finalize_stream = c->fin;
     int rc2 = propagate_device_impl(p, m, di, di + 3 * m, di + 6 * m, di + 7 * m, di + 8 * m,
-                                    (const int8_t*)(dbi + up((size_t)m * 9 * sizeof(double))), max_crossings, &dso,
-                                    dxbp, st, TrajArgs(), donate);
+                                    (const int8_t*)((const char*)di + up((size_t)m * 9 * sizeof(double))), max_crossings,
+                                    &dso, dxbp, st, TrajArgs(), lo_);
     if (rc2) return rc2;
     rings.push_back(c->last);
-    HIP_OK(hipEventRecord(ev_done[k], st));
+    HIP_OK(hipEventRecord(ev_done[k], c->fin));
     if (trace) std::fprintf(stderr, "[art-host] t=%.2f compute k=%lld submit %.2f ms\n", t0 - t_start, (long long)k, clk() - t0);
-    return ART_OK;
-  };
-  auto download = [&](int64_t k) -> int {
-    const double t0 = clk();
-    HIP_OK(hipStreamWaitEvent(c->d2h, ev_done[k], 0));
-    HIP_OK(hipMemcpyAsync(pin_out + ooff[k], dev_out + ooff[k], out_bytes(lo[k + 1] - lo[k]), hipMemcpyDeviceToHost,
-                          c->d2h));
-    HIP_OK(hipEventRecord(ev_out[k], c->d2h));
-    if (trace) std::fprintf(stderr, "[art-host] t=%.2f download k=%lld submit %.2f ms\n", t0 - t_start, (long long)k, clk() - t0);
     return ART_OK;
   };
   if ((rc = upload(0)) || (rc = compute(0))) return rc;
@@ -676,12 +716,10 @@ int propagate_host_chunked(DeviceCtx* c, const art_params* p, int64_t n, const d
     if ((rc = upload(k))) return rc;
   for (int64_t k = 1; k < K; ++k)
     if ((rc = compute(k))) return rc;
-  for (int64_t k = 0; k < K; ++k)
-    if ((rc = download(k))) return rc;
   // the chunks' outputs, in order: pinned staging -> the caller's arrays
   for (int64_t k = 0; k < K; ++k) {
     const double tw0 = clk();
-    HIP_OK(hipEventSynchronize(ev_out[k]));
+    HIP_OK(hipEventSynchronize(ev_done[k]));
     const double tw1 = clk();
     const int64_t l0 = lo[k], m = lo[k + 1] - lo[k];
     const char* bo = pin_out + ooff[k];
@@ -761,9 +799,6 @@ int propagate_host_impl(const art_params* p, int64_t n, const double* x0, const 
   if (cap) {
     int32_t* cnt = (int32_t*)dxc;
     double* xd = (double*)((char*)dxc + cnt_bytes);
-    // slots without a crossing come back as NaN, not as whatever the pooled staging buffer
-    // last held (every dword 0x7FF80000: each double is 0x7FF800007FF80000, a quiet NaN)
-    HIP_OK(hipMemsetD32Async((hipDeviceptr_t)xd, 0x7FF80000, (size_t)cap * nd * 9 * 2, s));
     dxb = art_crossing_buf{cap, cnt, xd, xd + 3 * cap * nd, xd + 6 * cap * nd, xd + 7 * cap * nd, xd + 8 * cap * nd};
     dxbp = &dxb;
   }
@@ -777,8 +812,12 @@ int propagate_host_impl(const art_params* p, int64_t n, const double* x0, const 
     dtr.t = dtr.traj + 3 * nt;
     dtr.count = (int32_t*)(dtr.t + nt);
   }
+  // slots without a crossing come back as NaN, not as whatever the pooled staging buffer last
+  // held: finalize_kernel writes them (LaunchOpts::nan_fill)
+  LaunchOpts opt;
+  opt.nan_fill = true;
   rc = propagate_device_impl(p, n, di, di + 3 * nd, di + 6 * nd, di + 7 * nd, di + 8 * nd, (const int8_t*)(di + 9 * nd),
-                             max_crossings, &dso, dxbp, s, dtr);
+                             max_crossings, &dso, dxbp, s, dtr, opt);
   if (rc) return rc;
   if (htr.ntimes != 0) {
     const size_t nt = (size_t)htr.ntimes * nd;

@@ -1266,8 +1266,22 @@ __host__ __device__ inline T sampler_condition(const KParams& P, const T* x, con
 }
 
 // The same with 1/E² given (the cooperative scan of sample_kernel evaluates other lanes' lines).
+//
+// Algebra (round 3): the reference builds w = (ṙ/√AA, (z ṙ - r v_z)/sinθ, x v_y - y v_x)/AA,
+// rescales it onto the axion shell, w' = √nrm w with nrm = (-E² g^tt - m_a²)/|w|²_g, and
+// evaluates ½(ksqr + ωp²(1 - g^rr k∥(w')²/E²))/E². After the rescale the kinetic part is
+// ksqr = g^tt E² + |w'|²_g = -m_a² by construction, and k∥(w')² = nrm k∥(w)², so neither √nrm
+// nor the rescaled w is needed, and the common factor 1/AA of w cancels in nrm k∥(w)². Scaling
+// k∥'s numerator and |w|²_g by sin²θ clears the 1/sinθ's:
+//   g^rr k∥(w')² = g^rr (-E² g^tt - m_a²) p²/(D (4a1² + a2² + a3²)),
+//   p = 2 √(g^rr/AA) ṙ a1 sinθ + ((z ṙ - r v_z) a2 + (x v_y - y v_x) a3)/r,
+//   D = (g^rr/AA) ṙ² sin²θ + ((z ṙ - r v_z)² + (x v_y - y v_x)²)/r²,
+// one reciprocal instead of the reference's divisions and two square roots. Equal to the
+// reference's value to rounding (tests/test_corecheck.py against the oracle's literal form);
+// NaN where it is (r = 0 or on the z axis).
 template <class T>
 __host__ __device__ inline T sampler_condition_e(const KParams& P, const T* x, const T* vl, double E, double iE2) {
+  ART_FP_FAST
   const T rho2 = x[0] * x[0] + x[1] * x[1];
   const T r = msqrt(rho2 + x[2] * x[2]);
   const T ir = trcp(r);
@@ -1277,32 +1291,26 @@ __host__ __device__ inline T sampler_condition_e(const KParams& P, const T* x, c
   const T cp = x[0] * irho, sp = x[1] * irho;  // ψ = φ at t0 = 0
   T AA = 1.0 - P.rs_gr * ir;
   if (r < P.rNS) AA = 1.0;
-  const T iAA = trcp(AA);
-  const T dr_dt = (x[0] * vl[0] + x[1] * vl[1] + x[2] * vl[2]) * ir;
-  T w0 = dr_dt * trcp(msqrt(AA)) * iAA;
-  T w1 = (x[2] * dr_dt - r * vl[2]) * trcp(st) * iAA;
-  T w2 = (x[0] * vl[1] - x[1] * vl[0]) * iAA;
   T gtt, grr;
   metric_tr(r, P.rs_gr, gtt, grr);
-  const T ir2 = ir * ir;
-  const T gpp = ir2 * trcp(st * st);
-  const double E2 = E * E;
-  const T nrm = (-E2 * gtt - P.mass_a2) * trcp(grr * w0 * w0 + ir2 * w1 * w1 + gpp * w2 * w2);
-  const T f = msqrt(nrm);
-  w0 = w0 * f; w1 = w1 * f; w2 = w2 * f;
+  const T dr = (x[0] * vl[0] + x[1] * vl[1] + x[2] * vl[2]) * ir;
+  const T u1 = x[2] * dr - r * vl[2];          // sinθ w1 AA
+  const T u2 = x[0] * vl[1] - x[1] * vl[0];    // w2 AA
+  const T g = grr * trcp(AA);                  // 1 outside the star, up to rounding
+  const T ds = dr * st;
   const DipoleAng<T> d = dipole_ang(P, st, ct, sp, cp);
-  T wp2 = P.wp2n * ir2 * ir * mabs(d.b);  // GJ_Model_ωp_vec: no zeroIn
+  T wp2 = P.wp2n * (ir * ir) * ir * mabs(d.b);  // GJ_Model_ωp_vec: no zeroIn
   if (P.bndry_lyr > 0.0 && r >= P.rNS) {
     const T w = msqrt(wp2) + layer_wp(P, r, P.rmax);
     wp2 = w * w;
   }
-  T kpar2 = 0.0;
+  T kn = 0.0;  // g^rr k∥(w')²
   if (!P.isotropic) {
-    const T p = 2.0 * msqrt(grr) * w0 * d.a1 + ir * (w1 * d.a2 + w2 * d.a3 * trcp(mabs(st)));
-    kpar2 = p * p * trcp(4.0 * d.a1 * d.a1 + d.a2 * d.a2 + d.a3 * d.a3);
+    const T p = 2.0 * msqrt(g) * ds * d.a1 + (u1 * d.a2 + u2 * d.a3) * ir;
+    const T D = g * ds * ds + (u1 * u1 + u2 * u2) * (ir * ir);
+    kn = grr * (-(E * E) * gtt - P.mass_a2) * (p * p) * trcp(D * (4.0 * d.a1 * d.a1 + d.a2 * d.a2 + d.a3 * d.a3));
   }
-  const T ksqr = gtt * E2 + grr * w0 * w0 + ir2 * w1 * w1 + gpp * w2 * w2;
-  return 0.5 * (ksqr + wp2 * (1.0 - grr * kpar2 * iE2)) * iE2;
+  return 0.5 * (wp2 * (1.0 - kn * iE2) - P.mass_a2) * iE2;
 }
 
 // ωp from GJ_Model_ωp_vec (no zeroIn) at Cartesian x, t = 0 (sampler affect!, :1587)

@@ -50,6 +50,9 @@ struct SegOut {
   const unsigned long long* cont_src_count;
   double* cont2;  // the second-level records (set on the launch's SegOut; read by launch_propagate)
   unsigned long long *cont2_count, *cont2_queue;
+  // 1: finalize_kernel writes NaN into the crossing slots j >= min(count, cap) (the *_host
+  // entry points' contract, include/art.h), so no fill of the outputs is needed beforehand
+  int32_t nan_fill;
 };
 constexpr int END_REC = 16;
 constexpr int X_REC = 8;
@@ -59,10 +62,12 @@ constexpr int N_STATS = 8;  // propagate statistics: attempts, accepted, root re
 int persistent_blocks(const void* func, int64_t work, int block, int fallback_per_cu);
 // propagate = init (u0 of every ray) -> the persistent integrator -> finalize (Cartesian
 // end state, conversion probability at the crossings); ev0/ev1 (may be null) bracket the
-// integrator kernel alone.
+// integrator kernels alone. With fs (and ev1) given, finalize runs on stream fs after ev1,
+// so s can go on with its next launch while the outputs are written (the chunked host
+// pipeline writes them over PCIe into pinned memory).
 hipError_t launch_propagate(const KParams& P, int64_t n, const SegIn& in, const SegOut& out, int32_t max_crossings,
                             unsigned long long* queue, unsigned long long* stats, hipStream_t s, int* grid_out,
-                            hipEvent_t ev0, hipEvent_t ev1);
+                            hipEvent_t ev0, hipEvent_t ev1, hipStream_t fs = nullptr);
 hipError_t launch_sample(const KParams& P, double maxR, uint64_t seed, int64_t ray_offset, int64_t n, double* x,
                          double* k, double* erg, double* vifty, int32_t* w, int32_t* att, unsigned long long* queue,
                          hipStream_t s);

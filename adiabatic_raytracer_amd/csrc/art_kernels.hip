@@ -1998,6 +1998,18 @@ __global__ __launch_bounds__(256) void finalize_kernel(const KParams P, const in
     out.xdw[int64_t(j) * n + i] = dwc;
     out.xp[int64_t(j) * n + i] = prob_nonad_single(P, x, k, erg * fabs(dwc));  // erg_inf_ini .* abs.(Δωc)
   }
+  if (out.nan_fill) {
+    for (int j = m; j < out.cap; ++j) {
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        out.xpos[(int64_t(c) * out.cap + j) * n + i] = NAN;
+        out.xk[(int64_t(c) * out.cap + j) * n + i] = NAN;
+      }
+      out.xt[int64_t(j) * n + i] = NAN;
+      out.xdw[int64_t(j) * n + i] = NAN;
+      out.xp[int64_t(j) * n + i] = NAN;
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -2030,10 +2042,12 @@ __device__ inline double line_rmin2(const double* x0, const double* va, double s
   return xm[0] * xm[0] + xm[1] * xm[1] + xm[2] * xm[2];
 }
 
-#ifndef ART_SAMPLER_WPS
-#define ART_SAMPLER_WPS 2  // waves per SIMD the sampler is compiled for (LDS allows 3)
-#endif
-__global__ __launch_bounds__(256, ART_SAMPLER_WPS) void sample_kernel(const KParams P, const double maxR, const uint64_t seed,
+// Two builds, by waves per SIMD (the LDS allows 3): at 3 the kernel spills a few
+// loop-invariant values, reloaded once per scan step -- a good trade where a line has ~111
+// steps with uncertified ones among them, not where it has ~650 mostly skipped ones
+// (launch_sample picks by the line length).
+template <int WPS>
+__global__ __launch_bounds__(256, WPS) void sample_kernel(const KParams P, const double maxR, const uint64_t seed,
                                                      const int64_t ray_offset, const int64_t n, double* __restrict__ xo,
                                                      double* __restrict__ ko, double* __restrict__ ergo,
                                                      double* __restrict__ vifo, int32_t* __restrict__ wo,
@@ -2092,14 +2106,17 @@ __global__ __launch_bounds__(256, ART_SAMPLER_WPS) void sample_kernel(const KPar
     // ---- one attempt of every active lane: its line (:1486-1531) ----
     double U[10];
     attempt_uniforms(seed, uint64_t(ray_offset + (active ? ray : 0)), attempt, U);
+    // sin(acos c) as √((1 - c)(1 + c)) and the FMA sincos of the integrator (arguments in
+    // [0, 2π)): equal to the reference's values to an ulp, without ocml's acos and its
+    // large-argument sincos path, whose registers set the kernel's occupancy
     double sti, cti, spi, cpi, stl, ctl, spl, cpl, sR, cR;
     cti = 1.0 - 2.0 * U[0];
-    sti = sin(acos(cti));
-    sincos(U[1] * 2.0 * PI, &spi, &cpi);
+    sti = sqrt((1.0 - cti) * (1.0 + cti));
+    msincos(U[1] * 2.0 * PI, spi, cpi);
     ctl = 1.0 - 2.0 * U[2];
-    stl = sin(acos(ctl));
-    sincos(U[3] * 2.0 * PI, &spl, &cpl);
-    sincos(U[4] * 2.0 * PI, &sR, &cR);
+    stl = sqrt((1.0 - ctl) * (1.0 + ctl));
+    msincos(U[3] * 2.0 * PI, spl, cpl);
+    msincos(U[4] * 2.0 * PI, sR, cR);
     const double rR = sqrt(U[5]) * maxR;
     const double va[3] = {sti * cpi, sti * spi, cti};
     const double vl[3] = {stl * cpl, stl * spl, ctl};
@@ -2602,7 +2619,7 @@ static bool w1_builds() {
 
 hipError_t launch_propagate(const KParams& P, int64_t n, const SegIn& in, const SegOut& out, int32_t max_crossings,
                             unsigned long long* queue, unsigned long long* stats, hipStream_t s, int* grid_out,
-                            hipEvent_t ev0, hipEvent_t ev1) {
+                            hipEvent_t ev0, hipEvent_t ev1, hipStream_t fs) {
   const int64_t gr = (n + 255) / 256;
   const unsigned g1 = (unsigned)((n + 255) / 256);
 #ifdef ART_LAUNCH_DEBUG
@@ -2691,7 +2708,12 @@ hipError_t launch_propagate(const KParams& P, int64_t n, const SegIn& in, const 
     }
   }
   if (ev1 && (e = hipEventRecord(ev1, s)) != hipSuccess) return e;
-  hipLaunchKernelGGL(finalize_kernel, dim3(g1), dim3(256), 0, s, P, n, in, out);
+  hipStream_t sf = s;
+  if (fs && ev1 && fs != s) {
+    if ((e = hipStreamWaitEvent(fs, ev1, 0)) != hipSuccess) return e;
+    sf = fs;
+  }
+  hipLaunchKernelGGL(finalize_kernel, dim3(g1), dim3(256), 0, sf, P, n, in, out);
   ART_DBG("finalize_kernel")
   return hipGetLastError();
 }
@@ -2699,9 +2721,19 @@ hipError_t launch_propagate(const KParams& P, int64_t n, const SegIn& in, const 
 hipError_t launch_sample(const KParams& P, double maxR, uint64_t seed, int64_t ray_offset, int64_t n, double* x,
                          double* k, double* erg, double* vifty, int32_t* w, int32_t* att, unsigned long long* queue,
                          hipStream_t s) {
-  const int grid = persistent_blocks((const void*)sample_kernel, n, 256, 1);
-  hipLaunchKernelGGL(sample_kernel, dim3(grid), dim3(256), 0, s, P, maxR, seed, ray_offset, n, x, k, erg, vifty, w, att,
-                     queue);
+  // lines of up to 2.2 x 60 km (264 steps): the 3-wave build; longer ones: 2 waves
+  // (ART_SAMPLER_WPS=2|3 forces one, for A/B runs)
+  int wps = maxR <= 60.0 ? 3 : 2;
+  if (const char* e = std::getenv("ART_SAMPLER_WPS"))
+    if (e[0] == '2' || e[0] == '3') wps = e[0] - '0';
+  const void* fn = wps == 3 ? (const void*)sample_kernel<3> : (const void*)sample_kernel<2>;
+  const int grid = persistent_blocks(fn, n, 256, 1);
+  if (wps == 3)
+    hipLaunchKernelGGL(sample_kernel<3>, dim3(grid), dim3(256), 0, s, P, maxR, seed, ray_offset, n, x, k, erg, vifty, w,
+                       att, queue);
+  else
+    hipLaunchKernelGGL(sample_kernel<2>, dim3(grid), dim3(256), 0, s, P, maxR, seed, ray_offset, n, x, k, erg, vifty, w,
+                       att, queue);
   return hipGetLastError();
 }
 
