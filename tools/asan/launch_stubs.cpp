@@ -4,9 +4,11 @@
 #include "../../adiabatic_raytracer_amd/csrc/art_internal.h"
 
 namespace art {
-int persistent_blocks(const void*, int64_t, int) { return 1; }
+int persistent_blocks(const void*, int64_t, int, int) { return 1; }
 hipError_t launch_propagate(const KParams&, int64_t, const SegIn&, const SegOut&, int32_t, unsigned long long*,
-                            unsigned long long*, hipStream_t, int*, hipEvent_t, hipEvent_t) { return hipErrorNoDevice; }
+                            unsigned long long*, hipStream_t, int*, hipEvent_t, hipEvent_t, hipStream_t) {
+  return hipErrorNoDevice;
+}
 hipError_t launch_sample(const KParams&, double, uint64_t, int64_t, int64_t, double*, double*, double*, double*, int32_t*,
                          int32_t*, unsigned long long*, hipStream_t) { return hipErrorNoDevice; }
 hipError_t launch_prob(const KParams&, int64_t, const double*, const double*, const double*, int64_t, const int64_t*,
