@@ -109,7 +109,15 @@ __host__ __device__ inline double fmax_q(double a, double b) {
 // The radius clamped to rNS (:531): max(r, rNS) for the double path (one v_max_f64 instead
 // of a compare and two selects; a NaN radius gives rNS here, and the NaN state itself is
 // what the integrator reports), the select for the op-counting and dual types.
-__host__ __device__ inline double rclamp(double r, double rns) { return fmax(r, rns); }
+__host__ __device__ inline double rclamp(double r, double rns) {
+#if defined(__HIP_DEVICE_COMPILE__) && defined(ART_EXP_ASM)
+  double m;
+  asm("v_max_f64 %0, %1, %2" : "=v"(m) : "v"(r), "s"(rns));
+  return m;
+#else
+  return fmax(r, rns);
+#endif
+}
 template <class T>
 __host__ __device__ inline T rclamp(const T& r, double rns) {
   return (r < rns) ? T(rns) : r;
@@ -133,22 +141,33 @@ __host__ __device__ inline double frcp(double x) {
 // on |r| <= ln2/2 (truncation < 0.05 ulp) and one ldexp. <= 1 ulp for |x| < 708
 // (tests/test_corecheck.py); no overflow/underflow/NaN special-casing beyond what the
 // arithmetic propagates (the integrator's arguments are moderate ln t and ln EEst values).
+// Horner step p r + c as one three-operand v_fma_f64 (the backend otherwise picks the two-
+// address v_fmac_f64 with the coefficient copied into the accumulator: a v_mov_b64 per step)
+__host__ __device__ inline double horner_fma(double p, double r, double c) {
+#if defined(__HIP_DEVICE_COMPILE__) && defined(ART_EXP_ASM)
+  double o;
+  asm("v_fma_f64 %0, %1, %2, %3" : "=v"(o) : "v"(p), "v"(r), "v"(c));
+  return o;
+#else
+  return fma(p, r, c);
+#endif
+}
 __host__ __device__ inline double exp_fma(double x) {
   ART_FP_FAST
   const double k = rint(x * 1.4426950408889634);
   double r = fma(-k, 0.6931471805599453, x);
   r = fma(-k, 2.3190468138462996e-17, r);
   double p = 1.0 / 6227020800.0;  // 1/13!
-  p = fma(p, r, 1.0 / 479001600.0);
-  p = fma(p, r, 1.0 / 39916800.0);
-  p = fma(p, r, 1.0 / 3628800.0);
-  p = fma(p, r, 1.0 / 362880.0);
-  p = fma(p, r, 1.0 / 40320.0);
-  p = fma(p, r, 1.0 / 5040.0);
-  p = fma(p, r, 1.0 / 720.0);
-  p = fma(p, r, 1.0 / 120.0);
-  p = fma(p, r, 1.0 / 24.0);
-  p = fma(p, r, 1.0 / 6.0);
+  p = horner_fma(p, r, 1.0 / 479001600.0);
+  p = horner_fma(p, r, 1.0 / 39916800.0);
+  p = horner_fma(p, r, 1.0 / 3628800.0);
+  p = horner_fma(p, r, 1.0 / 362880.0);
+  p = horner_fma(p, r, 1.0 / 40320.0);
+  p = horner_fma(p, r, 1.0 / 5040.0);
+  p = horner_fma(p, r, 1.0 / 720.0);
+  p = horner_fma(p, r, 1.0 / 120.0);
+  p = horner_fma(p, r, 1.0 / 24.0);
+  p = horner_fma(p, r, 1.0 / 6.0);
   p = fma(p, r, 0.5);
   p = fma(p, r, 1.0);
   p = fma(p, r, 1.0);
@@ -1289,14 +1308,9 @@ __host__ __device__ inline T sampler_condition_e(const KParams& P, const T* x, c
   const T st = rho * ir, ct = x[2] * ir;
   const T irho = trcp(rho);
   const T cp = x[0] * irho, sp = x[1] * irho;  // ψ = φ at t0 = 0
-  T AA = 1.0 - P.rs_gr * ir;
-  if (r < P.rNS) AA = 1.0;
-  T gtt, grr;
-  metric_tr(r, P.rs_gr, gtt, grr);
   const T dr = (x[0] * vl[0] + x[1] * vl[1] + x[2] * vl[2]) * ir;
   const T u1 = x[2] * dr - r * vl[2];          // sinθ w1 AA
   const T u2 = x[0] * vl[1] - x[1] * vl[0];    // w2 AA
-  const T g = grr * trcp(AA);                  // 1 outside the star, up to rounding
   const T ds = dr * st;
   const DipoleAng<T> d = dipole_ang(P, st, ct, sp, cp);
   T wp2 = P.wp2n * (ir * ir) * ir * mabs(d.b);  // GJ_Model_ωp_vec: no zeroIn
@@ -1306,9 +1320,24 @@ __host__ __device__ inline T sampler_condition_e(const KParams& P, const T* x, c
   }
   T kn = 0.0;  // g^rr k∥(w')²
   if (!P.isotropic) {
-    const T p = 2.0 * msqrt(g) * ds * d.a1 + (u1 * d.a2 + u2 * d.a3) * ir;
-    const T D = g * ds * ds + (u1 * u1 + u2 * u2) * (ir * ir);
-    kn = grr * (-(E * E) * gtt - P.mass_a2) * (p * p) * trcp(D * (4.0 * d.a1 * d.a1 + d.a2 * d.a2 + d.a3 * d.a3));
+    if (r > 10.0 && r >= P.rNS) {
+      // outside the star and g_schwartz's interior patch, g^rr = 1 - rs/r = AA, so g = 1 and
+      // g^rr (-E² g^tt - m_a²) = E² - g^rr m_a²: no square root and no division (the same
+      // value to rounding; the general form below divides twice and takes √g)
+      const T gx = 1.0 - P.rs_gr * ir;
+      const T p = 2.0 * ds * d.a1 + (u1 * d.a2 + u2 * d.a3) * ir;
+      const T D = ds * ds + (u1 * u1 + u2 * u2) * (ir * ir);
+      kn = (E * E - gx * P.mass_a2) * (p * p) * trcp(D * (4.0 * d.a1 * d.a1 + d.a2 * d.a2 + d.a3 * d.a3));
+    } else {
+      T AA = 1.0 - P.rs_gr * ir;
+      if (r < P.rNS) AA = 1.0;
+      T gtt, grr;
+      metric_tr(r, P.rs_gr, gtt, grr);
+      const T g = grr * trcp(AA);  // 1 outside the star, up to rounding
+      const T p = 2.0 * msqrt(g) * ds * d.a1 + (u1 * d.a2 + u2 * d.a3) * ir;
+      const T D = g * ds * ds + (u1 * u1 + u2 * u2) * (ir * ir);
+      kn = grr * (-(E * E) * gtt - P.mass_a2) * (p * p) * trcp(D * (4.0 * d.a1 * d.a1 + d.a2 * d.a2 + d.a3 * d.a3));
+    }
   }
   return 0.5 * (wp2 * (1.0 - kn * iE2) - P.mass_a2) * iE2;
 }

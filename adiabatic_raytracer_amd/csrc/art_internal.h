@@ -53,7 +53,20 @@ struct SegOut {
   // 1: finalize_kernel writes NaN into the crossing slots j >= min(count, cap) (the *_host
   // entry points' contract, include/art.h), so no fill of the outputs is needed beforehand
   int32_t nan_fill;
+  // The streamed host pipeline (propagate_kernel<..., DON = 2>, art_propagate_host): one
+  // integrator launch over the whole batch while its inputs are still arriving and its
+  // outputs already leave. Rays [0, *ready) have their fresh state in HBM (a stream write
+  // raises *ready after each piece's init_kernel); a wave waits for its chunk (at most
+  // STREAM_WAIT_TICKS of s_memrealtime, then it sets *abort and stops: the host falls back).
+  // Piece p = ray >> piece_shift; every finished ray counts into piece_cnt[p], and the wave
+  // that completes a piece sets *piece_sig[p] = 1 (signal memory a finalize stream waits on).
+  const unsigned long long* ready;
+  unsigned long long* piece_cnt;
+  unsigned long long* const* piece_sig;
+  unsigned int* abort_word;
+  int32_t piece_shift;
 };
+constexpr unsigned long long STREAM_WAIT_TICKS = 200000000ull;  // 2 s at 100 MHz
 constexpr int END_REC = 16;
 constexpr int X_REC = 8;
 constexpr int CONT_REC = 24;  // [u (7) | f (7) | τ, dt, qpow, cprev, bstart, erg | int4 {ray, n_acc, n_rej, ncross} | int4 {iter, sprev, flags, save_k}]
@@ -68,6 +81,16 @@ int persistent_blocks(const void* func, int64_t work, int block, int fallback_pe
 hipError_t launch_propagate(const KParams& P, int64_t n, const SegIn& in, const SegOut& out, int32_t max_crossings,
                             unsigned long long* queue, unsigned long long* stats, hipStream_t s, int* grid_out,
                             hipEvent_t ev0, hipEvent_t ev1, hipStream_t fs = nullptr);
+// The streamed host pipeline's launches (art_capi.cpp, propagate_host_streamed): init of rays
+// [i0, i1); the integrator (DON = 2) with `blocks` persistent blocks; finalize of rays
+// [i0, i0 + m) into piece-local SoA outputs `ol` (row stride m).
+hipError_t launch_init_range(const KParams& P, int64_t n, int64_t i0, int64_t i1, const SegIn& in,
+                             unsigned long long* stats, hipStream_t s);
+hipError_t launch_integrator_streamed(const KParams& P, int64_t n, const SegIn& in, const SegOut& out,
+                                      int32_t max_crossings, unsigned long long* queue, unsigned long long* stats,
+                                      int ncus, hipStream_t s, int* grid_out);
+hipError_t launch_finalize_range(const KParams& P, int64_t n, int64_t i0, int64_t m, const SegIn& in,
+                                 const SegOut& ol, hipStream_t s);
 hipError_t launch_sample(const KParams& P, double maxR, uint64_t seed, int64_t ray_offset, int64_t n, double* x,
                          double* k, double* erg, double* vifty, int32_t* w, int32_t* att, unsigned long long* queue,
                          hipStream_t s);

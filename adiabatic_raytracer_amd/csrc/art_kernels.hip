@@ -260,8 +260,33 @@ __device__ inline double illinois_interp(const KParams& P, const double* u0, con
   return tr;
 }
 
+// A 16-byte record store. WT (the streamed pipeline, ART_STREAM_WT): a system-coherent
+// store (sc0 sc1: written through the XCD's L2 to memory), so a wave makes its records visible
+// to every XCD with a wait for its stores instead of an L2 write-back.
+typedef double art_d2 __attribute__((ext_vector_type(2)));
+typedef int art_i4 __attribute__((ext_vector_type(4)));
+template <bool WT>
+__device__ inline void rec_store(double2* p, double a, double b) {
+  if constexpr (WT) {
+    const art_d2 v = {a, b};
+    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(p), "v"(v) : "memory");
+  } else {
+    *p = make_double2(a, b);
+  }
+}
+template <bool WT>
+__device__ inline void rec_store(int4* p, int a, int b, int c, int d) {
+  if constexpr (WT) {
+    const art_i4 v = {a, b, c, d};
+    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(p), "v"(v) : "memory");
+  } else {
+    *p = make_int4(a, b, c, d);
+  }
+}
+
 // ---------------------------------------------------------------------------
 // affect! (RayTracer.jl:301-350). Returns 0 = skipped, 1 = recorded, 2 = recorded + terminate.
+template <bool WT = false>
 __device__ inline int affect(const KParams& P, const SegIn& in, const SegOut& out, int64_t n, int64_t ray,
                              const double* u, double tau, double erg, int& ncross, int max_crossings) {
   double st, ct, sp, cp;
@@ -286,10 +311,10 @@ __device__ inline int affect(const KParams& P, const SegIn& in, const SegOut& ou
   if (out.xcount && j < out.cap) {
     const double dwc = u[6] / erg;  // P_nonAD: finalize_kernel
     double2* rq = reinterpret_cast<double2*>(out.xrec + ((int64_t)ray * out.cap + j) * X_REC);
-    rq[0] = make_double2(x[0], x[1]);
-    rq[1] = make_double2(x[2], k[0]);
-    rq[2] = make_double2(k[1], k[2]);
-    rq[3] = make_double2(exp(tau), dwc);
+    rec_store<WT>(rq + 0, x[0], x[1]);
+    rec_store<WT>(rq + 1, x[2], k[0]);
+    rec_store<WT>(rq + 2, k[1], k[2]);
+    rec_store<WT>(rq + 3, exp(tau), dwc);
   }
   ncross = j + 1;
   const int maxc = max_crossings <= 0 ? -1 : max_crossings;
@@ -384,6 +409,14 @@ constexpr int SCAN_WORDS = 4;  // 2-bit codes for up to 64 grid points (interp_p
 #ifndef ART_WAVES_PER_SIMD
 #define ART_WAVES_PER_SIMD 2
 #endif
+#ifdef ART_STREAM_WT
+constexpr bool STREAM_WT = true;
+#else
+constexpr bool STREAM_WT = false;
+#endif
+#ifndef ART_STREAM_FLUSH
+#define ART_STREAM_FLUSH 31  // (DON = 2) a wave's finished-ray counts go out every 32 iterations
+#endif
 
 // ---------------------------------------------------------------------------
 // One loop iteration = one step attempt for every live lane: a runtime loop over the
@@ -398,6 +431,57 @@ constexpr int SCAN_WORDS = 4;  // 2-bit codes for up to 64 grid points (interp_p
 // GEOM_GR: Schwarzschild (rs > 0), no boundary layer, anisotropic (configs[3]): only the
 // boundary-layer and isotropic branches fold away, and rs != 0 is assumed.
 enum { GEOM_ANY = 0, GEOM_FLAT = 1, GEOM_GR = 2 };
+
+// The streamed host pipeline (DON = 2): the fresh state of rays [0, need) is in HBM once
+// *out.ready >= need (a stream write after each piece's init_kernel). The leader lane polls it
+// (system scope: the command processor writes it), at most STREAM_WAIT_TICKS; on time-out, or
+// when another wave gave up, it raises *out.abort_word and the wave stops taking rays (the host
+// then discards the call's results and runs the batch again without streaming).
+__device__ inline bool stream_ready(const SegOut& out, int64_t need, int leader) {
+  int ok = 1;
+  if ((int)(threadIdx.x & 63) == leader) {  // (a wave with nothing else to integrate)
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    while (__hip_atomic_load(out.ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < (unsigned long long)need) {
+      if (__hip_atomic_load(out.abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u ||
+          __builtin_amdgcn_s_memrealtime() - t0 > STREAM_WAIT_TICKS) {
+        __hip_atomic_store(out.abort_word, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        ok = 0;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(64);
+    }
+  }
+  return __shfl(ok, leader) != 0;
+}
+
+// the ready counter as one lane reads it now (wave-uniform)
+__device__ inline int64_t stream_poll(const SegOut& out, int leader) {
+  unsigned long long r = 0;
+  if ((int)(threadIdx.x & 63) == leader) r = __hip_atomic_load(out.ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+  return (int64_t)__shfl(r, leader);
+}
+
+// A wave's finished rays of piece p, counted c at a time: the wave's record stores are released
+// first (agent scope: the end and crossing records reach memory every XCD reads), then the
+// count; the count that completes the piece raises the piece's signal. Waves batch their
+// counts (at most every 32 iterations, at a piece change and at exit), so the L2 write-backs of
+// the release stay rare.
+__device__ inline void stream_count(const SegOut& out, int64_t n, int p, unsigned long long c) {
+  if constexpr (STREAM_WT)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's write-through records are in memory
+  else
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  const int leader = __ffsll((long long)__ballot(1)) - 1;
+  if ((int)(threadIdx.x & 63) == leader) {
+    const unsigned long long old = __hip_atomic_fetch_add(out.piece_cnt + p, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int64_t lo = (int64_t)p << out.piece_shift;
+    const int64_t hi = (lo + ((int64_t)1 << out.piece_shift)) < n ? lo + ((int64_t)1 << out.piece_shift) : n;
+    if ((int64_t)(old + c) == hi - lo) {  // the piece's last count: every wave's records are out
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      __hip_atomic_store(out.piece_sig[p], 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+}
 
 template <int GEOM>
 __device__ inline KParams specialize(const KParams& P) {
@@ -419,7 +503,7 @@ __device__ inline KParams specialize(const KParams& P) {
 // carry none of that code, so a lone pass pays nothing for it
 // WPS: waves per SIMD the registers are budgeted for (the default 2; the GR continuation
 // launch, below, uses 1)
-template <int INTEG, int GEOM, bool SAVE, bool DON, int WPS = ART_WAVES_PER_SIMD>
+template <int INTEG, int GEOM, bool SAVE, int DON, int WPS = ART_WAVES_PER_SIMD>
 __global__ __launch_bounds__(BLOCK, WPS) void propagate_kernel(const KParams P_in, const int64_t n,
                                                                               const SegIn in, const SegOut out,
                                                                               const int32_t max_crossings,
@@ -428,7 +512,7 @@ __global__ __launch_bounds__(BLOCK, WPS) void propagate_kernel(const KParams P_i
   const KParams P = specialize<GEOM>(P_in);
   constexpr bool RK4 = (INTEG == ART_RK4);
   // the work queue: fresh rays [0, n), or in a continuation launch the donated records
-  const bool cont = DON && out.cont_mode;
+  const bool cont = DON == 1 && out.cont_mode;
   const int64_t nq = cont ? (int64_t)*out.cont_src_count : n;
   unsigned long long* const rqueue = cont ? out.cont_queue : queue;
   // the callbacks (RayTracer.jl:357-368) are installed only when make_tree (:361-377)
@@ -466,6 +550,16 @@ __global__ __launch_bounds__(BLOCK, WPS) void propagate_kernel(const KParams P_i
   double hroot = 0.0, r_tha = 0.0, r_ca = 0.0, r_thb = 0.0, r_cb = 0.0, r_t = 0.0, r_slope = 1.0, post_c = 0.0;
   int post_s = 0, r_side = 0, r_it = 0;
   int wnext = 0, wend = 0;
+  // (DON = 2) per wave, in LDS to keep them out of the integrator's registers: the ready counter
+  // as last read, the piece whose finished rays are being counted, that count, a tick
+  __shared__ long long s_strm[4 * (BLOCK / 64)];
+  volatile long long* const strm = s_strm + 4 * (threadIdx.x >> 6);
+  if (DON == 2) {
+    strm[0] = 0;
+    strm[1] = -1;
+    strm[2] = 0;
+    strm[3] = 0;
+  }
   int save_k = 1;  // SAVE: the next interior saveat index
   bool exhausted = false;
   unsigned s_att = 0, s_acc = 0, s_root = 0, s_scan = 0, s_interp = 0, s_rays = 0, s_cert = 0;
@@ -530,9 +624,27 @@ __global__ __launch_bounds__(BLOCK, WPS) void propagate_kernel(const KParams P_i
           wnext = __builtin_amdgcn_readfirstlane((int)base);
           wend = __builtin_amdgcn_readfirstlane((int)((int64_t)base + CHUNK < nq ? (int64_t)base + CHUNK : nq));
         }
+        int lim = wend;
+#ifdef ART_STREAM_NOGATE
+        if constexpr (false) {  // dev timing build: the inputs are all in HBM before the launch
+#else
+        if constexpr (DON == 2) {
+#endif
+          // only rays whose fresh state has arrived; while none of the chunk has, a wave with
+          // other rays goes on integrating them, and an empty wave waits (bounded)
+          const int leader = __ffsll((long long)need) - 1;
+          int64_t rdy = strm[0];
+          if (rdy < wend) strm[0] = rdy = stream_poll(out, leader);
+          if (rdy <= wnext) {
+            if (__ballot(mode != M_IDLE) != 0ull) break;
+            if (!stream_ready(out, wnext + 1, leader)) { exhausted = true; break; }
+            strm[0] = rdy = stream_poll(out, leader);
+          }
+          lim = rdy < wend ? (int)rdy : wend;
+        }
         const int rank = __popcll(need & ((1ull << lane) - 1ull));
         const int cnt = __popcll(need);
-        const int take = (wend - wnext) < cnt ? (wend - wnext) : cnt;
+        const int take = (lim - wnext) < cnt ? (lim - wnext) : cnt;
         if (mode == M_IDLE && rank < take && cont) {
           // a donated ray: its complete state from the tail-donation record
           mode = M_STEP;
@@ -1211,7 +1323,7 @@ __global__ __launch_bounds__(BLOCK, WPS) void propagate_kernel(const KParams P_i
     if (root_done || (scan && !hit)) bstart = bend;
     if (root_done) {
       const double tau_r = tau + hs;
-      const int a = affect(P, in, out, n, ray, u, tau_r, erg, ncross, max_crossings);
+      const int a = affect<DON == 2 && STREAM_WT>(P, in, out, n, ray, u, tau_r, erg, ncross, max_crossings);
       tau = tau_r;
       cprev = post_c;  // the post-event side (DiffEq repeat_nudge): the root is not re-found
       cprev_ok = true;
@@ -1234,22 +1346,49 @@ __global__ __launch_bounds__(BLOCK, WPS) void propagate_kernel(const KParams P_i
       else if (iter >= P.maxiters) finish = ART_STATUS_MAXITERS;
     }
 
+    int fin_piece = -1;  // (DON = 2) the piece of a ray finishing now
     if (finish >= 0) {  // the raw end record; finalize_kernel back-transforms it (RayTracer.jl:393-416)
+      if constexpr (DON == 2) fin_piece = ray >> out.piece_shift;
+      constexpr bool WT = DON == 2 && STREAM_WT;
       double2* rq = reinterpret_cast<double2*>(out.rec + (int64_t)ray * END_REC);
-      rq[0] = make_double2(u[0], u[1]);
-      rq[1] = make_double2(u[2], u[3]);
-      rq[2] = make_double2(u[4], u[5]);
-      rq[3] = make_double2(u[6], tau);
+      rec_store<WT>(rq + 0, u[0], u[1]);
+      rec_store<WT>(rq + 1, u[2], u[3]);
+      rec_store<WT>(rq + 2, u[4], u[5]);
+      rec_store<WT>(rq + 3, u[6], tau);
       int4* ri = reinterpret_cast<int4*>(rq + 4);
-      ri[0] = make_int4(finish, n_acc, n_rej, ncross);
+      rec_store<WT>(ri, finish, n_acc, n_rej, ncross);
       if constexpr (SAVE) ri[1] = make_int4(save_k + 1, 0, 0, 0);  // start + interior + end
       ray = -1;
       mode = M_IDLE;
     }
+    if constexpr (DON == 2) {
+      // the streamed host pipeline: count the rays finishing now into their pieces (batched,
+      // stream_count)
+      unsigned long long fm = __ballot(fin_piece >= 0);
+      while (fm != 0ull) {
+        const int pc = __shfl(fin_piece, __ffsll((long long)fm) - 1);
+        const unsigned long long same = __ballot(fin_piece == pc);
+        if (pc != (int)strm[1]) {
+          if (strm[2] != 0) stream_count(out, n, (int)strm[1], (unsigned long long)strm[2]);
+          strm[1] = pc;
+          strm[2] = 0;
+        }
+        strm[2] = strm[2] + __popcll(same);
+        fm &= ~same;
+      }
+      if (strm[2] != 0) {
+        const long long t = strm[3] + 1;
+        strm[3] = t;
+        if ((t & ART_STREAM_FLUSH) == 0 || exhausted) {
+          stream_count(out, n, (int)strm[1], (unsigned long long)strm[2]);
+          strm[2] = 0;
+        }
+      }
+    }
     ART_TMARK(0)  // saveat, reload, events, finish and the output stores (+ refill)
     // tail donation (SegOut::donate): the drained wave's last few rays, all at a step
     // boundary, leave for the continuation launch and the wave retires
-    if (DON && exhausted && out.donate > 0) {
+    if (DON == 1 && exhausted && out.donate > 0) {
       const unsigned long long live = __ballot(mode != M_IDLE);
       if (live != 0ull && __popcll(live) <= out.donate && __ballot(mode == M_ROOT) == 0ull) {
         const int leader = __ffsll((long long)live) - 1;
@@ -1273,6 +1412,9 @@ __global__ __launch_bounds__(BLOCK, WPS) void propagate_kernel(const KParams P_i
     }
   }
 
+  if constexpr (DON == 2) {
+    if (strm[2] != 0) stream_count(out, n, (int)strm[1], (unsigned long long)strm[2]);
+  }
   // wave-reduce the statistics and add them once per wave
 #if defined(ART_SLOT_TIMING)
   if (lane == 0) {  // [refill etc, combination, RHS, slot rest, norm..park, grid, fast+walk+coop, fallback]
@@ -1892,10 +2034,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
 // its probe RHS; RK4: the fixed step) and the condition value that seeds the callback's
 // sign memory. Kept out of the persistent integrator, whose registers it would otherwise
 // crowd. Out: in.u0 = 16n doubles [u0 (7) | f0 (7) | dt | c0].
-__global__ __launch_bounds__(256) void init_kernel(const KParams P, const int64_t n, const SegIn in,
-                                                   unsigned long long* __restrict__ stats) {
+// Rays [i0, i1) of the n (the streamed host pipeline initialises the batch piece by piece).
+__global__ __launch_bounds__(256) void init_kernel(const KParams P, const int64_t n, const int64_t i0, const int64_t i1,
+                                                   const SegIn in, unsigned long long* __restrict__ stats) {
   unsigned nrhs = 0;  // grid-stride over the rays: one stats atomic per wave
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+  for (int64_t i = i0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < i1; i += (int64_t)gridDim.x * blockDim.x) {
     const double xs[3] = {in.x0[i], in.x0[n + i], in.x0[2 * n + i]};
     const double ks[3] = {in.k0[i], in.k0[n + i], in.k0[2 * n + i]};
     const double erg = in.erg[i], tau = in.lnt0[i];
@@ -1930,10 +2073,13 @@ __global__ __launch_bounds__(256) void init_kernel(const KParams P, const int64_
 // End state in Cartesian form (back-transform, RayTracer.jl:393-416) from the raw end record
 // the integrator left in out.rec (spread into the SoA outputs here), and the conversion probability of every
 // recorded crossing (get_Prob_nonAD with Nc = 1, MainRunner.jl:265). One thread per ray.
-__global__ __launch_bounds__(256) void finalize_kernel(const KParams P, const int64_t n, const SegIn in,
-                                                       const SegOut out) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
+// Rays [i0, i0 + m) of the n; the outputs are indexed o = i - i0 with row stride m (the whole
+// batch: i0 = 0, m = n; the streamed host pipeline: one piece into its own SoA blob).
+__global__ __launch_bounds__(256) void finalize_kernel(const KParams P, const int64_t n, const int64_t i0,
+                                                       const int64_t m, const SegIn in, const SegOut out) {
+  const int64_t o = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (o >= m) return;
+  const int64_t i = i0 + o;
   const double erg = in.erg[i];
   int ncross = 0;
   {
@@ -1945,69 +2091,69 @@ __global__ __launch_bounds__(256) void finalize_kernel(const KParams P, const in
     back_transform(P, u, erg, xe, ke);
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
-      out.x_end[c * n + i] = xe[c];
-      out.k_end[c * n + i] = ke[c];
+      out.x_end[c * m + o] = xe[c];
+      out.k_end[c * m + o] = ke[c];
     }
-    out.u7_end[i] = u[6];
-    out.tau_end[i] = q3.y;
-    out.status[i] = ri.x;
-    out.n_acc[i] = ri.y;
-    out.n_rej[i] = ri.z;
+    out.u7_end[o] = u[6];
+    out.tau_end[o] = q3.y;
+    out.status[o] = ri.x;
+    out.n_acc[o] = ri.y;
+    out.n_rej[o] = ri.z;
     ncross = ri.w;
-    if (out.xcount) out.xcount[i] = ncross;
-    if (out.ntimes >= 2) out.traj_n[i] = reinterpret_cast<const int4*>(rq + 4)[1].x;
+    if (out.xcount) out.xcount[o] = ncross;
+    if (out.ntimes >= 2) out.traj_n[o] = reinterpret_cast<const int4*>(rq + 4)[1].x;
   }
   if (out.ntimes >= 2) {  // saveat: start (u0 back-transformed), interior to Cartesian, end
     double u0[7], xs[3], ks[3];
 #pragma unroll
     for (int c = 0; c < 7; ++c) u0[c] = in.u0[c * n + i];
     back_transform(P, u0, erg, xs, ks);
-    const int m = out.traj_n[i];
-    for (int k = 0; k < m; ++k) {
+    const int mt = out.traj_n[o];
+    for (int k = 0; k < mt; ++k) {
       double x[3];
       if (k == 0) {
         x[0] = xs[0]; x[1] = xs[1]; x[2] = xs[2];
-        out.traj_t[i] = in.lnt0[i];
-      } else if (k == m - 1) {
-        x[0] = out.x_end[i]; x[1] = out.x_end[n + i]; x[2] = out.x_end[2 * n + i];
-        out.traj_t[int64_t(k) * n + i] = out.tau_end[i];
+        out.traj_t[o] = in.lnt0[i];
+      } else if (k == mt - 1) {
+        x[0] = out.x_end[o]; x[1] = out.x_end[m + o]; x[2] = out.x_end[2 * m + o];
+        out.traj_t[int64_t(k) * m + o] = out.tau_end[o];
       } else {
-        const double r = out.traj[(int64_t(0) * out.ntimes + k) * n + i];
+        const double r = out.traj[(int64_t(0) * out.ntimes + k) * m + o];
         double st, ct, sp, cp;
-        msincos(out.traj[(int64_t(1) * out.ntimes + k) * n + i], st, ct);
-        msincos(out.traj[(int64_t(2) * out.ntimes + k) * n + i], sp, cp);
+        msincos(out.traj[(int64_t(1) * out.ntimes + k) * m + o], st, ct);
+        msincos(out.traj[(int64_t(2) * out.ntimes + k) * m + o], sp, cp);
         x[0] = r * st * cp; x[1] = r * st * sp; x[2] = r * ct;
       }
 #pragma unroll
-      for (int c = 0; c < 3; ++c) out.traj[(int64_t(c) * out.ntimes + k) * n + i] = x[c];
+      for (int c = 0; c < 3; ++c) out.traj[(int64_t(c) * out.ntimes + k) * m + o] = x[c];
     }
   }
   if (!out.xcount) return;
-  const int m = ncross < out.cap ? ncross : out.cap;
-  for (int j = 0; j < m; ++j) {
+  const int mc = ncross < out.cap ? ncross : out.cap;
+  for (int j = 0; j < mc; ++j) {
     const double2* rq = reinterpret_cast<const double2*>(out.xrec + (i * out.cap + j) * X_REC);
     const double2 q0 = rq[0], q1 = rq[1], q2 = rq[2], q3 = rq[3];
     const double x[3] = {q0.x, q0.y, q1.x}, k[3] = {q1.y, q2.x, q2.y};
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
-      out.xpos[(int64_t(c) * out.cap + j) * n + i] = x[c];
-      out.xk[(int64_t(c) * out.cap + j) * n + i] = k[c];
+      out.xpos[(int64_t(c) * out.cap + j) * m + o] = x[c];
+      out.xk[(int64_t(c) * out.cap + j) * m + o] = k[c];
     }
-    out.xt[int64_t(j) * n + i] = q3.x;
+    out.xt[int64_t(j) * m + o] = q3.x;
     const double dwc = q3.y;
-    out.xdw[int64_t(j) * n + i] = dwc;
-    out.xp[int64_t(j) * n + i] = prob_nonad_single(P, x, k, erg * fabs(dwc));  // erg_inf_ini .* abs.(Δωc)
+    out.xdw[int64_t(j) * m + o] = dwc;
+    out.xp[int64_t(j) * m + o] = prob_nonad_single(P, x, k, erg * fabs(dwc));  // erg_inf_ini .* abs.(Δωc)
   }
   if (out.nan_fill) {
-    for (int j = m; j < out.cap; ++j) {
+    for (int j = mc; j < out.cap; ++j) {
 #pragma unroll
       for (int c = 0; c < 3; ++c) {
-        out.xpos[(int64_t(c) * out.cap + j) * n + i] = NAN;
-        out.xk[(int64_t(c) * out.cap + j) * n + i] = NAN;
+        out.xpos[(int64_t(c) * out.cap + j) * m + o] = NAN;
+        out.xk[(int64_t(c) * out.cap + j) * m + o] = NAN;
       }
-      out.xt[int64_t(j) * n + i] = NAN;
-      out.xdw[int64_t(j) * n + i] = NAN;
-      out.xp[int64_t(j) * n + i] = NAN;
+      out.xt[int64_t(j) * m + o] = NAN;
+      out.xdw[int64_t(j) * m + o] = NAN;
+      out.xp[int64_t(j) * m + o] = NAN;
     }
   }
 }
@@ -2061,6 +2207,7 @@ __global__ __launch_bounds__(256, WPS) void sample_kernel(const KParams P, const
   __shared__ unsigned char ssrc[2 * 256];  // compact lists: uncertified lanes, certified lanes
   __shared__ double sqa[4 * SQCAP], sqb[4 * SQCAP];  // bracket queue: ends -> root
   __shared__ unsigned char sqsrc[4 * SQCAP], sqok[4 * SQCAP];
+  __shared__ double sgrid[32];  // (0.5 j)/19: a full step's grid offsets, the same rounding as the division
   const int lane = threadIdx.x & 63;
   const int wb = threadIdx.x & ~63;
   const int wq = (threadIdx.x >> 6) * SQCAP;
@@ -2079,6 +2226,8 @@ __global__ __launch_bounds__(256, WPS) void sample_kernel(const KParams P, const
   // r_win³ = 2 wp2n / (m_a² (1 - 1e-6)) with a margin: ωp² < m_a² (1 - 1e-6) beyond it
   const double r_win2 = cert_ok ? pow(cert_lhs / cert_rhs, 2.0 / 3.0) * (1.0 + 3e-6) : 0.0;
   const unsigned long long lt = (1ull << lane) - 1ull;
+  if (threadIdx.x < np) sgrid[threadIdx.x] = 0.5 * double(threadIdx.x) / double(np - 1);
+  __syncthreads();
   while (true) {
     if (!exhausted) {
       unsigned long long need = __ballot(ray < 0);
@@ -2265,9 +2414,12 @@ __global__ __launch_bounds__(256, WPS) void sample_kernel(const KParams P, const
         for (int i = 0; i < 3; ++i) { xa[i] = X0[i] + VA[i] * s0; xb[i] = X0[i] + VA[i] * s1; }
         const double ra2 = xa[0] * xa[0] + xa[1] * xa[1] + xa[2] * xa[2];
         const double rb2 = xb[0] * xb[0] + xb[1] * xb[1] + xb[2] * xb[2];
-        const double ba = (P.cm * (3.0 * xa[2] * xa[2] - ra2) + 3.0 * P.sm * xa[0] * xa[2]) / ra2;
-        const double bb = (P.cm * (3.0 * xb[2] * xb[2] - rb2) + 3.0 * P.sm * xb[0] * xb[2]) / rb2;
-        const double al = (s1 - s0) / rmin;
+        // (reciprocals from frcp, <= 1 ulp: the certificate's margins, 1e-9 relative and 1e-12
+        // absolute on db and 1e-6 on m_a², dwarf that; a certified step is still provably one-signed)
+        const double ba = (P.cm * (3.0 * xa[2] * xa[2] - ra2) + 3.0 * P.sm * xa[0] * xa[2]) * frcp(ra2);
+        const double bb = (P.cm * (3.0 * xb[2] * xb[2] - rb2) + 3.0 * P.sm * xb[0] * xb[2]) * frcp(rb2);
+        const double irmin = frcp(rmin);
+        const double al = (s1 - s0) * irmin;
         const double db = 0.75 * al * al * (1.0 + 1e-9) + 1e-12;
         if (c_prev < 0.0) {
           const double bmax = fmin(2.0, fmax(fabs(ba), fabs(bb)) + db);
@@ -2275,7 +2427,7 @@ __global__ __launch_bounds__(256, WPS) void sample_kernel(const KParams P, const
         } else if (rmin > 10.0) {
           const double bmin = (ba * bb > 0.0) ? fmin(fabs(ba), fabs(bb)) - db : -1.0;
           const double rmax2 = fmax(ra2, rb2);
-          const double grr = 1.0 - P.rs_gr / rmin;
+          const double grr = 1.0 - P.rs_gr * irmin * (1.0 + 1e-15);  // (rounded down: a smaller g^rr)
           cert = bmin > 0.0 && P.wp2n * bmin * grr > E * E * (1.0 + 1e-6) * (rmax2 * sqrt(rmax2));
         }
       }
@@ -2300,7 +2452,8 @@ __global__ __launch_bounds__(256, WPS) void sample_kernel(const KParams P, const
           const int j = t / nU + 1;
           const int src = ssrc[wb + t % nU];
           const double* S = sline + wb + src;
-          const double sc = s0 + (s1 - s0) * double(j) / double(np - 1);
+          // (s1 - s0) j / 19: from the table for a full 0.5 km step (wave-uniform), else divided
+          const double sc = s0 + (s1 - s0 == 0.5 ? sgrid[j] : (s1 - s0) * double(j) / double(np - 1));
           double xl[3];
 #pragma unroll
           for (int i = 0; i < 3; ++i) xl[i] = S[i * 256] + S[(3 + i) * 256] * sc;
@@ -2321,7 +2474,8 @@ __global__ __launch_bounds__(256, WPS) void sample_kernel(const KParams P, const
       }
       // the previous step's last grid point, where a bracket at point 1 opens
       const double ps0 = (st - 1) * 0.5;
-      const double s_start = st == 0 ? 0.0 : ps0 + (fmin(ps0 + 0.5, send) - ps0) * double(nper) / double(np - 1);
+      const double pds = fmin(ps0 + 0.5, send) - ps0;
+      const double s_start = st == 0 ? 0.0 : ps0 + (pds == 0.5 ? sgrid[nper] : pds * double(nper) / double(np - 1));
       // queue the brackets, each lane's in its order along the line
       unsigned long long bm = __ballot(br != 0u);
       while (bm != 0ull) {
@@ -2581,7 +2735,7 @@ int persistent_blocks(const void* func, int64_t work, int block, int fallback_pe
 using KFn = void (*)(const KParams, const int64_t, const SegIn, const SegOut, const int32_t, unsigned long long*,
                      unsigned long long*);
 
-template <bool DON>
+template <int DON>
 static KFn pick_propagate(bool save, bool rk4, bool flat, bool sch) {
   if (save)  // saveat requested: the saving instantiations
     return rk4 ? propagate_kernel<ART_RK4, GEOM_ANY, true, DON>
@@ -2635,15 +2789,16 @@ hipError_t launch_propagate(const KParams& P, int64_t n, const SegIn& in, const 
 #else
 #define ART_DBG(stage)
 #endif
-  hipLaunchKernelGGL(init_kernel, dim3((unsigned)(gr < 2048 ? gr : 2048)), dim3(256), 0, s, P, n, in, stats);
+  hipLaunchKernelGGL(init_kernel, dim3((unsigned)(gr < 2048 ? gr : 2048)), dim3(256), 0, s, P, n, (int64_t)0, n, in,
+                     stats);
   ART_DBG("init_kernel")
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   const bool flat = P.rs_eff == 0.0 && !(P.bndry_lyr > 0.0) && !P.isotropic;
   const bool sch = P.rs_eff > 0.0 && !(P.bndry_lyr > 0.0) && !P.isotropic;
   const bool rk4 = P.integrator == ART_RK4;
-  KFn fn = out.donate > 0 ? pick_propagate<true>(out.ntimes >= 2, rk4, flat, sch)
-                           : pick_propagate<false>(out.ntimes >= 2, rk4, flat, sch);
+  KFn fn = out.donate > 0 ? pick_propagate<1>(out.ntimes >= 2, rk4, flat, sch)
+                           : pick_propagate<0>(out.ntimes >= 2, rk4, flat, sch);
   // A batch that fits one ray per lane of 1 wave per SIMD runs the 1-wave/SIMD build, which
   // does not spill: lone GR tail ray -3%, flat -4.5% per attempt, bit-identical
   // (profiles/r02j_small_batch_w1_ab.txt, tests/test_edges.py). ART_W1=0 switches it off (A/B).
@@ -2653,7 +2808,7 @@ hipError_t launch_propagate(const KParams& P, int64_t n, const SegIn& in, const 
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
     if (n <= (int64_t)ncu * 4 * 64) {
-      fn = flat ? propagate_kernel<ART_VERN6, GEOM_FLAT, false, false, 1> : propagate_kernel<ART_VERN6, GEOM_GR, false, false, 1>;
+      fn = flat ? propagate_kernel<ART_VERN6, GEOM_FLAT, false, 0, 1> : propagate_kernel<ART_VERN6, GEOM_GR, false, 0, 1>;
       w1 = true;
     }
   }
@@ -2682,7 +2837,7 @@ hipError_t launch_propagate(const KParams& P, int64_t n, const SegIn& in, const 
     // GR continuations at 1 wave/SIMD: no spills (68 VGPRs spill to scratch at 2). A/B on the
     // configs[3] bench line: 3.21e8 -> 3.35e8 ray-steps/s, bit-identical
     // (profiles/r02h_continuation_w1_ab.txt); flat stays at 2 (measured -3.5% at 1).
-    const KFn cfn = (w1_builds() && sch && !rk4 && out.ntimes < 2) ? propagate_kernel<ART_VERN6, GEOM_GR, false, true, 1> : fn;
+    const KFn cfn = (w1_builds() && sch && !rk4 && out.ntimes < 2) ? propagate_kernel<ART_VERN6, GEOM_GR, false, 1, 1> : fn;
     hipLaunchKernelGGL(cfn, dim3(cgrid), dim3(BLOCK), 0, s, P, n, in, oc, max_crossings, queue, stats);
     ART_DBG("continuation")
     if ((e = hipGetLastError()) != hipSuccess) return e;
@@ -2713,8 +2868,41 @@ hipError_t launch_propagate(const KParams& P, int64_t n, const SegIn& in, const 
     if ((e = hipStreamWaitEvent(fs, ev1, 0)) != hipSuccess) return e;
     sf = fs;
   }
-  hipLaunchKernelGGL(finalize_kernel, dim3(g1), dim3(256), 0, sf, P, n, in, out);
+  hipLaunchKernelGGL(finalize_kernel, dim3(g1), dim3(256), 0, sf, P, n, (int64_t)0, n, in, out);
   ART_DBG("finalize_kernel")
+  return hipGetLastError();
+}
+
+hipError_t launch_init_range(const KParams& P, int64_t n, int64_t i0, int64_t i1, const SegIn& in,
+                             unsigned long long* stats, hipStream_t s) {
+  const int64_t gr = (i1 - i0 + 255) / 256;
+  if (gr <= 0) return hipSuccess;
+  hipLaunchKernelGGL(init_kernel, dim3((unsigned)(gr < 2048 ? gr : 2048)), dim3(256), 0, s, P, n, i0, i1, in, stats);
+  return hipGetLastError();
+}
+
+// The streamed pipeline's integrator: Vern6 (flat / GR / general geometry), no saveat, no
+// donation, `ncus` CUs' worth of persistent blocks (the stream's CU mask leaves the rest to
+// the init and finalize kernels of the pieces).
+hipError_t launch_integrator_streamed(const KParams& P, int64_t n, const SegIn& in, const SegOut& out,
+                                      int32_t max_crossings, unsigned long long* queue, unsigned long long* stats,
+                                      int ncus, hipStream_t s, int* grid_out) {
+  const bool flat = P.rs_eff == 0.0 && !(P.bndry_lyr > 0.0) && !P.isotropic;
+  const bool sch = P.rs_eff > 0.0 && !(P.bndry_lyr > 0.0) && !P.isotropic;
+  const KFn fn = flat ? propagate_kernel<ART_VERN6, GEOM_FLAT, false, 2>
+                      : (sch ? propagate_kernel<ART_VERN6, GEOM_GR, false, 2> : propagate_kernel<ART_VERN6, GEOM_ANY, false, 2>);
+  const int per_cu = ART_WAVES_PER_SIMD * 4 / (BLOCK / 64);
+  const int64_t need = (n + BLOCK - 1) / BLOCK;
+  const int grid = (int)(need < (int64_t)ncus * per_cu ? need : (int64_t)ncus * per_cu);
+  if (grid_out) *grid_out = grid;
+  hipLaunchKernelGGL(fn, dim3(grid), dim3(BLOCK), 0, s, P, n, in, out, max_crossings, queue, stats);
+  return hipGetLastError();
+}
+
+hipError_t launch_finalize_range(const KParams& P, int64_t n, int64_t i0, int64_t m, const SegIn& in,
+                                 const SegOut& ol, hipStream_t s) {
+  if (m <= 0) return hipSuccess;
+  hipLaunchKernelGGL(finalize_kernel, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, P, n, i0, m, in, ol);
   return hipGetLastError();
 }
 

@@ -235,8 +235,9 @@ def test_chunked_host_pipeline_is_bit_exact(cfg, species, cap, chunks, slots, mo
     s = A.sample_conversion_points(p, n, seed=1769)
     q, k, mc = (p, s["k_init"], -1) if species == 1 else (replace(p, B0=-p.B0), -s["k_init"], 100000)
     args = (s["x"], k, s["erg"], -np.ones(n), np.full(n, -30.0), np.full(n, species, np.int8))
-    monkeypatch.setenv("ART_HOST_CHUNKS", "1")
+    monkeypatch.setenv("ART_HOST_MODE", "single")
     ref = A.propagate_batch(q, *args, max_crossings=mc, capacity=cap)
+    monkeypatch.setenv("ART_HOST_MODE", "chunked")
     monkeypatch.setenv("ART_HOST_CHUNKS", str(chunks))
     monkeypatch.setenv("ART_HOST_SLOTS", str(slots))
     monkeypatch.setenv("ART_HOST_CHUNK_MIN", "1000")
@@ -247,3 +248,56 @@ def test_chunked_host_pipeline_is_bit_exact(cfg, species, cap, chunks, slots, mo
     assert np.isnan(got["xc_t"].reshape(cap, n)[:, got["n_cross"] == 0]).all()
     for key in ("attempts", "accepted", "root_steps", "scan_evals", "rays", "cert_steps"):
         assert ref["stats"][key] == got["stats"][key], key
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg,species,cap,shift", [("flat", 1, 1, 11), ("flat", 0, 3, 12), ("gr", 1, 2, 11)])
+def test_streamed_host_pipeline_is_bit_exact(cfg, species, cap, shift, monkeypatch):
+    """art_propagate_host's default for large batches is the streamed pipeline: one integrator
+    launch over the whole batch while pieces of its inputs are still being uploaded and
+    initialised (a wave waits for its rays' fresh state), each piece finalized and downloaded
+    once its last ray is done (a signal the download stream waits on). With pieces of 2^11 or
+    2^12 rays (10 or 5 of them) it returns exactly the single launch's outputs, every crossing
+    slot included, and the same statistics."""
+    from dataclasses import replace
+    import adiabatic_raytracer_amd as A
+    p = A.Params(**CONFIGS[cfg])
+    n = 20011
+    s = A.sample_conversion_points(p, n, seed=1769)
+    q, k, mc = (p, s["k_init"], -1) if species == 1 else (replace(p, B0=-p.B0), -s["k_init"], 100000)
+    args = (s["x"], k, s["erg"], -np.ones(n), np.full(n, -30.0), np.full(n, species, np.int8))
+    monkeypatch.setenv("ART_HOST_MODE", "single")
+    ref = A.propagate_batch(q, *args, max_crossings=mc, capacity=cap)
+    monkeypatch.setenv("ART_HOST_MODE", "stream")
+    monkeypatch.setenv("ART_HOST_PIECE_SHIFT", str(shift))
+    monkeypatch.setenv("ART_HOST_CHUNK_MIN", "1000")
+    for _ in range(2):  # the second call reuses the streams, signals and staging
+        got = A.propagate_batch(q, *args, max_crossings=mc, capacity=cap)
+        for key, v in ref.items():
+            if isinstance(v, np.ndarray):
+                assert np.array_equal(v, got[key], equal_nan=True), (cfg, key)
+        for key in ("attempts", "accepted", "root_steps", "scan_evals", "rays", "cert_steps"):
+            assert ref["stats"][key] == got["stats"][key], key
+
+
+@pytest.mark.gpu
+def test_streamed_host_pipeline_gives_up_cleanly(monkeypatch):
+    """A streamed call whose piece waits outlast their bound (here 0 ms) releases every wait it
+    queued, lets its streams run out and runs the batch again as one launch: the results are
+    the single launch's, and the next streamed call works normally."""
+    import adiabatic_raytracer_amd as A
+    p = A.Params(**CONFIGS["flat"])
+    n = 20011
+    s = A.sample_conversion_points(p, n, seed=1769)
+    args = (s["x"], s["k_init"], s["erg"], -np.ones(n), np.full(n, -30.0), np.ones(n, np.int8))
+    monkeypatch.setenv("ART_HOST_MODE", "single")
+    ref = A.propagate_batch(p, *args)
+    monkeypatch.setenv("ART_HOST_MODE", "stream")
+    monkeypatch.setenv("ART_HOST_PIECE_SHIFT", "11")
+    monkeypatch.setenv("ART_HOST_CHUNK_MIN", "1000")
+    for limit in ("0", "30000"):
+        monkeypatch.setenv("ART_HOST_STREAM_TIMEOUT_MS", limit)
+        got = A.propagate_batch(p, *args)
+        for key, v in ref.items():
+            if isinstance(v, np.ndarray):
+                assert np.array_equal(v, got[key], equal_nan=True), (limit, key)

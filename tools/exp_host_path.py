@@ -2,7 +2,9 @@
 batch, for several pipeline settings (ART_HOST_CHUNKS / ART_HOST_SLOTS / ART_HOST_THREADS are
 read per call). Prints one JSON line per setting; with ART_HOST_TRACE=1 the library also
 prints the host side of every chunk to stderr.
-Usage: exp_host_path.py [rays] [chunks,slots ...]   e.g. exp_host_path.py 10000000 1,1 8,3 16,3"""
+Usage: exp_host_path.py [rays] [setting ...]; a setting is "stream" or "stream:R" (the streamed
+pipeline, R reserved CUs), "single", or "chunks,slots" (the chunked pipeline), e.g.
+exp_host_path.py 10000000 stream single 4,2"""
 import ctypes as C
 import json
 import os
@@ -17,7 +19,7 @@ from adiabatic_raytracer_amd import Engine  # noqa: E402
 from adiabatic_raytracer_amd._lib import CrossingBuf, SegmentOut, check  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 10_000_000
-settings = [tuple(int(v) for v in a.split(",")) for a in sys.argv[2:]] or [(1, 1), (8, 3)]
+settings = sys.argv[2:] or ["stream", "single"]
 eng = Engine(A.Params(theta_m=0.2, mass_a=1e-5, flat=True))
 inp = eng.forward_roots(n, seed=1769)
 h = {k: inp[k].cpu().numpy() for k in ("x0", "k0", "erg", "dw", "ln_t0", "species")}
@@ -37,9 +39,18 @@ def outputs(fault):
 
 cp = eng.cp
 ref = None
-for chunks, slots in settings:
-    os.environ["ART_HOST_CHUNKS"] = str(chunks)
-    os.environ["ART_HOST_SLOTS"] = str(slots)
+for setting in settings:
+    chunks = slots = 0
+    if setting.startswith("stream"):
+        os.environ["ART_HOST_MODE"] = "stream"
+        os.environ["ART_HOST_RESERVE_CUS"] = setting.split(":")[1] if ":" in setting else "8"
+    elif setting == "single":
+        os.environ["ART_HOST_MODE"] = "single"
+    else:
+        chunks, slots = (int(v) for v in setting.split(","))
+        os.environ["ART_HOST_MODE"] = "chunked"
+        os.environ["ART_HOST_CHUNKS"] = str(chunks)
+        os.environ["ART_HOST_SLOTS"] = str(slots)
     for fault in (True, False):
         times = []
         for rep in range(3):
@@ -53,6 +64,6 @@ for chunks, slots in settings:
             ref = o
         same = all(np.array_equal(o[k], ref[k], equal_nan=True) for k in o)
         ms = min(times[1:]) * 1e3
-        print(json.dumps({"rays": n, "chunks": chunks, "slots": slots, "outputs_prefaulted": fault, "ms": ms,
+        print(json.dumps({"rays": n, "setting": setting, "chunks": chunks, "slots": slots, "outputs_prefaulted": fault, "ms": ms,
                           "ms_all": [t * 1e3 for t in times], "ray_steps_per_s": acc / (ms * 1e-3),
                           "kernel_ms_sum": lib.art_last_kernel_ms(), "bit_identical_to_first": same}), flush=True)
