@@ -773,10 +773,20 @@ int propagate_host_chunked(DeviceCtx* c, const art_params* p, int64_t n, const d
 // signal): the call's results are discarded and the batch runs again on another path.
 constexpr int STREAM_FALLBACK = 1 << 20;
 
+// The streamed pipeline's three streams, each its own hardware queue (a CU-masked stream gets
+// one; a stream that shared a queue could sit behind another's wait): the integrator's on all
+// CUs but `reserve`, the uploads' (with the pieces' init kernels) and the downloads' (with the
+// finalize kernels) on those `reserve` CUs, the last logical CUs of the device -- one per XCD
+// for reserve = 8 (tools/probe_cumask.hip). A helper mask must reach every XCD: a kernel's
+// blocks are dealt to the XCDs round-robin, and blocks dealt to an XCD without a CU of the mask
+// never run (8 CUs from one XCD: every call gave up, profiles/r03zd_streamed_reserve.txt).
+// Tried: helpers in block slots the integrator's grid leaves free (no masks): they fit only
+// with 32 free slots and an init kernel bounded to 256 VGPRs (94 spilled), and were no faster.
 int stream_setup(DeviceCtx* c, int reserve, int nsig) {
   int ncu = 0;
   HIP_OK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device));
-  if (reserve < 1 || reserve >= ncu / 2) return fail(ART_E_INVALID, "ART_HOST_RESERVE_CUS out of range");
+  if (reserve < 8 || reserve % 8 != 0 || reserve >= ncu / 2)
+    return fail(ART_E_INVALID, "ART_HOST_RESERVE_CUS must be a multiple of 8 in [8, %s)", std::to_string(ncu / 2).c_str());
   const int key = reserve * 2 + (env_int("ART_HOST_RESERVE_XCD", 0) != 0 ? 1 : 0);
   if (!c->s_comp || c->reserve != key) {
     for (hipStream_t* st : {&c->s_comp, &c->s_in, &c->s_out})
@@ -785,12 +795,10 @@ int stream_setup(DeviceCtx* c, int reserve, int nsig) {
         HIP_OK(hipStreamDestroy(*st));
         *st = nullptr;
       }
-    // logical CUs ncu - reserve .. ncu - 1: for reserve = 8 one CU of each XCD (the mask's
-    // last bits are spread over the XCDs, tools/probe_cumask.hip)
     const int words = (ncu + 31) / 32;
     std::vector<uint32_t> mc(words, 0u), mh(words, 0u);
-    // ART_HOST_RESERVE_XCD=1 (dev): the reserved CUs from the last XCD (logical CU i sits on XCD
-    // i % 8) instead of one per XCD
+    // (ART_HOST_RESERVE_XCD=1, dev: the reserved CUs from the last XCD -- logical CU i sits on
+    // XCD i % 8 -- which starves the helpers, see above)
     const bool one_xcd = env_int("ART_HOST_RESERVE_XCD", 0) != 0;
     int taken = 0;
     for (int i = ncu - 1; i >= 0; --i) {
@@ -834,9 +842,9 @@ int stream_setup(DeviceCtx* c, int reserve, int nsig) {
 //   * the download stream waits for each piece's signal (hipStreamWaitValue64), finalizes the
 //     piece into its own SoA blob in HBM and copies the blob to pinned memory (DMA engines);
 //   * the host scatters the pieces into the caller's arrays as they land.
-// The init and finalize kernels run on the `reserve` CUs the integrator's stream leaves free
-// (CU-masked streams, each its own hardware queue, so no queue order can hold one stream
-// behind another). Per-ray results do not depend on the launch split (tests/test_edges.py), so
+// The init and finalize kernels run on the `reserve` CUs the integrator's stream leaves out
+// (three CU-masked streams, each its own hardware queue, so no queue order can hold one stream
+// behind another, stream_setup). Per-ray results do not depend on the launch split (tests/test_edges.py), so
 // the outputs equal the single launch's bit for bit. Any wait that outlasts its bound makes
 // the call fall back (STREAM_FALLBACK) instead of hanging.
 int propagate_host_streamed(DeviceCtx* c, const art_params* p, int64_t n, const double* x0, const double* k0,
@@ -952,8 +960,8 @@ int propagate_host_streamed(DeviceCtx* c, const art_params* p, int64_t n, const 
   so.abort_word = c->abort_dev;
   so.piece_shift = shift;
   HIP_OK(hipEventRecord(L->ev0, c->s_comp));
-  HIP_OK(art::launch_integrator_streamed(K, n, in, so, max_crossings, words, words + 1, ncu - reserve, c->s_comp,
-                                         &L->grid));
+  const int blocks = 2 * (ncu - reserve);  // persistent: 2 per CU of the integrator's mask
+  HIP_OK(art::launch_integrator_streamed(K, n, in, so, max_crossings, words, words + 1, blocks, c->s_comp, &L->grid));
   HIP_OK(hipEventRecord(L->ev1, c->s_comp));
   HIP_OK(hipMemcpyAsync(L->host_stats, words + 1, sizeof(unsigned long long) * art::N_STATS, hipMemcpyDeviceToHost,
                         c->s_comp));

@@ -82,13 +82,13 @@ hipError_t launch_propagate(const KParams& P, int64_t n, const SegIn& in, const 
                             unsigned long long* queue, unsigned long long* stats, hipStream_t s, int* grid_out,
                             hipEvent_t ev0, hipEvent_t ev1, hipStream_t fs = nullptr);
 // The streamed host pipeline's launches (art_capi.cpp, propagate_host_streamed): init of rays
-// [i0, i1); the integrator (DON = 2) with `blocks` persistent blocks; finalize of rays
+// [i0, i1); the integrator (DON = 2) with at most `blocks` persistent blocks; finalize of rays
 // [i0, i0 + m) into piece-local SoA outputs `ol` (row stride m).
 hipError_t launch_init_range(const KParams& P, int64_t n, int64_t i0, int64_t i1, const SegIn& in,
                              unsigned long long* stats, hipStream_t s);
 hipError_t launch_integrator_streamed(const KParams& P, int64_t n, const SegIn& in, const SegOut& out,
                                       int32_t max_crossings, unsigned long long* queue, unsigned long long* stats,
-                                      int ncus, hipStream_t s, int* grid_out);
+                                      int blocks, hipStream_t s, int* grid_out);
 hipError_t launch_finalize_range(const KParams& P, int64_t n, int64_t i0, int64_t m, const SegIn& in,
                                  const SegOut& ol, hipStream_t s);
 hipError_t launch_sample(const KParams& P, double maxR, uint64_t seed, int64_t ray_offset, int64_t n, double* x,

@@ -260,33 +260,8 @@ __device__ inline double illinois_interp(const KParams& P, const double* u0, con
   return tr;
 }
 
-// A 16-byte record store. WT (the streamed pipeline, ART_STREAM_WT): a system-coherent
-// store (sc0 sc1: written through the XCD's L2 to memory), so a wave makes its records visible
-// to every XCD with a wait for its stores instead of an L2 write-back.
-typedef double art_d2 __attribute__((ext_vector_type(2)));
-typedef int art_i4 __attribute__((ext_vector_type(4)));
-template <bool WT>
-__device__ inline void rec_store(double2* p, double a, double b) {
-  if constexpr (WT) {
-    const art_d2 v = {a, b};
-    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(p), "v"(v) : "memory");
-  } else {
-    *p = make_double2(a, b);
-  }
-}
-template <bool WT>
-__device__ inline void rec_store(int4* p, int a, int b, int c, int d) {
-  if constexpr (WT) {
-    const art_i4 v = {a, b, c, d};
-    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(p), "v"(v) : "memory");
-  } else {
-    *p = make_int4(a, b, c, d);
-  }
-}
-
 // ---------------------------------------------------------------------------
 // affect! (RayTracer.jl:301-350). Returns 0 = skipped, 1 = recorded, 2 = recorded + terminate.
-template <bool WT = false>
 __device__ inline int affect(const KParams& P, const SegIn& in, const SegOut& out, int64_t n, int64_t ray,
                              const double* u, double tau, double erg, int& ncross, int max_crossings) {
   double st, ct, sp, cp;
@@ -311,10 +286,10 @@ __device__ inline int affect(const KParams& P, const SegIn& in, const SegOut& ou
   if (out.xcount && j < out.cap) {
     const double dwc = u[6] / erg;  // P_nonAD: finalize_kernel
     double2* rq = reinterpret_cast<double2*>(out.xrec + ((int64_t)ray * out.cap + j) * X_REC);
-    rec_store<WT>(rq + 0, x[0], x[1]);
-    rec_store<WT>(rq + 1, x[2], k[0]);
-    rec_store<WT>(rq + 2, k[1], k[2]);
-    rec_store<WT>(rq + 3, exp(tau), dwc);
+    rq[0] = make_double2(x[0], x[1]);
+    rq[1] = make_double2(x[2], k[0]);
+    rq[2] = make_double2(k[1], k[2]);
+    rq[3] = make_double2(exp(tau), dwc);
   }
   ncross = j + 1;
   const int maxc = max_crossings <= 0 ? -1 : max_crossings;
@@ -409,11 +384,6 @@ constexpr int SCAN_WORDS = 4;  // 2-bit codes for up to 64 grid points (interp_p
 #ifndef ART_WAVES_PER_SIMD
 #define ART_WAVES_PER_SIMD 2
 #endif
-#ifdef ART_STREAM_WT
-constexpr bool STREAM_WT = true;
-#else
-constexpr bool STREAM_WT = false;
-#endif
 #ifndef ART_STREAM_FLUSH
 #define ART_STREAM_FLUSH 31  // (DON = 2) a wave's finished-ray counts go out every 32 iterations
 #endif
@@ -467,10 +437,7 @@ __device__ inline int64_t stream_poll(const SegOut& out, int leader) {
 // counts (at most every 32 iterations, at a piece change and at exit), so the L2 write-backs of
 // the release stay rare.
 __device__ inline void stream_count(const SegOut& out, int64_t n, int p, unsigned long long c) {
-  if constexpr (STREAM_WT)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's write-through records are in memory
-  else
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
   const int leader = __ffsll((long long)__ballot(1)) - 1;
   if ((int)(threadIdx.x & 63) == leader) {
     const unsigned long long old = __hip_atomic_fetch_add(out.piece_cnt + p, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -550,16 +517,9 @@ __global__ __launch_bounds__(BLOCK, WPS) void propagate_kernel(const KParams P_i
   double hroot = 0.0, r_tha = 0.0, r_ca = 0.0, r_thb = 0.0, r_cb = 0.0, r_t = 0.0, r_slope = 1.0, post_c = 0.0;
   int post_s = 0, r_side = 0, r_it = 0;
   int wnext = 0, wend = 0;
-  // (DON = 2) per wave, in LDS to keep them out of the integrator's registers: the ready counter
-  // as last read, the piece whose finished rays are being counted, that count, a tick
-  __shared__ long long s_strm[4 * (BLOCK / 64)];
-  volatile long long* const strm = s_strm + 4 * (threadIdx.x >> 6);
-  if (DON == 2) {
-    strm[0] = 0;
-    strm[1] = -1;
-    strm[2] = 0;
-    strm[3] = 0;
-  }
+  int64_t rdy = 0;                       // (DON = 2) the ready counter as last read
+  int pend_p = -1, tick = 0;             // (DON = 2) the piece whose finished rays are being counted
+  unsigned long long pend_c = 0;         //           and their count (per wave; in LDS: 1.5% slower)
   int save_k = 1;  // SAVE: the next interior saveat index
   bool exhausted = false;
   unsigned s_att = 0, s_acc = 0, s_root = 0, s_scan = 0, s_interp = 0, s_rays = 0, s_cert = 0;
@@ -625,20 +585,15 @@ __global__ __launch_bounds__(BLOCK, WPS) void propagate_kernel(const KParams P_i
           wend = __builtin_amdgcn_readfirstlane((int)((int64_t)base + CHUNK < nq ? (int64_t)base + CHUNK : nq));
         }
         int lim = wend;
-#ifdef ART_STREAM_NOGATE
-        if constexpr (false) {  // dev timing build: the inputs are all in HBM before the launch
-#else
         if constexpr (DON == 2) {
-#endif
           // only rays whose fresh state has arrived; while none of the chunk has, a wave with
           // other rays goes on integrating them, and an empty wave waits (bounded)
           const int leader = __ffsll((long long)need) - 1;
-          int64_t rdy = strm[0];
-          if (rdy < wend) strm[0] = rdy = stream_poll(out, leader);
+          if (rdy < wend) rdy = stream_poll(out, leader);
           if (rdy <= wnext) {
             if (__ballot(mode != M_IDLE) != 0ull) break;
             if (!stream_ready(out, wnext + 1, leader)) { exhausted = true; break; }
-            strm[0] = rdy = stream_poll(out, leader);
+            rdy = stream_poll(out, leader);
           }
           lim = rdy < wend ? (int)rdy : wend;
         }
@@ -1323,7 +1278,7 @@ __global__ __launch_bounds__(BLOCK, WPS) void propagate_kernel(const KParams P_i
     if (root_done || (scan && !hit)) bstart = bend;
     if (root_done) {
       const double tau_r = tau + hs;
-      const int a = affect<DON == 2 && STREAM_WT>(P, in, out, n, ray, u, tau_r, erg, ncross, max_crossings);
+      const int a = affect(P, in, out, n, ray, u, tau_r, erg, ncross, max_crossings);
       tau = tau_r;
       cprev = post_c;  // the post-event side (DiffEq repeat_nudge): the root is not re-found
       cprev_ok = true;
@@ -1349,14 +1304,13 @@ __global__ __launch_bounds__(BLOCK, WPS) void propagate_kernel(const KParams P_i
     int fin_piece = -1;  // (DON = 2) the piece of a ray finishing now
     if (finish >= 0) {  // the raw end record; finalize_kernel back-transforms it (RayTracer.jl:393-416)
       if constexpr (DON == 2) fin_piece = ray >> out.piece_shift;
-      constexpr bool WT = DON == 2 && STREAM_WT;
       double2* rq = reinterpret_cast<double2*>(out.rec + (int64_t)ray * END_REC);
-      rec_store<WT>(rq + 0, u[0], u[1]);
-      rec_store<WT>(rq + 1, u[2], u[3]);
-      rec_store<WT>(rq + 2, u[4], u[5]);
-      rec_store<WT>(rq + 3, u[6], tau);
+      rq[0] = make_double2(u[0], u[1]);
+      rq[1] = make_double2(u[2], u[3]);
+      rq[2] = make_double2(u[4], u[5]);
+      rq[3] = make_double2(u[6], tau);
       int4* ri = reinterpret_cast<int4*>(rq + 4);
-      rec_store<WT>(ri, finish, n_acc, n_rej, ncross);
+      ri[0] = make_int4(finish, n_acc, n_rej, ncross);
       if constexpr (SAVE) ri[1] = make_int4(save_k + 1, 0, 0, 0);  // start + interior + end
       ray = -1;
       mode = M_IDLE;
@@ -1368,21 +1322,17 @@ __global__ __launch_bounds__(BLOCK, WPS) void propagate_kernel(const KParams P_i
       while (fm != 0ull) {
         const int pc = __shfl(fin_piece, __ffsll((long long)fm) - 1);
         const unsigned long long same = __ballot(fin_piece == pc);
-        if (pc != (int)strm[1]) {
-          if (strm[2] != 0) stream_count(out, n, (int)strm[1], (unsigned long long)strm[2]);
-          strm[1] = pc;
-          strm[2] = 0;
+        if (pc != pend_p) {
+          if (pend_c != 0ull) stream_count(out, n, pend_p, pend_c);
+          pend_p = pc;
+          pend_c = 0ull;
         }
-        strm[2] = strm[2] + __popcll(same);
+        pend_c += (unsigned long long)__popcll(same);
         fm &= ~same;
       }
-      if (strm[2] != 0) {
-        const long long t = strm[3] + 1;
-        strm[3] = t;
-        if ((t & ART_STREAM_FLUSH) == 0 || exhausted) {
-          stream_count(out, n, (int)strm[1], (unsigned long long)strm[2]);
-          strm[2] = 0;
-        }
+      if (pend_c != 0ull && ((++tick & ART_STREAM_FLUSH) == 0 || exhausted)) {
+        stream_count(out, n, pend_p, pend_c);
+        pend_c = 0ull;
       }
     }
     ART_TMARK(0)  // saveat, reload, events, finish and the output stores (+ refill)
@@ -1413,7 +1363,7 @@ __global__ __launch_bounds__(BLOCK, WPS) void propagate_kernel(const KParams P_i
   }
 
   if constexpr (DON == 2) {
-    if (strm[2] != 0) stream_count(out, n, (int)strm[1], (unsigned long long)strm[2]);
+    if (pend_c != 0ull) stream_count(out, n, pend_p, pend_c);
   }
   // wave-reduce the statistics and add them once per wave
 #if defined(ART_SLOT_TIMING)
@@ -2882,18 +2832,17 @@ hipError_t launch_init_range(const KParams& P, int64_t n, int64_t i0, int64_t i1
 }
 
 // The streamed pipeline's integrator: Vern6 (flat / GR / general geometry), no saveat, no
-// donation, `ncus` CUs' worth of persistent blocks (the stream's CU mask leaves the rest to
-// the init and finalize kernels of the pieces).
+// donation, at most `blocks` persistent blocks (the block slots it leaves free run the init and
+// finalize kernels of the pieces).
 hipError_t launch_integrator_streamed(const KParams& P, int64_t n, const SegIn& in, const SegOut& out,
                                       int32_t max_crossings, unsigned long long* queue, unsigned long long* stats,
-                                      int ncus, hipStream_t s, int* grid_out) {
+                                      int blocks, hipStream_t s, int* grid_out) {
   const bool flat = P.rs_eff == 0.0 && !(P.bndry_lyr > 0.0) && !P.isotropic;
   const bool sch = P.rs_eff > 0.0 && !(P.bndry_lyr > 0.0) && !P.isotropic;
   const KFn fn = flat ? propagate_kernel<ART_VERN6, GEOM_FLAT, false, 2>
                       : (sch ? propagate_kernel<ART_VERN6, GEOM_GR, false, 2> : propagate_kernel<ART_VERN6, GEOM_ANY, false, 2>);
-  const int per_cu = ART_WAVES_PER_SIMD * 4 / (BLOCK / 64);
   const int64_t need = (n + BLOCK - 1) / BLOCK;
-  const int grid = (int)(need < (int64_t)ncus * per_cu ? need : (int64_t)ncus * per_cu);
+  const int grid = (int)(need < (int64_t)blocks ? need : (int64_t)blocks);
   if (grid_out) *grid_out = grid;
   hipLaunchKernelGGL(fn, dim3(grid), dim3(BLOCK), 0, s, P, n, in, out, max_crossings, queue, stats);
   return hipGetLastError();
