@@ -1,11 +1,24 @@
 #!/bin/bash
-# Round-end evidence for profiles/: the GPU test suite, smoke, the default bench line, a
-# rocprofv3 kernel-trace summary of the same command, and the GR / 1e6 / scan side figures.
-# Usage: tools/gpu_final.sh TAG   (writes gpurun_out/TAG_*; stops at the first failure)
-TAG=${1:-r02b}
+# Round-end evidence for profiles/: the GPU test suite, smoke, the PMC passes of this library
+# build (so bench.py reports roofline.traffic), the default bench line, a rocprofv3 kernel-trace
+# summary of the same command, and the GR / scan / sampler / host-path side figures.
+# Usage: TAG=r03z9 bash tools/gpu_final.sh   (writes gpurun_out/TAG_*; stops at the first failure)
+TAG=${TAG:-r03final}
+set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
-timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/${TAG}_pytest_gpu.log 2>&1 || exit 1
+timeout -k 10 900 python3 -u -m pytest tests -m gpu -v --timeout 600 --timeout-method thread > gpurun_out/${TAG}_pytest_gpu.log 2>&1
+rc=$?; echo "pytest rc=$rc"; [ $rc -le 1 ] || exit $rc
 timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${TAG}_smoke.log 2>&1 || exit 1
-timeout -k 10 600 python3 bench.py > gpurun_out/${TAG}_bench_flat1e7.json 2> gpurun_out/${TAG}_bench.err || exit 1
+bash tools/pmc_passes.sh gpurun_out/${TAG}_pmc 10000000 > gpurun_out/${TAG}_pmc.log 2>&1 || exit 1
+cp gpurun_out/${TAG}_pmc/pmc_summary.json profiles/pmc_summary.json || exit 1
+timeout -k 10 600 python3 -u bench.py > gpurun_out/${TAG}_bench_flat1e7.json 2> gpurun_out/${TAG}_bench.err || exit 1
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_prof -o prof --output-format csv -- python3 bench.py --steps 5 --no-cpu-baseline --no-pcie > gpurun_out/${TAG}_bench_prof.json 2>&1 || exit 1
+for s in 8 12; do
+  timeout -k 10 300 python3 -u bench.py --config gr --rays 1000000 --streams $s --steps 12 --no-cpu-baseline --no-pcie > gpurun_out/${TAG}_bench_gr1e6_s$s.json 2>> gpurun_out/${TAG}_gr.err || exit 1
+done
+timeout -k 10 300 python3 -u tools/exp_scan_streams.py 1000000 8 32 16 > gpurun_out/${TAG}_param_scan_1e6_8streams.jsonl 2> gpurun_out/${TAG}_scan.err || exit 1
+timeout -k 10 300 python3 -u tools/exp_sampler_time.py > gpurun_out/${TAG}_sampler_time.jsonl 2> gpurun_out/${TAG}_sampler.err || exit 1
+TAIL_DONATE=4 timeout -k 10 300 python3 -u tools/exp_gr_tail.py > gpurun_out/${TAG}_gr_tail.jsonl 2> gpurun_out/${TAG}_gr_tail.err || exit 1
+ART_HOST_TRACE=1 timeout -k 10 200 python3 -u tools/exp_host_path.py 10000000 stream single > gpurun_out/${TAG}_host_path.jsonl 2> gpurun_out/${TAG}_host_path.err || exit 1
+echo done
