@@ -136,7 +136,7 @@ def main():
     ap.add_argument("--nbins", type=int, default=50)
     ap.add_argument("--streams", type=int, default=0,
                     help="batches in flight (HIP streams); 0: 1 for per-GPU batches of >= 8e6 rays, else 4 "
-                         "(8 for the GR config)")
+                         "(12 for the GR config)")
     ap.add_argument("--cpu-rays", type=int, default=int(os.environ.get("ART_CPU_RAYS", "500000")))
     ap.add_argument("--cpu-rays-1t", type=int, default=int(os.environ.get("ART_CPU_RAYS_1T", "24000")))
     ap.add_argument("--donate", type=int, default=-1,
@@ -151,14 +151,14 @@ def main():
         # hides most of it there. Measured per shard size with donation
         # (profiles/r02d_streams_by_shard_donation.txt): 1e6-5e6 rays best with 3 passes in
         # flight; round 3 (tail kernel, two-level donation): 1.25e6 rays 3.16e9 on 3 streams,
-        # 3.31e9 on 4, 3.30e9 on 6 (profiles/r03q_bench_1p25e6_s*.json), so 4. The GR batch is
-        # bound by its longest ray (~185 ms alone), so only more passes in flight amortise
-        # it: 4.2e8 on 3, 5.2e8 on 4, 6.3e8 on 6, 7.5e8 on 8 (profiles/r03p_*, r03q_*), so 8
+        # 3.31e9 on 4, 3.30e9 on 6, so 4. The GR batch is bound by its longest ray (~185 ms
+        # alone on the tail kernel), so only more passes in flight amortise it: 4.2e8 on 3,
+        # 6.3e8 on 6, 6.1e8 on 8, 8.7e8 on 12 (profiles/r03fin1_bench_gr1e6_s*.json), so 12
         # for the GR configs. Overlapped launches stretch each other's measured duration, so
         # the single-GPU headline (1e7 rays) runs one pass at a time and its roofline is the
-        # kernel's own (2 passes with donation: +1%, profiles/r03q_bench_s2.json).
+        # kernel's own (2 passes with donation: +1%).
         gr = not CONFIGS[args.config].get("flat", False)
-        args.streams = 1 if n_shard >= 8_000_000 else (8 if gr else 4)
+        args.streams = 1 if n_shard >= 8_000_000 else (12 if gr else 4)
     # concurrent passes need a hardware queue each (read at HIP init; the image's default is 4)
     if args.streams > 3 and int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < args.streams + 1:
         os.environ["GPU_MAX_HW_QUEUES"] = str(min(16, args.streams + 1))
