@@ -12,13 +12,17 @@ draws), and requires the GPU-vs-oracle discrepancy to be no larger than the enve
 per-ray maximum) of those oracle-vs-oracle discrepancies:
   * segment status agreement >= min(0.99, perturbed agreement - 0.02);
   * final position and momentum, u7, ln t, the crossing's position, momentum, t, Δω and
-    conversion probability: the 50th, 90th and 99th
-    percentiles of the relative error are <= 10x the perturbed run's percentiles
-    (+1e-12), and the fraction of rays off by more than 1e-3 exceeds the perturbed
-    run's by at most 0.01 (chaotic rays, e.g. grazing a kink of |B_z|, exist in both);
+    conversion probability: the 50th, 90th and 99th percentiles of the relative error are
+    <= 2x, 4x and 6x the perturbed run's percentiles (+1e-12), and the fraction of rays off by
+    more than 1e-3 exceeds the perturbed run's by at most 0.006 (chaotic rays, e.g. grazing a
+    kink of |B_z|, exist in both). Round 3 measured at most 1.2x, 3.2x and 5.1x and 0.0047
+    over every comparison (profiles/r03par_parity.jsonl); round 2 allowed 10x and 0.01;
   * the median accepted-step count differs by <= 1.
 Measured (MI355X, 512 rays): median x_end error 5e-14 (flat) / 5e-11 (GR), p99 1-2e-5,
 exactly the oracle's own 1-ulp sensitivity (p99 1.4-3e-5)."""
+import json
+import os
+
 import numpy as np
 import pytest
 
@@ -61,10 +65,19 @@ def _rel1(a, b, key):
 def _within(err, ref_err, what):
     qs = [50, 90, 99]
     e, r = np.percentile(err, qs), np.percentile(ref_err, qs)
-    assert np.all(e <= 10.0 * r + 1e-12), (what, "gpu", e, "oracle 1-ulp", r)
-    # outliers (> 1e-3): chaotic rays exist in both; at most 1% of rays more than the oracle's own
+    if os.environ.get("ART_PARITY_REPORT"):  # the measured margins, one JSON line per comparison
+        with open(os.environ["ART_PARITY_REPORT"], "a") as fh:
+            fh.write(json.dumps({"test": os.environ.get("PYTEST_CURRENT_TEST", "").split(" ")[0], "what": what,
+                                 "gpu": e.tolist(), "oracle_1ulp": r.tolist(),
+                                 "outliers": [float(np.mean(err > 1e-3)), float(np.mean(ref_err > 1e-3))]}) + "\n")
+    # round 3 measured at most 1.2x / 3.2x / 5.1x the oracle's own 1-ulp envelope at the 50th /
+    # 90th / 99th percentile over every comparison of this module and of test_gpu_saveat.py and
+    # test_gpu_configs2_full.py (profiles/r03par_parity.jsonl); round 2 allowed 10x throughout
+    assert np.all(e <= np.array([2.0, 4.0, 6.0]) * r + 1e-12), (what, "gpu", e, "oracle 1-ulp", r)
+    # outliers (> 1e-3): chaotic rays exist in both; at most 0.6% of rays (3 of 512) more than the
+    # oracle's own (measured: at most 0.47%; round 2 allowed 1%)
     bad, bad_ref = np.mean(err > 1e-3), np.mean(ref_err > 1e-3)
-    assert bad <= bad_ref + 0.01, (what, bad, bad_ref, err.max())
+    assert bad <= bad_ref + 0.006, (what, bad, bad_ref, err.max())
 
 
 def _crossings(a, b, n, mask):
@@ -276,7 +289,6 @@ def test_axion_backtrace_all_crossings(cfg, flip_b0, oracle_lib):
 def test_golden_fixture_roundtrip(oracle_lib):
     """The committed golden fixture (tests/golden/segments_flat.npz, generated by the oracle
     with tests/golden/make_golden.py) is reproduced by the GPU."""
-    import os
     import adiabatic_raytracer_amd as A
     path = os.path.join(os.path.dirname(__file__), "golden", "segments_flat.npz")
     z = np.load(path)
@@ -284,18 +296,30 @@ def test_golden_fixture_roundtrip(oracle_lib):
     p = A.Params(**{k: z["params_" + k].item() for k in ("theta_m", "mass_a", "flat")})
     g = A.propagate_batch(p, z["x0"], z["k0"], z["erg"], z["dw"], z["ln_t0"], z["species"], max_crossings=-1)
     same = g["status"] == z["status"]
-    assert same.mean() >= 0.98
-    # the bulk is reproduced to rounding; the tail at the oracle's own 1-ulp sensitivity (module doc)
+    if os.environ.get("ART_PARITY_REPORT"):
+        rep = {"status_same": float(same.mean())}
+        for key in ("x_end", "k_end"):
+            rep[key] = np.percentile(_rel_end(g, z, n, key)[same], [50, 99]).tolist()
+        for key in ("u7_end", "tau_end"):
+            rep[key] = np.percentile(_rel1(g, z, key)[same], [50, 99]).tolist()
+        cc = same & (z["status"] == 1) & (g["n_cross"] == z["n_cross"])
+        rep.update({w: np.percentile(r_, [50, 99]).tolist() for w, r_ in _crossings(g, z, n, cc).items()})
+        with open(os.environ["ART_PARITY_REPORT"], "a") as fh:
+            fh.write(json.dumps({"test": "golden_fixture", **rep}) + "\n")
+    assert same.mean() >= 0.995  # measured 1.0
+    # the bulk is reproduced to rounding; the tail at the oracle's own 1-ulp sensitivity (module
+    # doc). Measured (profiles/r03par2_parity.jsonl): medians <= 1e-12, 99th percentiles <= 1.9e-5
+    # (k_end); the bounds are 1e-11 and 6e-5 (round 2: 1e-9 and 3e-4)
     for key in ("x_end", "k_end"):
         rel = _rel_end(g, z, n, key)[same]
-        assert np.median(rel) <= 1e-9 and np.percentile(rel, 99) <= 3e-4, (key, np.percentile(rel, [50, 99]))
+        assert np.median(rel) <= 1e-11 and np.percentile(rel, 99) <= 6e-5, (key, np.percentile(rel, [50, 99]))
     for key in ("u7_end", "tau_end"):
         rel = _rel1(g, z, key)[same]
-        assert np.median(rel) <= 1e-9 and np.percentile(rel, 99) <= 3e-4, (key, np.percentile(rel, [50, 99]))
+        assert np.median(rel) <= 1e-11 and np.percentile(rel, 99) <= 6e-5, (key, np.percentile(rel, [50, 99]))
     c = same & (z["status"] == 1) & (g["n_cross"] == z["n_cross"])
     assert c.sum() >= 20
     for what, rel in _crossings(g, z, n, c).items():
-        assert np.median(rel) <= 1e-9 and np.percentile(rel, 99) <= 3e-4, (what, np.percentile(rel, [50, 99]))
+        assert np.median(rel) <= 1e-11 and np.percentile(rel, 99) <= 6e-5, (what, np.percentile(rel, [50, 99]))
     assert np.array_equal(g["n_cross"][same], z["n_cross"][same])
 
 

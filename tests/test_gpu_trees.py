@@ -68,8 +68,19 @@ def test_forward_trees_match_oracle(oracle_lib, mode):
             rel.extend(np.abs(g["weight"] - w_o) / np.abs(w_o))
             xo = np.array([e.x_end for e in tree])
             rel.extend(np.abs(g["x_end"] - xo).max(1) / np.linalg.norm(xo, axis=1))
-    assert same >= 0.9 * n, (same, n)
+    _report(f"forward_{mode}", same, n, rel)
+    assert same >= 0.95 * n, (same, n)  # measured 48 of 48 (profiles/r03par_parity.jsonl); round 2: 0.9
     assert np.median(rel) <= 1e-8, np.percentile(rel, [50, 90, 100])
+
+
+def _report(what, same, n, rel):
+    """The measured agreement, one JSON line per test (ART_PARITY_REPORT=path)."""
+    import json
+    import os
+    if os.environ.get("ART_PARITY_REPORT"):
+        with open(os.environ["ART_PARITY_REPORT"], "a") as fh:
+            fh.write(json.dumps({"test": "trees", "what": what, "same_trees": same, "n": n,
+                                 "rel_p50_p90_max": np.percentile(rel, [50, 90, 100]).tolist()}) + "\n")
 
 
 def test_backtrace_trees_match_oracle(oracle_lib):
@@ -93,7 +104,8 @@ def test_backtrace_trees_match_oracle(oracle_lib):
         if nb["n_cross"][i] == len(e.xc):
             same += 1
             rel.append(abs(nb["weight"][i] * nb["prob"][i] - e.weight * e.prob) / (e.weight * e.prob))
-    assert same >= 0.9 * n, same
+    _report("backtrace", same, n, rel)
+    assert same >= 0.95 * n, same  # measured 47 of 48
     assert np.median(rel) <= 1e-8, np.percentile(rel, [50, 90, 100])
 
 
