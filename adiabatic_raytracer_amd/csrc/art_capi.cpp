@@ -327,14 +327,17 @@ struct ScratchLayout {
   size_t head = 256, u0b = 0, recb = 0, xrb = 0, ncont = 0, contb = 0;
   size_t total() const { return head + u0b + recb + xrb + contb; }
 };
-int scratch_layout(DeviceCtx* c, int64_t n, int cap, int32_t donate, ScratchLayout* L) {
+int scratch_layout(DeviceCtx* c, int64_t n, int cap, int32_t donate, ScratchLayout* L, bool small_tail = false) {
   const size_t nd = (size_t)n;
   L->u0b = nd * 16 * sizeof(double);
   L->recb = nd * art::END_REC * sizeof(double);
   L->xrb = (size_t)cap * nd * art::X_REC * sizeof(double);
-  // tail donation: at most (resident waves) x donate records of CONT_REC doubles
+  // tail donation: at most (resident waves) x donate records of CONT_REC doubles; a small batch
+  // sent to the tail kernel: one record per ray
   L->ncont = 0;
-  if (donate > 0) {
+  if (small_tail) {
+    L->ncont = nd;
+  } else if (donate > 0) {
     int ncu = 0;
     HIP_OK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device));
     L->ncont = std::min(nd, (size_t)ncu * 32 * (size_t)donate);
@@ -357,9 +360,13 @@ int propagate_device_impl(const art_params* p, int64_t n, const double* x0, cons
   hipStream_t s = pick(c, stream);
   const art::KParams K = kparams(*p);
   const int cap = (xc && xc->count) ? xc->capacity : 0;
-  const int32_t donate = launch_donate(c, opt);
+  // a small Vern6 batch without saveat runs every ray on a wave of its own (tail_kernel): the
+  // latency of a Julia host's per-event calls (its rays run ~40% faster per attempt than a lone
+  // lane of the persistent integrator), bit-identical results
+  const bool small_tail = tr.ntimes == 0 && p->integrator == ART_VERN6 && n <= art::small_tail_limit();
+  const int32_t donate = small_tail ? 0 : launch_donate(c, opt);
   ScratchLayout SL;
-  if ((rc = scratch_layout(c, n, cap, donate, &SL))) return rc;
+  if ((rc = scratch_layout(c, n, cap, donate, &SL, small_tail))) return rc;
   const size_t head = SL.head, u0b = SL.u0b, recb = SL.recb, xrb = SL.xrb, ncont = SL.ncont;
   LaunchRec* L;
   if ((rc = take_slot(c, &L))) return rc;
@@ -393,6 +400,7 @@ int propagate_device_impl(const art_params* p, int64_t n, const double* x0, cons
     so.cont2_count = words + 18;
     so.cont2_queue = words + 19;
     so.donate = donate;
+    so.small_tail = small_tail ? 1 : 0;
   }
   HIP_OK(hipMemsetAsync(words, 0, head, s));
   HIP_OK(art::launch_propagate(K, n, in, so, max_crossings, words, words + 1, s, &L->grid, L->ev0, L->ev1,

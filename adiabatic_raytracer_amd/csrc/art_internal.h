@@ -65,6 +65,10 @@ struct SegOut {
   unsigned long long* const* piece_sig;
   unsigned int* abort_word;
   int32_t piece_shift;
+  // Small batches (art_capi.cpp, propagate_device_impl): 1 = every fresh ray goes straight to
+  // tail_kernel, one wave per ray (pack_fresh_kernel writes their CONT_REC records to cont),
+  // instead of one lane per ray of the persistent integrator
+  int32_t small_tail;
 };
 constexpr unsigned long long STREAM_WAIT_TICKS = 200000000ull;  // 2 s at 100 MHz
 constexpr int END_REC = 16;
@@ -91,6 +95,9 @@ hipError_t launch_integrator_streamed(const KParams& P, int64_t n, const SegIn& 
                                       int blocks, hipStream_t s, int* grid_out);
 hipError_t launch_finalize_range(const KParams& P, int64_t n, int64_t i0, int64_t m, const SegIn& in,
                                  const SegOut& ol, hipStream_t s);
+// The batch size up to which launch_propagate runs every ray on a wave of its own (tail_kernel):
+// ART_SMALL_TAIL, default one ray per SIMD of the device; 0 switches it off.
+int64_t small_tail_limit();
 hipError_t launch_sample(const KParams& P, double maxR, uint64_t seed, int64_t ray_offset, int64_t n, double* x,
                          double* k, double* erg, double* vifty, int32_t* w, int32_t* att, unsigned long long* queue,
                          hipStream_t s);

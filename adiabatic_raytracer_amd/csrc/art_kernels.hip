@@ -1978,6 +1978,44 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
   }
 }
 
+// Small batches (SegOut::small_tail): every fresh ray as a CONT_REC record for tail_kernel, the
+// state the persistent integrator gives a ray it takes from the queue (its refill: u0, f0, dt
+// and c0 from init_kernel, the controller's qold power at qoldinit = 1e-4, no b at the step
+// start, counters at zero, the sign memory from c0), so a ray's arithmetic is the same whether
+// a lane or a wave of its own integrates it (tests/test_edges.py compares small batches with
+// large ones bit for bit).
+__global__ __launch_bounds__(256) void pack_fresh_kernel(const int64_t n, const SegIn in, const SegOut out,
+                                                         unsigned long long* __restrict__ stats) {
+  const int64_t ray = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (ray == 0) {
+    *out.cont_count = (unsigned long long)n;
+    atomicAdd(&stats[ST_RAYS], (unsigned long long)n);
+  }
+  if (ray >= n) return;
+  const double qpow_init = pow(1e-4, 1.0 / 15.0);
+  double v[20];
+#pragma unroll
+  for (int i = 0; i < 7; ++i) {
+    v[i] = in.u0[i * n + ray];
+    v[7 + i] = in.u0[(7 + i) * n + ray];
+  }
+  const double cprev = in.u0[15 * n + ray];
+  v[14] = in.lnt0[ray];
+  v[15] = in.u0[14 * n + ray];
+  v[16] = qpow_init;
+  v[17] = cprev;
+  v[18] = NAN;
+  v[19] = in.erg[ray];
+  double2* rq = reinterpret_cast<double2*>(out.cont + ray * CONT_REC);
+#pragma unroll
+  for (int i = 0; i < 10; ++i) rq[i] = make_double2(v[2 * i], v[2 * i + 1]);
+  const int photon = in.species[ray] != ART_AXION;
+  const int sprev = isnan(cprev) ? 0 : sgn(cprev);
+  int4* ri = reinterpret_cast<int4*>(rq + 10);
+  ri[0] = make_int4((int)ray, 0, 0, 0);
+  ri[1] = make_int4(0, sprev, photon | 2 /* cprev_ok */, 1 /* save_k */);
+}
+
 // Fresh state of every segment, one thread per ray: u0 (RayTracer.jl:179-216: k_norm_Cart
 // onto the axion shell, Cartesian -> (r, θ, φ), covariant celerity), f(u0) with the
 // hamiltonian's in-place clamp (:531), the initial dt (ode_determine_initdt, order 6, with
@@ -2698,6 +2736,15 @@ static KFn pick_propagate(bool save, bool rk4, bool flat, bool sch) {
                             : propagate_kernel<ART_VERN6, GEOM_ANY, false, DON>));
 }
 
+int64_t small_tail_limit() {
+  const char* e = std::getenv("ART_SMALL_TAIL");  // read per launch (tests switch it)
+  if (e && *e) return std::atoll(e);
+  int dev = 0, ncu = 0;
+  (void)hipGetDevice(&dev);
+  (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+  return (int64_t)ncu * 4;
+}
+
 // The one-wave-per-ray tail kernel for donated rays: ART_TAIL=0 off, ART_TAIL=k at most k rays
 // (default 1: one per SIMD of the device).
 static int tail_rays() {
@@ -2747,6 +2794,33 @@ hipError_t launch_propagate(const KParams& P, int64_t n, const SegIn& in, const 
   const bool flat = P.rs_eff == 0.0 && !(P.bndry_lyr > 0.0) && !P.isotropic;
   const bool sch = P.rs_eff > 0.0 && !(P.bndry_lyr > 0.0) && !P.isotropic;
   const bool rk4 = P.integrator == ART_RK4;
+  if (out.small_tail) {  // a small Vern6 batch: every ray on a wave of its own (tail_kernel)
+    int dev = 0, ncu = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    SegOut ot = out;
+    ot.cont_count = out.cont_count;
+    ot.cont_queue = out.cont_queue;
+    hipLaunchKernelGGL(pack_fresh_kernel, dim3(g1), dim3(256), 0, s, n, in, ot, stats);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    const int waves = (int)(n < (int64_t)ncu * 4 ? n : (int64_t)ncu * 4);
+    if (grid_out) *grid_out = waves;
+    if (ev0 && (e = hipEventRecord(ev0, s)) != hipSuccess) return e;
+    using TFn = void (*)(const KParams, const int64_t, const SegIn, const SegOut, const int32_t, const int32_t,
+                         unsigned long long*);
+    const TFn tfn = flat ? tail_kernel<GEOM_FLAT> : (sch ? tail_kernel<GEOM_GR> : tail_kernel<GEOM_ANY>);
+    hipLaunchKernelGGL(tfn, dim3(waves), dim3(64), 0, s, P, n, in, ot, max_crossings, waves, stats);
+    ART_DBG("tail_kernel (small batch)")
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if (ev1 && (e = hipEventRecord(ev1, s)) != hipSuccess) return e;
+    hipStream_t sf = s;
+    if (fs && ev1 && fs != s) {
+      if ((e = hipStreamWaitEvent(fs, ev1, 0)) != hipSuccess) return e;
+      sf = fs;
+    }
+    hipLaunchKernelGGL(finalize_kernel, dim3(g1), dim3(256), 0, sf, P, n, (int64_t)0, n, in, out);
+    return hipGetLastError();
+  }
   KFn fn = out.donate > 0 ? pick_propagate<1>(out.ntimes >= 2, rk4, flat, sch)
                            : pick_propagate<0>(out.ntimes >= 2, rk4, flat, sch);
   // A batch that fits one ray per lane of 1 wave per SIMD runs the 1-wave/SIMD build, which

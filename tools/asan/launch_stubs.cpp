@@ -17,6 +17,7 @@ hipError_t launch_integrator_streamed(const KParams&, int64_t, const SegIn&, con
 hipError_t launch_finalize_range(const KParams&, int64_t, int64_t, int64_t, const SegIn&, const SegOut&, hipStream_t) {
   return hipErrorNoDevice;
 }
+int64_t small_tail_limit() { return 0; }
 hipError_t launch_sample(const KParams&, double, uint64_t, int64_t, int64_t, double*, double*, double*, double*, int32_t*,
                          int32_t*, unsigned long long*, hipStream_t) { return hipErrorNoDevice; }
 hipError_t launch_prob(const KParams&, int64_t, const double*, const double*, const double*, int64_t, const int64_t*,
