@@ -6,7 +6,7 @@ Each event is one sampled conversion point (find_samples_new). It then gets its 
 tree (axion, -B0, every crossing) and its forward photon tree. The defaults are
 num_cutoff = MC_nodes = 5 and max_nodes = 50.
 
-usage: exp_events.py [flat|gr] [gpu event counts, comma-separated] [cpu events]
+usage: [ART_DONATE=lanes] exp_events.py [flat|gr] [gpu event counts, comma-separated] [cpu events]
 Prints one JSON line per run."""
 import json
 import os
@@ -22,6 +22,10 @@ cfg = sys.argv[1] if len(sys.argv) > 1 else "flat"
 counts = [int(c) for c in (sys.argv[2] if len(sys.argv) > 2 else "1000,10000").split(",")]
 n_cpu = int(sys.argv[3]) if len(sys.argv) > 3 else 50
 p = A.Params(**CFG[cfg])
+DONATE = int(os.environ.get("ART_DONATE", "0"))  # tail donation of the forest's launches (art_set_tail_donation)
+if DONATE:
+    import ctypes as C
+    A._lib.load().art_set_tail_donation(C.c_int32(DONATE))
 
 trees.main_runner_tree(p, 65)  # warm-up: library load, kernels, pools
 for n in counts:
@@ -29,7 +33,7 @@ for n in counts:
     t0 = time.perf_counter()
     rows = trees.main_runner_tree(p, n + 1, run_info=info)
     dt = time.perf_counter() - t0
-    print(json.dumps({"config": cfg, "side": "gpu", "events": n, "wall_s": dt, "events_per_s": n / dt,
+    print(json.dumps({"config": cfg, "side": "gpu", "donate": DONATE, "events": n, "wall_s": dt, "events_per_s": n / dt,
                       "rows": int(rows.shape[0]), "f_inx": info["f_inx"]}), flush=True)
 
 if n_cpu > 0:

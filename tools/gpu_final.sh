@@ -1,7 +1,8 @@
 #!/bin/bash
 # Round-end evidence for profiles/: the GPU test suite, smoke, the PMC passes of this library
 # build (so bench.py reports roofline.traffic), the default bench line, a rocprofv3 kernel-trace
-# summary of the same command, and the GR / scan / sampler / host-path side figures.
+# summary of the same command, and the GR / scan / sampler / host-path / small-batch / event
+# side figures.
 # Usage: TAG=r03z9 bash tools/gpu_final.sh   (writes gpurun_out/TAG_*; stops at the first failure)
 TAG=${TAG:-r03final}
 set -o pipefail
@@ -21,4 +22,7 @@ timeout -k 10 300 python3 -u tools/exp_scan_streams.py 1000000 8 32 16 > gpurun_
 timeout -k 10 300 python3 -u tools/exp_sampler_time.py > gpurun_out/${TAG}_sampler_time.jsonl 2> gpurun_out/${TAG}_sampler.err || exit 1
 TAIL_DONATE=4 timeout -k 10 300 python3 -u tools/exp_gr_tail.py > gpurun_out/${TAG}_gr_tail.jsonl 2> gpurun_out/${TAG}_gr_tail.err || exit 1
 ART_HOST_TRACE=1 timeout -k 10 200 python3 -u tools/exp_host_path.py 10000000 stream single > gpurun_out/${TAG}_host_path.jsonl 2> gpurun_out/${TAG}_host_path.err || exit 1
+timeout -k 10 300 python3 -u tools/exp_small_batch.py > gpurun_out/${TAG}_small_batch.jsonl 2>> gpurun_out/${TAG}.err || exit 1
+timeout -k 10 300 python3 -u tools/exp_events.py flat 1000,10000,100000 0 > gpurun_out/${TAG}_events_flat.jsonl 2>> gpurun_out/${TAG}.err || exit 1
+timeout -k 10 300 python3 -u tools/exp_events.py gr 1000,10000 0 > gpurun_out/${TAG}_events_gr.jsonl 2>> gpurun_out/${TAG}.err || exit 1
 echo done
