@@ -15,7 +15,7 @@ bash tools/pmc_passes.sh gpurun_out/${TAG}_pmc 10000000 > gpurun_out/${TAG}_pmc.
 cp gpurun_out/${TAG}_pmc/pmc_summary.json profiles/pmc_summary.json || exit 1
 timeout -k 10 600 python3 -u bench.py > gpurun_out/${TAG}_bench_flat1e7.json 2> gpurun_out/${TAG}_bench.err || exit 1
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_prof -o prof --output-format csv -- python3 bench.py --steps 5 --no-cpu-baseline --no-pcie > gpurun_out/${TAG}_bench_prof.json 2>&1 || exit 1
-for s in 8 12; do
+for s in 12 16; do
   timeout -k 10 300 python3 -u bench.py --config gr --rays 1000000 --streams $s --steps 12 --no-cpu-baseline --no-pcie > gpurun_out/${TAG}_bench_gr1e6_s$s.json 2>> gpurun_out/${TAG}_gr.err || exit 1
 done
 timeout -k 10 300 python3 -u tools/exp_scan_streams.py 1000000 8 32 16 > gpurun_out/${TAG}_param_scan_1e6_8streams.jsonl 2> gpurun_out/${TAG}_scan.err || exit 1
