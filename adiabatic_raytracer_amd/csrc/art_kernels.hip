@@ -385,7 +385,9 @@ constexpr int SCAN_WORDS = 4;  // 2-bit codes for up to 64 grid points (interp_p
 #define ART_WAVES_PER_SIMD 2
 #endif
 #ifndef ART_STREAM_FLUSH
-#define ART_STREAM_FLUSH 31  // (DON = 2) a wave's finished-ray counts go out every 32 iterations
+// (DON = 2) a wave's finished-ray counts go out every 128 iterations (~2.5 ms of a flat ray's
+// steps; every 8: -3%, every 32: -1%, profiles/r03sg_flush.jsonl)
+#define ART_STREAM_FLUSH 127
 #endif
 
 // ---------------------------------------------------------------------------
@@ -424,17 +426,18 @@ __device__ inline bool stream_ready(const SegOut& out, int64_t need, int leader)
   return __shfl(ok, leader) != 0;
 }
 
-// the ready counter as one lane reads it now (wave-uniform)
-__device__ inline int64_t stream_poll(const SegOut& out, int leader) {
+// the ready counter as one lane reads it now, returned in a scalar register (ray indices are
+// 32-bit in the integrator; the streamed kernel is short of vector registers)
+__device__ inline int stream_poll(const SegOut& out, int leader) {
   unsigned long long r = 0;
   if ((int)(threadIdx.x & 63) == leader) r = __hip_atomic_load(out.ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
-  return (int64_t)__shfl(r, leader);
+  return __builtin_amdgcn_readlane((int)r, leader);
 }
 
 // A wave's finished rays of piece p, counted c at a time: the wave's record stores are released
 // first (agent scope: the end and crossing records reach memory every XCD reads), then the
 // count; the count that completes the piece raises the piece's signal. Waves batch their
-// counts (at most every 32 iterations, at a piece change and at exit), so the L2 write-backs of
+// counts (at most every 128 iterations, at a piece change and at exit), so the L2 write-backs of
 // the release stay rare.
 __device__ inline void stream_count(const SegOut& out, int64_t n, int p, unsigned long long c) {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
@@ -517,7 +520,7 @@ __global__ __launch_bounds__(BLOCK, WPS) void propagate_kernel(const KParams P_i
   double hroot = 0.0, r_tha = 0.0, r_ca = 0.0, r_thb = 0.0, r_cb = 0.0, r_t = 0.0, r_slope = 1.0, post_c = 0.0;
   int post_s = 0, r_side = 0, r_it = 0;
   int wnext = 0, wend = 0;
-  int64_t rdy = 0;                       // (DON = 2) the ready counter as last read
+  int rdy = 0;                           // (DON = 2) the ready counter as last read
   int pend_p = -1, tick = 0;             // (DON = 2) the piece whose finished rays are being counted
   unsigned long long pend_c = 0;         //           and their count (per wave; in LDS: 1.5% slower)
   int save_k = 1;  // SAVE: the next interior saveat index
@@ -595,7 +598,7 @@ __global__ __launch_bounds__(BLOCK, WPS) void propagate_kernel(const KParams P_i
             if (!stream_ready(out, wnext + 1, leader)) { exhausted = true; break; }
             rdy = stream_poll(out, leader);
           }
-          lim = rdy < wend ? (int)rdy : wend;
+          lim = rdy < wend ? rdy : wend;
         }
         const int rank = __popcll(need & ((1ull << lane) - 1ull));
         const int cnt = __popcll(need);
@@ -1320,7 +1323,7 @@ __global__ __launch_bounds__(BLOCK, WPS) void propagate_kernel(const KParams P_i
       // stream_count)
       unsigned long long fm = __ballot(fin_piece >= 0);
       while (fm != 0ull) {
-        const int pc = __shfl(fin_piece, __ffsll((long long)fm) - 1);
+        const int pc = __builtin_amdgcn_readlane(fin_piece, __ffsll((long long)fm) - 1);
         const unsigned long long same = __ballot(fin_piece == pc);
         if (pc != pend_p) {
           if (pend_c != 0ull) stream_count(out, n, pend_p, pend_c);
@@ -2701,6 +2704,9 @@ int persistent_blocks(const void* func, int64_t work, int block, int fallback_pe
   int dev = 0, ncu = 0, per_cu = 0;
   (void)hipGetDevice(&dev);
   (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+#ifdef ART_DEV_GRID_CUS
+  ncu = ART_DEV_GRID_CUS;  // (dev builds: a grid sized for a CU-masked stream)
+#endif
   const hipError_t oe = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, func, block, 0);
 #ifdef ART_LAUNCH_DEBUG
   fprintf(stderr, "[art-debug] occupancy rc=%d (%s) per_cu=%d ncu=%d\n", (int)oe, hipGetErrorString(oe), per_cu, ncu);
