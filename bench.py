@@ -153,7 +153,7 @@ def main():
         # flight; round 3 (tail kernel, two-level donation): 1.25e6 rays 3.16e9 on 3 streams,
         # 3.31e9 on 4, 3.30e9 on 6, so 4. The GR batch is bound by its longest ray (~185 ms
         # alone on the tail kernel), so only more passes in flight amortise it: 4.2e8 on 3,
-        # 6.3e8 on 6, 5.9-6.2e8 on 8, 7.4-8.7e8 on 12, 8.6-9.8e8 on 16 across fresh boxes
+        # 6.3e8 on 6, 5.9-6.2e8 on 8, 7.4-8.7e8 on 12, 7.8-9.8e8 on 16 across fresh boxes
         # (profiles/r03grv_gr_streams_variance.txt), so 16 for the GR configs. Overlapped launches stretch each other's measured duration, so
         # the single-GPU headline (1e7 rays) runs one pass at a time and its roofline is the
         # kernel's own (2 passes with donation: +1%).
