@@ -136,7 +136,7 @@ def main():
     ap.add_argument("--nbins", type=int, default=50)
     ap.add_argument("--streams", type=int, default=0,
                     help="batches in flight (HIP streams); 0: 1 for per-GPU batches of >= 8e6 rays, else 4 "
-                         "(12 for the GR config)")
+                         "(16 for the GR configs)")
     ap.add_argument("--cpu-rays", type=int, default=int(os.environ.get("ART_CPU_RAYS", "500000")))
     ap.add_argument("--cpu-rays-1t", type=int, default=int(os.environ.get("ART_CPU_RAYS_1T", "24000")))
     ap.add_argument("--donate", type=int, default=-1,
