@@ -51,6 +51,7 @@ SIGNATURES = {
     "art_device_count": (C.c_int, [C.POINTER(C.c_int32)]),
     "art_set_device": (C.c_int, [_i32]),
     "art_synchronize": (C.c_int, []),
+    "art_shutdown": (C.c_int, []),
     "art_last_kernel_ms": (C.c_double, []),
     "art_last_stats": (C.c_int, [C.POINTER(C.c_uint64), C.POINTER(C.c_int32)]),
     "art_vern6_tableau": (C.c_int, [_v, _v, _v, _v]),
@@ -59,6 +60,9 @@ SIGNATURES = {
                                      C.POINTER(CrossingBuf)]),
     "art_propagate_device": (C.c_int, [_P, _i64, _v, _v, _v, _v, _v, _v, _i32, C.POINTER(SegmentOut),
                                        C.POINTER(CrossingBuf), _v]),
+    "art_propagate_host_flux": (C.c_int, [_P, _i64, _v, _v, _v, _v, _v, _v, _i32, C.POINTER(SegmentOut),
+                                          C.POINTER(CrossingBuf), _i32, _v]),
+    "art_host_path_counters": (C.c_int, [_v, _i32, _i32]),
     "art_propagate_traj_host": (C.c_int, [_P, _i64, _v, _v, _v, _v, _v, _v, _i32, C.POINTER(SegmentOut),
                                           C.POINTER(CrossingBuf), _i32, _v, _v, _v]),
     "art_propagate_traj_device": (C.c_int, [_P, _i64, _v, _v, _v, _v, _v, _v, _i32, C.POINTER(SegmentOut),
@@ -76,6 +80,7 @@ SIGNATURES = {
     "art_recent_kernel_ms": (C.c_int, [_i32, _v]),
     "art_set_tail_donation": (C.c_int, [_i32]),
     "art_flux_histogram_phi_device": (C.c_int, [_i64, _v, _v, _v, _i32, _v, _v]),
+    "art_flux_histogram_phi_range_device": (C.c_int, [_i64, _v, _v, _v, _i32, _d, _d, _v, _v]),
     "art_comm_unique_id": (C.c_int, [_v]),
     "art_comm_init": (C.c_int, [_i32, _i32, _v]),
     "art_flux_allreduce": (C.c_int, [_v, _i64, _v]),

@@ -32,6 +32,11 @@ thread_local std::string g_err;
 double g_last_ms = 0.0;
 unsigned long long g_last_stats[art::N_STATS] = {0};
 int g_last_grid = 0;
+// What the art_propagate_host* calls ran as (art_host_path_counters): calls, streamed
+// pipeline completions, streamed give-ups (each batch then ran again as one launch), chunked
+// pipeline calls, single-launch calls
+enum { HC_CALLS, HC_STREAMED, HC_GIVEUPS, HC_CHUNKED, HC_SINGLE, HC_N };
+uint64_t g_host_cnt[HC_N] = {0};
 
 // One propagate launch's bookkeeping: the HIP events around the integrator kernel, an event
 // after its statistics were copied to pinned host memory, and that memory. A ring of them per
@@ -94,7 +99,21 @@ int fail(int code, const char* fmt, const char* a = "", const char* b = "") {
     if (e_ != hipSuccess) return fail(ART_E_HIP, "%s: %s", #expr, hipGetErrorString(e_)); \
   } while (0)
 
+void shutdown_at_exit();
+
 int current_ctx(DeviceCtx** out) {
+  // Release every HIP object of the library at exit, before the HIP runtime tears itself down:
+  // handlers registered with atexit run in reverse order, and the runtime (loaded and
+  // initialised before libart's first call) registered its teardown earlier. Left to static
+  // destruction, the library's streams, signal memory and pinned buffers outlived the runtime
+  // (and a profiler's finalisation), DESIGN.md §4 "exit".
+  static bool at_exit = false;
+  if (!at_exit) {
+#ifndef ART_NO_EXIT_RELEASE  // (dev A/B: the round-3 behaviour, static destruction only)
+    std::atexit(shutdown_at_exit);
+#endif
+    at_exit = true;
+  }
   int dev = 0;
   HIP_OK(hipGetDevice(&dev));
   if ((int)g_ctx.size() <= dev) g_ctx.resize(dev + 1);
@@ -237,10 +256,55 @@ int env_int(const char* name, int dflt) {
   return (e && *e) ? std::atoi(e) : dflt;
 }
 
+// (a heap object, not a function-local static: art_shutdown joins its threads before the HIP
+// runtime's own teardown, and no static destructor of libart is left to run after it)
+CopyPool* g_copy_pool = nullptr;
 CopyPool& copy_pool() {
   // ART_HOST_THREADS: worker threads besides the caller (default 7)
-  static CopyPool pool(std::max(0, env_int("ART_HOST_THREADS", 7)));
-  return pool;
+  if (!g_copy_pool) g_copy_pool = new CopyPool(std::max(0, env_int("ART_HOST_THREADS", 7)));
+  return *g_copy_pool;
+}
+
+// Every HIP object a device context holds, released in dependency order (the streams drained
+// first). Used by art_shutdown, which runs at exit ahead of the HIP runtime's teardown.
+void release_ctx(DeviceCtx& c) {
+  if (c.device < 0) return;
+  (void)hipSetDevice(c.device);
+  (void)hipDeviceSynchronize();
+  for (LaunchRec& L : c.ring) {
+    if (L.ev0) (void)hipEventDestroy(L.ev0);
+    if (L.ev1) (void)hipEventDestroy(L.ev1);
+    if (L.done) (void)hipEventDestroy(L.done);
+  }
+  if (c.ring[0].host_stats) (void)hipHostFree(c.ring[0].host_stats);  // one block for the ring
+  for (auto& e : c.pool)
+    if (e.first) (void)hipFree(e.first);
+  for (auto& e : c.pinned)
+    if (e.p) (void)hipHostFree(e.p);
+  for (hipEvent_t e : c.pev) (void)hipEventDestroy(e);
+  for (hipStream_t s : c.pstreams)
+    if (s && s != c.stream) (void)hipStreamDestroy(s);
+  for (hipStream_t s : {c.h2d, c.fin, c.s_comp, c.s_in, c.s_out})
+    if (s) (void)hipStreamDestroy(s);
+  for (unsigned long long* w : c.sigs) (void)hipFree(w);
+  if (c.sig_dev) (void)hipFree(c.sig_dev);
+  if (c.abort_host) (void)hipHostFree(c.abort_host);
+  if (c.stream) (void)hipStreamDestroy(c.stream);
+  c = DeviceCtx();
+}
+
+void shutdown_locked() {
+  for (DeviceCtx& c : g_ctx) release_ctx(c);
+  delete g_copy_pool;
+  g_copy_pool = nullptr;
+}
+
+void shutdown_at_exit() {
+  // (a call still running on another thread at exit keeps its objects: releasing them under it
+  // would be worse than leaving them to the runtime)
+  if (!g_mu.try_lock()) return;
+  shutdown_locked();
+  g_mu.unlock();
 }
 
 // Device scratch of ONE launch, allocated and freed in the order of its stream (hipMallocAsync /
@@ -285,6 +349,13 @@ struct TrajArgs {
   int32_t* count = nullptr;
 };
 
+// art_propagate_host_flux: the batch's binned radiated flux (flux_kernel over the outputs while
+// they are still in HBM), 2 * nbins doubles into the caller's `hist`; nbins = 0: none
+struct FluxArgs {
+  int32_t nbins = 0;
+  double* hist = nullptr;
+};
+
 // Argument checks shared by the host and device entry points, before any device call (the
 // host path stages buffers of n elements, so a bad n or a NULL buffer must stop it first).
 // Returns ART_OK with *empty set for n == 0 (nothing to do, nothing written).
@@ -314,11 +385,20 @@ int check_segment_args(const art_params* p, int64_t n, const double* x0, const d
 struct LaunchOpts {
   int donate = -1;
   void* scratch = nullptr;
+  size_t scratch_bytes = 0;  // the size of `scratch` (checked against the launch's layout)
   bool nan_fill = false;
   hipStream_t finalize_stream = nullptr;  // finalize_kernel on this stream (after the integrator)
 };
 
 int launch_donate(DeviceCtx* c, const LaunchOpts& o) { return o.donate >= 0 ? o.donate : c->donate; }
+
+// A small Vern6 batch without saveat runs every ray on a wave of its own (tail_kernel): the
+// latency of a Julia host's per-event calls (its rays run ~40% faster per attempt than a lone
+// lane of the persistent integrator), bit-identical results. One decision for the launch and
+// for every caller that lays out a launch's scratch ahead of it (the chunked host pipeline).
+bool use_small_tail(const art_params* p, int64_t n, const TrajArgs& tr) {
+  return tr.ntimes == 0 && p->integrator == ART_VERN6 && n <= art::small_tail_limit();
+}
 
 // this launch's scratch: [queue head + statistics (256 B) | u0: 16n doubles of fresh state
 // (init_kernel -> the integrator) | END_REC n doubles of end records | X_REC cap n doubles of
@@ -360,13 +440,13 @@ int propagate_device_impl(const art_params* p, int64_t n, const double* x0, cons
   hipStream_t s = pick(c, stream);
   const art::KParams K = kparams(*p);
   const int cap = (xc && xc->count) ? xc->capacity : 0;
-  // a small Vern6 batch without saveat runs every ray on a wave of its own (tail_kernel): the
-  // latency of a Julia host's per-event calls (its rays run ~40% faster per attempt than a lone
-  // lane of the persistent integrator), bit-identical results
-  const bool small_tail = tr.ntimes == 0 && p->integrator == ART_VERN6 && n <= art::small_tail_limit();
+  const bool small_tail = use_small_tail(p, n, tr);
   const int32_t donate = small_tail ? 0 : launch_donate(c, opt);
   ScratchLayout SL;
   if ((rc = scratch_layout(c, n, cap, donate, &SL, small_tail))) return rc;
+  if (opt.scratch && SL.total() > opt.scratch_bytes)
+    return fail(ART_E_INVALID, "caller scratch of %s bytes is smaller than the launch needs (%s)",
+                std::to_string(opt.scratch_bytes).c_str(), std::to_string(SL.total()).c_str());
   const size_t head = SL.head, u0b = SL.u0b, recb = SL.recb, xrb = SL.xrb, ncont = SL.ncont;
   LaunchRec* L;
   if ((rc = take_slot(c, &L))) return rc;
@@ -617,9 +697,10 @@ unsigned out_coherence() {
 int propagate_host_chunked(DeviceCtx* c, const art_params* p, int64_t n, const double* x0, const double* k0,
                            const double* erg, const double* dw, const double* ln_t0, const int8_t* species,
                            int32_t max_crossings, art_segment_out* out, art_crossing_buf* xc, int nchunks,
-                           int nslots) {
+                           int nslots, const FluxArgs& fx) {
   const int cap = (xc && xc->count) ? xc->capacity : 0;
   const int64_t K = std::max(2, nchunks);
+  const art::KParams KP = kparams(*p);
   auto up = [](size_t b) { return (b + 255) & ~size_t(255); };
   // blob layouts of a chunk of m rays (inputs: pinned staging and HBM; outputs: pinned)
   auto in_bytes = [&](int64_t m) { return up((size_t)m * 9 * sizeof(double)) + up((size_t)m); };
@@ -638,8 +719,11 @@ int propagate_host_chunked(DeviceCtx* c, const art_params* p, int64_t n, const d
   std::vector<size_t> ioff(K + 1, 0), ooff(K + 1, 0), soff(K + 1, 0);
   for (int64_t k = 0; k < K; ++k) {
     const int64_t m = lo[k + 1] - lo[k];
+    // the same layout propagate_device_impl will carve out of this chunk's slice (a chunk small
+    // enough for the tail kernel keeps one donation record per ray, whatever `donate` says)
+    const bool st = use_small_tail(p, m, TrajArgs());
     ScratchLayout SL;
-    int rc0 = scratch_layout(c, m, cap, donate, &SL);
+    int rc0 = scratch_layout(c, m, cap, st ? 0 : donate, &SL, st);
     if (rc0) return rc0;
     ioff[k + 1] = ioff[k] + in_bytes(m);
     ooff[k + 1] = ooff[k] + out_bytes(m);
@@ -667,6 +751,11 @@ int propagate_host_chunked(DeviceCtx* c, const art_params* p, int64_t n, const d
   void* po_dev = nullptr;
   HIP_OK(hipHostGetDevicePointer(&po_dev, po, 0));
   char *pin_in = (char*)pi, *pin_out = (char*)po, *out_dev = (char*)po_dev, *dev_in = (char*)di_, *scratch = (char*)sc_;
+  double* hist_dev = nullptr;
+  if (fx.nbins) {
+    if ((rc = pool_get(c, 23, 2 * (size_t)fx.nbins * sizeof(double), (void**)&hist_dev))) return rc;
+    HIP_OK(hipMemsetAsync(hist_dev, 0, 2 * (size_t)fx.nbins * sizeof(double), c->fin));
+  }
   using Seg = CopyPool::Seg;
   std::vector<int> rings;
   // ART_HOST_TRACE=1: the host side of every chunk to stderr (gathers, submits, waits, scatters)
@@ -719,12 +808,15 @@ int propagate_host_chunked(DeviceCtx* c, const art_params* p, int64_t n, const d
     LaunchOpts lo_;
     lo_.donate = donate;
     lo_.scratch = scratch + soff[k];
+    lo_.scratch_bytes = soff[k + 1] - soff[k];
     lo_.nan_fill = true;
     lo_.finalize_stream = c->fin;
-    int rc2 = propagate_device_impl(p, m, di, di + 3 * m, di + 6 * m, di + 7 * m, di + 8 * m,
-                                    (const int8_t*)((const char*)di + up((size_t)m * 9 * sizeof(double))), max_crossings,
+    const int8_t* dsp = (const int8_t*)((const char*)di + up((size_t)m * 9 * sizeof(double)));
+    int rc2 = propagate_device_impl(p, m, di, di + 3 * m, di + 6 * m, di + 7 * m, di + 8 * m, dsp, max_crossings,
                                     &dso, dxbp, st, TrajArgs(), lo_);
     if (rc2) return rc2;
+    if (fx.nbins)  // the chunk's flux from its outputs (mapped pinned memory), behind its finalize
+      HIP_OK(art::launch_flux(KP, m, dso.x_end, dso.k_end, dso.status, dsp, nullptr, fx.nbins, hist_dev, c->fin));
     rings.push_back(c->last);
     HIP_OK(hipEventRecord(ev_done[k], c->fin));
     if (trace) std::fprintf(stderr, "[art-host] t=%.2f compute k=%lld submit %.2f ms\n", t0 - t_start, (long long)k, clk() - t0);
@@ -774,6 +866,10 @@ int propagate_host_chunked(DeviceCtx* c, const art_params* p, int64_t n, const d
                    (long long)l0, tw1 - tw0, clk() - tw1);
   }
   if (trace) std::fprintf(stderr, "[art-host] total %.2f ms\n", clk() - t_start);
+  if (fx.nbins) {
+    HIP_OK(hipMemcpyAsync(fx.hist, hist_dev, 2 * (size_t)fx.nbins * sizeof(double), hipMemcpyDeviceToHost, c->fin));
+    HIP_OK(hipStreamSynchronize(c->fin));
+  }
   return finish_timing_sum(c, rings);
 }
 
@@ -857,7 +953,7 @@ int stream_setup(DeviceCtx* c, int reserve, int nsig) {
 // the call fall back (STREAM_FALLBACK) instead of hanging.
 int propagate_host_streamed(DeviceCtx* c, const art_params* p, int64_t n, const double* x0, const double* k0,
                             const double* erg, const double* dw, const double* ln_t0, const int8_t* species,
-                            int32_t max_crossings, art_segment_out* out, art_crossing_buf* xc) {
+                            int32_t max_crossings, art_segment_out* out, art_crossing_buf* xc, const FluxArgs& fx) {
   const int cap = (xc && xc->count) ? xc->capacity : 0;
   const art::KParams K = kparams(*p);
   int shift = 16;
@@ -910,6 +1006,11 @@ int propagate_host_streamed(DeviceCtx* c, const art_params* p, int64_t n, const 
   const double t_start = clk();
   // counters and signals to zero, ahead of everything that reads them
   HIP_OK(hipMemsetAsync(words, 0, head, c->s_in));
+  double* hist_dev = nullptr;
+  if (fx.nbins) {
+    if ((rc = pool_get(c, 23, 2 * (size_t)fx.nbins * sizeof(double), (void**)&hist_dev))) return rc;
+    HIP_OK(hipMemsetAsync(hist_dev, 0, 2 * (size_t)fx.nbins * sizeof(double), c->s_in));
+  }
   for (int k = 0; k <= np; ++k) HIP_OK(hipStreamWriteValue64(c->s_in, c->sigs[k], 0ull, 0));
   HIP_OK(hipEventRecord(ev_reset, c->s_in));
   HIP_OK(hipStreamWaitEvent(c->s_out, ev_reset, 0));
@@ -1001,6 +1102,8 @@ int propagate_host_streamed(DeviceCtx* c, const art_params* p, int64_t n, const 
     HIP_OK(hipStreamWaitValue64(c->s_out, c->sigs[k], 1ull, hipStreamWaitValueGte));
     HIP_OK(art::launch_finalize_range(K, n, lo, m, in, ol, c->s_out));
     HIP_OK(hipMemcpyAsync((char*)po + ooff[k], db, out_bytes(m), hipMemcpyDeviceToHost, c->s_out));
+    if (fx.nbins)  // the piece's flux from its SoA blob while it is still in HBM
+      HIP_OK(art::launch_flux(K, m, ol.x_end, ol.k_end, ol.status, in.species + lo, nullptr, fx.nbins, hist_dev, c->s_out));
     HIP_OK(hipEventRecord(ev_out[k], c->s_out));
   }
   // drain: wait for each piece (bounded), scatter it into the caller's arrays
@@ -1065,17 +1168,26 @@ int propagate_host_streamed(DeviceCtx* c, const art_params* p, int64_t n, const 
                    tw1 - tw0, clk() - tw1);
   }
   if (trace) std::fprintf(stderr, "[art-host] streamed total %.2f ms (%d pieces of 2^%d)\n", clk() - t_start, np, shift);
+  if (fx.nbins) {
+    HIP_OK(hipMemcpyAsync(fx.hist, hist_dev, 2 * (size_t)fx.nbins * sizeof(double), hipMemcpyDeviceToHost, c->s_out));
+    HIP_OK(hipStreamSynchronize(c->s_out));
+  }
   return finish_timing(c);
 }
 
 int propagate_host_impl(const art_params* p, int64_t n, const double* x0, const double* k0, const double* erg,
                         const double* dw, const double* ln_t0, const int8_t* species, int32_t max_crossings,
-                        art_segment_out* out, art_crossing_buf* xc, const TrajArgs& htr) {
+                        art_segment_out* out, art_crossing_buf* xc, const TrajArgs& htr,
+                        const FluxArgs& fx = FluxArgs()) {
   bool empty = false;
   int rc = check_segment_args(p, n, x0, k0, erg, dw, ln_t0, species, out, xc, htr, &empty);
-  if (rc || empty) return rc;
+  if (rc) return rc;
+  if (fx.nbins && (fx.nbins < 1 || fx.nbins > 4096 || !fx.hist)) return fail(ART_E_INVALID, "flux needs nbins in [1, 4096] and hist");
+  if (fx.nbins) std::fill(fx.hist, fx.hist + 2 * (size_t)fx.nbins, 0.0);
+  if (empty) return rc;
   DeviceCtx* c;
   if ((rc = current_ctx(&c))) return rc;
+  g_host_cnt[HC_CALLS] += 1;
   // large batches (ART_HOST_CHUNK_MIN rays and more, default 2^21; no saveat): the streamed
   // pipeline (ART_HOST_MODE=stream, the default, Vern6) or the chunked one (=chunked); smaller
   // batches, RK4, saveat, ART_HOST_MODE=single and a streamed call that gave up take the single
@@ -1084,13 +1196,20 @@ int propagate_host_impl(const art_params* p, int64_t n, const double* x0, const 
   const std::string mode = (mode_env && *mode_env) ? mode_env : "stream";
   if (htr.ntimes == 0 && n >= env_int("ART_HOST_CHUNK_MIN", 1 << 21)) {
     if (mode == "stream" && p->integrator == ART_VERN6) {
-      rc = propagate_host_streamed(c, p, n, x0, k0, erg, dw, ln_t0, species, max_crossings, out, xc);
-      if (rc != STREAM_FALLBACK) return rc;
+      rc = propagate_host_streamed(c, p, n, x0, k0, erg, dw, ln_t0, species, max_crossings, out, xc, fx);
+      if (rc != STREAM_FALLBACK) {
+        if (rc == ART_OK) g_host_cnt[HC_STREAMED] += 1;
+        return rc;
+      }
+      g_host_cnt[HC_GIVEUPS] += 1;
     } else if (mode == "chunked") {
+      g_host_cnt[HC_CHUNKED] += 1;
       return propagate_host_chunked(c, p, n, x0, k0, erg, dw, ln_t0, species, max_crossings, out, xc,
-                                    std::max(2, env_int("ART_HOST_CHUNKS", 4)), std::max(1, env_int("ART_HOST_SLOTS", 2)));
+                                    std::max(2, env_int("ART_HOST_CHUNKS", 4)), std::max(1, env_int("ART_HOST_SLOTS", 2)),
+                                    fx);
     }
   }
+  g_host_cnt[HC_SINGLE] += 1;
   const int cap = (xc && xc->count) ? xc->capacity : 0;
   const size_t nd = (size_t)n;
   // staging layout: inputs 3n+3n+n+n+n doubles + n int8; outputs 3n+3n+n+n doubles + 3n int32 (+ crossings)
@@ -1142,6 +1261,14 @@ int propagate_host_impl(const art_params* p, int64_t n, const double* x0, const 
   rc = propagate_device_impl(p, n, di, di + 3 * nd, di + 6 * nd, di + 7 * nd, di + 8 * nd, (const int8_t*)(di + 9 * nd),
                              max_crossings, &dso, dxbp, s, dtr, opt);
   if (rc) return rc;
+  if (fx.nbins) {  // the batch's flux from its outputs in HBM
+    double* hist_dev = nullptr;
+    if ((rc = pool_get(c, 23, 2 * (size_t)fx.nbins * sizeof(double), (void**)&hist_dev))) return rc;
+    HIP_OK(hipMemsetAsync(hist_dev, 0, 2 * (size_t)fx.nbins * sizeof(double), s));
+    HIP_OK(art::launch_flux(kparams(*p), n, dso.x_end, dso.k_end, dso.status, (const int8_t*)(di + 9 * nd), nullptr,
+                            fx.nbins, hist_dev, s));
+    HIP_OK(hipMemcpyAsync(fx.hist, hist_dev, 2 * (size_t)fx.nbins * sizeof(double), hipMemcpyDeviceToHost, s));
+  }
   if (htr.ntimes != 0) {
     const size_t nt = (size_t)htr.ntimes * nd;
     HIP_OK(hipMemcpyAsync(htr.traj, dtr.traj, nt * 3 * sizeof(double), hipMemcpyDeviceToHost, s));
@@ -1175,6 +1302,27 @@ int art_propagate_host(const art_params* p, int64_t n, const double* x0, const d
                        art_segment_out* out, art_crossing_buf* xc) {
   std::lock_guard<std::mutex> lk(g_mu);
   return propagate_host_impl(p, n, x0, k0, erg, dw, ln_t0, species, max_crossings, out, xc, TrajArgs());
+}
+
+int art_propagate_host_flux(const art_params* p, int64_t n, const double* x0, const double* k0, const double* erg,
+                            const double* dw, const double* ln_t0, const int8_t* species, int32_t max_crossings,
+                            art_segment_out* out, art_crossing_buf* xc, int32_t nbins, double* hist) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (nbins < 1) return fail(ART_E_INVALID, "nbins must be >= 1");
+  FluxArgs fx;
+  fx.nbins = nbins;
+  fx.hist = hist;
+  return propagate_host_impl(p, n, x0, k0, erg, dw, ln_t0, species, max_crossings, out, xc, TrajArgs(), fx);
+}
+
+int art_host_path_counters(uint64_t* counters, int32_t n, int32_t reset) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (n < 0 || (n > 0 && !counters)) return fail(ART_E_INVALID, "bad buffer");
+  for (int i = 0; i < n && i < HC_N; ++i) counters[i] = g_host_cnt[i];
+  for (int i = HC_N; i < n; ++i) counters[i] = 0;
+  if (reset)
+    for (uint64_t& v : g_host_cnt) v = 0;
+  return HC_N;
 }
 
 int art_propagate_traj_host(const art_params* p, int64_t n, const double* x0, const double* k0, const double* erg,
@@ -1373,7 +1521,22 @@ int art_flux_histogram_phi_device(int64_t n, const double* phi, const int8_t* sp
   DeviceCtx* c;
   int rc = current_ctx(&c);
   if (rc) return rc;
-  HIP_OK(art::launch_flux_phi(n, phi, species, w, nbins, hist, (hipStream_t)stream));
+  HIP_OK(art::launch_flux_phi(n, phi, species, w, nbins, -art::PI, art::PI, hist, (hipStream_t)stream));
+  return ART_OK;
+}
+
+int art_flux_histogram_phi_range_device(int64_t n, const double* phi, const int8_t* species, const double* w,
+                                        int32_t nbins, double lo, double hi, double* hist, void* stream) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (nbins < 1 || nbins > 4096) return fail(ART_E_INVALID, "nbins must be in [1, 4096]");
+  if (n < 0) return fail(ART_E_INVALID, "n must be >= 0");
+  if (!(lo < hi) || !std::isfinite(lo) || !std::isfinite(hi)) return fail(ART_E_INVALID, "need finite lo < hi");
+  if (n == 0) return ART_OK;
+  if (!phi || !hist) return fail(ART_E_INVALID, "NULL buffer");
+  DeviceCtx* c;
+  int rc = current_ctx(&c);
+  if (rc) return rc;
+  HIP_OK(art::launch_flux_phi(n, phi, species, w, nbins, lo, hi, hist, (hipStream_t)stream));
   return ART_OK;
 }
 
@@ -1512,6 +1675,12 @@ int art_flux_allreduce_host(double* buf, int64_t count) {
   if (r) return rccl_fail(r, "ncclAllReduce");
   HIP_OK(hipMemcpyAsync(buf, d, (size_t)count * sizeof(double), hipMemcpyDeviceToHost, c->stream));
   HIP_OK(hipStreamSynchronize(c->stream));
+  return ART_OK;
+}
+
+int art_shutdown(void) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  shutdown_locked();
   return ART_OK;
 }
 

@@ -106,7 +106,7 @@ hipError_t launch_prob(const KParams& P, int64_t nc, const double* pos, const do
 hipError_t launch_flux(const KParams& P, int64_t n, const double* x_end, const double* k_end, const int32_t* status,
                        const int8_t* species, const double* w, int32_t nbins, double* hist, hipStream_t s);
 hipError_t launch_flux_phi(int64_t n, const double* phi, const int8_t* species, const double* w, int32_t nbins,
-                           double* hist, hipStream_t s);
+                           double lo, double hi, double* hist, hipStream_t s);
 hipError_t launch_eval_rhs(const KParams& P, int64_t n, const double* u, const double* tau, const double* erg,
                            const int8_t* species, double* du, hipStream_t s);
 hipError_t launch_eval_hamiltonian(const KParams& P, int64_t n, const double* x, const double* k, const double* T,

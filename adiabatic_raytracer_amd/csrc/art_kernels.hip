@@ -669,7 +669,8 @@ __global__ __launch_bounds__(BLOCK, WPS) void propagate_kernel(const KParams P_i
     // SIMD's arbiter for issue priority. The one ray that sets a launch's (or a scan point's)
     // drain time then runs at close to its lone-wave speed while the bulk of the batch still
     // shares its SIMD; the other waves fill the issue slots it leaves.
-    if (__ballot(iter >= ART_PRIO_ITERS) != 0ull) __builtin_amdgcn_s_setprio(2);
+    const bool outlier = __ballot(iter >= ART_PRIO_ITERS) != 0ull;
+    if (outlier) __builtin_amdgcn_s_setprio(2);
     else __builtin_amdgcn_s_setprio(0);
     ART_PC(0)
     ART_TMARK(0)  // refill
@@ -748,6 +749,12 @@ __global__ __launch_bounds__(BLOCK, WPS) void propagate_kernel(const KParams P_i
       ART_SMARK(10)
     }
     ART_TMARK(1)  // step size and stage slots
+#ifdef ART_PRIO_PHASE
+    // (dev A/B) the latency-bound rest of the iteration at a higher issue priority than the
+    // partner wave's stage slots, so its short dependent chains issue as soon as they can
+    if (outlier) __builtin_amdgcn_s_setprio(3);
+    else __builtin_amdgcn_s_setprio(1);
+#endif
     // y = u_{n+1}, kk = f(u_{n+1}) for stepping lanes
     // EEst² = mean of the 7 squared scaled errors: the controller needs EEst only through
     // EEst <= 1 and its logarithm (ln EEst = ½ ln EEst²), so no square root is taken
@@ -2561,9 +2568,10 @@ __global__ __launch_bounds__(256) void prob_kernel(const KParams P, const int64_
 // index from (x - lo) / (hi - lo) * nbins, then corrected against the edges of
 // linspace(lo, hi, nbins + 1) = i * ((hi - lo) / nbins) + lo, the right edge in the last bin),
 // with the same roundings: no contraction into FMAs. -1 outside [lo, hi] (and for NaN).
-__device__ inline int np_hist_bin(double x, int nbins) {
+// The range defaults to flux_kernel's fixed [-π, π]; flux_phi_kernel also takes a data-dependent
+// one (np.histogram(a, bins) without `range` bins over [a.min(), a.max()], plot/flux.py:43-47).
+__device__ inline int np_hist_bin(double x, int nbins, double lo = -PI, double hi = PI) {
 #pragma clang fp contract(off)  // numpy rounds every product and sum (HIP's __dmul_rn would still fuse)
-  const double lo = -PI, hi = PI;
   if (!(x >= lo && x <= hi)) return -1;
   const double span = hi - lo;
   int i = (int)(((x - lo) / span) * (double)nbins);
@@ -2603,12 +2611,13 @@ __global__ __launch_bounds__(256) void flux_kernel(const KParams P, const int64_
 __global__ __launch_bounds__(256) void flux_phi_kernel(const int64_t n, const double* __restrict__ phi,
                                                        const int8_t* __restrict__ species,
                                                        const double* __restrict__ w, const int32_t nbins,
+                                                       const double lo, const double hi,
                                                        double* __restrict__ hist) {
   extern __shared__ __attribute__((aligned(16))) double sh[];
   for (int i = threadIdx.x; i < 2 * nbins; i += blockDim.x) sh[i] = 0.0;
   __syncthreads();
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const int bin = np_hist_bin(phi[i], nbins);
+    const int bin = np_hist_bin(phi[i], nbins, lo, hi);
     if (bin < 0) continue;
     const int row = (species && species[i] == ART_AXION) ? 0 : 1;
     atomicAdd(&sh[row * nbins + bin], w ? w[i] : 1.0);
@@ -2972,12 +2981,12 @@ hipError_t launch_flux(const KParams& P, int64_t n, const double* x_end, const d
 }
 
 hipError_t launch_flux_phi(int64_t n, const double* phi, const int8_t* species, const double* w, int32_t nbins,
-                           double* hist, hipStream_t s) {
+                           double lo, double hi, double* hist, hipStream_t s) {
   int64_t grid = (n + 255) / 256;
   if (grid > 1024) grid = 1024;
   if (grid < 1) grid = 1;
   hipLaunchKernelGGL(flux_phi_kernel, dim3((unsigned)grid), dim3(256), 2 * nbins * sizeof(double), s, n, phi, species, w,
-                     nbins, hist);
+                     nbins, lo, hi, hist);
   return hipGetLastError();
 }
 

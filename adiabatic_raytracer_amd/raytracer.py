@@ -177,10 +177,12 @@ def propagate(x0, k0, nsteps, Mvars, NumerP, rhs=func_photon, make_tree=False, i
 
 
 def propagate_batch(params: Params, x0, k0, erg, dw, ln_t0, species, max_crossings=-1, capacity=1,
-                    ntimes=None) -> dict:
+                    ntimes=None, flux_nbins=None) -> dict:
     """Low-level host entry (art_propagate_host): SoA numpy inputs, dict of numpy outputs.
     With ntimes >= 2 (art_propagate_traj_host) also the saved points of RayTracer.jl:176,383:
-    traj (3, ntimes, n) Cartesian positions, traj_t (ntimes, n) ln t, traj_n (n) points."""
+    traj (3, ntimes, n) Cartesian positions, traj_t (ntimes, n) ln t, traj_n (n) points.
+    With flux_nbins (art_propagate_host_flux) also `flux` (2, flux_nbins): the batch's binned
+    radiated flux (plot/flux.py:38-48), axions in row 0, photons in row 1."""
     lib = _lib.load()
     n = int(np.asarray(erg).size)
     f64 = lambda a: np.ascontiguousarray(a, np.float64)  # noqa: E731
@@ -204,6 +206,12 @@ def propagate_batch(params: Params, x0, k0, erg, dw, ln_t0, species, max_crossin
                                           _ptr(out["traj"]), _ptr(out["traj_t"]), _ptr(out["traj_n"])))
         out["traj"] = out["traj"].reshape(3, ntimes, n)
         out["traj_t"] = out["traj_t"].reshape(ntimes, n)
+    elif flux_nbins:
+        out["flux"] = np.zeros(2 * int(flux_nbins))
+        check(lib.art_propagate_host_flux(C.byref(cp), n, _ptr(x0), _ptr(k0), _ptr(erg), _ptr(dw), _ptr(ln_t0),
+                                          _ptr(species), int(max_crossings), C.byref(so), C.byref(xb),
+                                          int(flux_nbins), _ptr(out["flux"])))
+        out["flux"] = out["flux"].reshape(2, int(flux_nbins))
     else:
         check(lib.art_propagate_host(C.byref(cp), n, _ptr(x0), _ptr(k0), _ptr(erg), _ptr(dw), _ptr(ln_t0),
                                      _ptr(species), int(max_crossings), C.byref(so), C.byref(xb)))
@@ -221,6 +229,20 @@ def last_stats() -> dict:
     d = {k: int(s[i]) for i, k in enumerate(keys)}
     d["grid"] = int(g.value)
     return d
+
+
+HOST_PATH_KEYS = ("calls", "streamed", "stream_giveups", "chunked", "single")
+
+
+def host_path_counters(reset=False) -> dict:
+    """What this process's art_propagate_host* calls ran as (art_host_path_counters): calls,
+    streamed-pipeline completions, streamed give-ups (rerun as one launch), chunked and
+    single-launch calls."""
+    c = (C.c_uint64 * len(HOST_PATH_KEYS))()
+    rc = _lib.load().art_host_path_counters(c, len(HOST_PATH_KEYS), 1 if reset else 0)
+    if rc < 0:
+        check(rc)
+    return {k: int(c[i]) for i, k in enumerate(HOST_PATH_KEYS)}
 
 
 def Find_Conversion_Surface(params: Params) -> float:

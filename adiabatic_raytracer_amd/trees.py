@@ -268,23 +268,41 @@ def main_runner_tree(params: Params, Ntajs: int, *, seed=1769, ntimes=1000, rho_
     return rows
 
 
-def radiated_flux(phif, ident, weights, nbins=50) -> np.ndarray:
+def radiated_flux(phif, ident, weights, nbins=50, range=(-np.pi, np.pi)) -> np.ndarray:
     """The binned flux of plot/flux.py:38-48 on the GPU: np.histogram(phif, nbins,
-    range=(-π, π), weights=weights) for axion rows (ident 0) and photon rows (ident 1),
-    as a (2 * nbins,) array [axions | photons]. The reference's radiated flux is the photon
-    half with weights = weight * sln_prob (npy columns 9 and 8)."""
+    range=range, weights=weights) for axion rows (ident 0) and photon rows (ident 1), as a
+    (2 * nbins,) array [axions | photons]. The reference's radiated flux is the photon half with
+    weights = weight * sln_prob (npy columns 9 and 8). range=None bins like flux.py:43-47 itself,
+    np.histogram(phif, bins=nbins) without a range: over [min φf, max φf] of ALL the rows
+    (numpy's rule, ±0.5 when they are equal); `flux_edges` gives those edges."""
     import torch
     lib = _lib.load()
     n = len(phif)
+    lo, hi = flux_range(phif) if range is None else (float(range[0]), float(range[1]))
     dev = torch.device("cuda", torch.cuda.current_device())
     f = lambda a, dt=torch.float64: torch.as_tensor(np.ascontiguousarray(a), dtype=dt).to(dev)  # noqa: E731
     ph, sp, ww = f(phif), f(np.asarray(ident) != 0, torch.int8), f(weights)
     hist = torch.zeros(2 * nbins, dtype=torch.float64, device=dev)
     stream = C.c_void_p(torch.cuda.current_stream().cuda_stream)
-    check(lib.art_flux_histogram_phi_device(n, C.c_void_p(ph.data_ptr()), C.c_void_p(sp.data_ptr()),
-                                            C.c_void_p(ww.data_ptr()), int(nbins), C.c_void_p(hist.data_ptr()),
-                                            stream))
+    check(lib.art_flux_histogram_phi_range_device(n, C.c_void_p(ph.data_ptr()), C.c_void_p(sp.data_ptr()),
+                                                  C.c_void_p(ww.data_ptr()), int(nbins), lo, hi,
+                                                  C.c_void_p(hist.data_ptr()), stream))
     return hist.cpu().numpy()
+
+
+def flux_range(phif):
+    """np.histogram's range when none is given: (min, max) of the data, widened by 0.5 on each
+    side when they are equal, (0, 1) for no data."""
+    a = np.asarray(phif, np.float64)
+    if a.size == 0:
+        return 0.0, 1.0
+    lo, hi = float(a.min()), float(a.max())
+    return (lo - 0.5, hi + 0.5) if lo == hi else (lo, hi)
+
+
+def flux_edges(lo, hi, nbins=50):
+    """The bin edges np.histogram uses for `nbins` equal bins of [lo, hi] (np.linspace)."""
+    return np.linspace(lo, hi, nbins + 1)
 
 
 def gather_rank_rows(dir_tag, params: Params, Ntajs, world, file_tag="", ntimes=3, num_cutoff=5, MC_nodes=5,

@@ -4,11 +4,17 @@
 A "step" = one pass of the hot path over one batch: RT.propagate of every segment of the
 batch (RayTracer.jl:171-452: Vern6 + resonance scan + crossing polish + conversion
 probability at the crossing), the binned flux of the escaping photons (plot/flux.py:38-48)
-and, for N > 1, its RCCL all-reduce. Inputs are forward-tree roots sampled ON THE GPU with
+and, for N > 1, its RCCL all-reduce. Inputs are forward-tree roots sampled on the GPU with
 the restated find_samples_new (seed 1769, Philox keyed by global ray id) BEFORE the timed
-region, so they are resident in HBM when timing starts.
+region (reported apart, `ic_sampling_s`) and copied to host arrays.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--rays R] [--config flat|gr]
+
+The timed region is BASELINE.md §2 / SURVEY §8(d)'s: H2D + kernels + D2H. Each step hands
+the batch to art_propagate_host_flux as pageable host arrays (what a Julia ccall from
+MainRunner.jl:179-190 passes) and gets every output back in host arrays, so `value` is the
+drop-in rate. The same passes on device-resident inputs are reported as side figures
+(`device_resident`, and `device_resident_in_flight` with several batches on as many streams).
 
 N > 1: launched by torch.distributed.run, one rank per GPU; the R rays are sharded in
 contiguous blocks (strong scaling of the fixed 1e7-ray batch named by BASELINE.json).
@@ -91,37 +97,35 @@ def host_cores():
     return n
 
 
-def pcie_inclusive(eng, inp, n, accepted_per_launch, reps=2):
-    """The host-buffer rate: art_propagate_host on pageable host
-    arrays -- H2D of the inputs, the kernels, D2H of every output -- as a Julia ccall would
-    run it. Outputs are allocated and faulted in once, outside the timing."""
-    import ctypes as C
-    from adiabatic_raytracer_amd._lib import CrossingBuf, SegmentOut, check, load
-    lib = load()
-    h = {k: inp[k].cpu().numpy() for k in ("x0", "k0", "erg", "dw", "ln_t0", "species")}
+def host_arrays(inp, n):
+    """This rank's batch as a Julia caller holds it (MainRunner.jl:179-190 hands host arrays
+    to propagate): pageable numpy inputs, and output arrays allocated and faulted in once."""
+    h = {k: np.ascontiguousarray(inp[k].cpu().numpy()) for k in ("x0", "k0", "erg", "dw", "ln_t0", "species")}
     out = {"x_end": np.ones(3 * n), "k_end": np.ones(3 * n), "u7_end": np.ones(n), "tau_end": np.ones(n),
            "status": np.ones(n, np.int32), "n_accept": np.ones(n, np.int32), "n_reject": np.ones(n, np.int32),
            "n_cross": np.ones(n, np.int32), "xc_pos": np.ones(3 * n), "xc_k": np.ones(3 * n), "xc_t": np.ones(n),
            "xc_dw": np.ones(n), "xc_p": np.ones(n)}
-    P = lambda a: a.ctypes.data_as(C.c_void_p)  # noqa: E731
-    so = SegmentOut(*[P(out[k]) for k in ("x_end", "k_end", "u7_end", "tau_end", "status", "n_accept", "n_reject")])
-    xb = CrossingBuf(1, *[P(out[k]) for k in ("n_cross", "xc_pos", "xc_k", "xc_t", "xc_dw", "xc_p")])
-    cp = eng.cp
+    return h, out
 
-    def run():
-        check(lib.art_propagate_host(C.byref(cp), n, *[P(h[k]) for k in ("x0", "k0", "erg", "dw", "ln_t0", "species")],
-                                     -1, C.byref(so), C.byref(xb)))
-    run()  # staging buffers
+
+def timed(run, steps, warmup, world, sync):
+    """W untimed warmup steps, then EXACTLY `steps` steps bracketed by a barrier and a device
+    synchronize on both sides; returns this rank's elapsed seconds."""
+    import torch.distributed as dist
+    for i in range(warmup):
+        run(i)
+    sync()
+    if world > 1:
+        dist.barrier()
+    sync()
     t0 = time.perf_counter()
-    for _ in range(reps):
-        run()
-    dt = (time.perf_counter() - t0) / reps
-    in_b = sum(a.nbytes for a in h.values())
-    out_b = sum(a.nbytes for a in out.values())
-    return {"value": accepted_per_launch / dt, "unit": "ray-steps/s", "ms_per_step": dt * 1e3,
-            "h2d_bytes": in_b, "d2h_bytes": out_b,
-            "note": "art_propagate_host on pageable host buffers (H2D + init/integrator/finalize kernels + "
-                    "D2H), rank 0, same batch; value above is device-resident"}
+    for i in range(steps):
+        run(warmup + i)
+    sync()
+    if world > 1:
+        dist.barrier()
+    sync()
+    return time.perf_counter() - t0
 
 
 def main():
@@ -135,29 +139,25 @@ def main():
     ap.add_argument("--seed", type=int, default=1769)
     ap.add_argument("--nbins", type=int, default=50)
     ap.add_argument("--streams", type=int, default=0,
-                    help="batches in flight (HIP streams); 0: 1 for per-GPU batches of >= 8e6 rays, else 4 "
-                         "(16 for the GR configs)")
+                    help="device-resident side figure: batches in flight (HIP streams); 0: 1 for per-GPU batches "
+                         "of >= 8e6 rays, else 4 (16 for the GR configs)")
     ap.add_argument("--cpu-rays", type=int, default=int(os.environ.get("ART_CPU_RAYS", "500000")))
     ap.add_argument("--cpu-rays-1t", type=int, default=int(os.environ.get("ART_CPU_RAYS_1T", "24000")))
     ap.add_argument("--donate", type=int, default=-1,
-                    help="tail donation lanes (art_set_tail_donation); -1: auto by streams in flight")
+                    help="tail donation lanes for the device-resident passes in flight; -1: auto")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-pcie", action="store_true")
+    ap.add_argument("--no-device", action="store_true", help="skip the device-resident side figures")
+    ap.add_argument("--no-pcie", action="store_true", help="(compat) same as --no-device")
     args = ap.parse_args()
     n_shard = args.rays // max(1, int(os.environ.get("WORLD_SIZE", "1")))  # this rank's share (to within one ray)
+    gr = not CONFIGS[args.config].get("flat", False)
     if args.streams <= 0:
-        # the drain tail (~3 ms: the last long rays) is ~3% of a 1e7-ray pass but ~20% of the
-        # 1.25e6 rays per GPU of the 8-GPU split; overlapping passes (with tail donation, below)
-        # hides most of it there. Measured per shard size with donation
-        # (profiles/r02d_streams_by_shard_donation.txt): 1e6-5e6 rays best with 3 passes in
-        # flight; round 3 (tail kernel, two-level donation): 1.25e6 rays 3.16e9 on 3 streams,
-        # 3.31e9 on 4, 3.30e9 on 6, so 4. The GR batch is bound by its longest ray (~185 ms
-        # alone on the tail kernel), so only more passes in flight amortise it: 4.2e8 on 3,
-        # 6.3e8 on 6, 5.9-6.2e8 on 8, 7.4-8.7e8 on 12, 7.8-9.8e8 on 16 across fresh boxes
-        # (profiles/r03grv_gr_streams_variance.txt), so 16 for the GR configs. Overlapped launches stretch each other's measured duration, so
-        # the single-GPU headline (1e7 rays) runs one pass at a time and its roofline is the
-        # kernel's own (2 passes with donation: +1%).
-        gr = not CONFIGS[args.config].get("flat", False)
+        # device-resident side figure only (value is one host call per batch). The drain tail
+        # (~3 ms: the last long rays) is ~3% of a 1e7-ray pass but ~20% of the 1.25e6 rays per GPU
+        # of the 8-GPU split; overlapping passes (with tail donation) hides most of it: 1.25e6
+        # rays 3.31e9 on 4 streams. The GR batch is bound by its longest ray (~185 ms alone on the
+        # tail kernel), so only more passes in flight amortise it (profiles/r03grv_gr_streams_
+        # variance.txt): 16 for the GR configs.
         args.streams = 1 if n_shard >= 8_000_000 else (16 if gr else 4)
     # concurrent passes need a hardware queue each (read at HIP init; the image's default is 4)
     if args.streams > 3 and int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < args.streams + 1:
@@ -168,6 +168,7 @@ def main():
 
     import adiabatic_raytracer_amd as A
     from adiabatic_raytracer_amd import Engine
+    from adiabatic_raytracer_amd._lib import CrossingBuf, SegmentOut, check
     from adiabatic_raytracer_amd.shard import allreduce_flux, reduce_totals, shard_range
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -187,6 +188,7 @@ def main():
 
     params = A.Params(integrator=args.integrator, **CONFIGS[args.config])
     eng = Engine(params, device=local)
+    lib = A._lib.load()
     # contiguous shard of the global batch; Philox keyed by global ray id -> GPU-count independent
     lo, hi = shard_range(args.rays, rank, world)
     n = hi - lo
@@ -194,138 +196,200 @@ def main():
     inp = eng.forward_roots(n, seed=args.seed, ray_offset=lo)
     torch.cuda.synchronize()
     sample_s = time.perf_counter() - t_s
-    # `streams` batches in flight: step i runs on stream i % streams with its own outputs, so
-    # the drain tail of one pass (its last long rays on a few CUs) overlaps the next pass's
-    # bulk instead of idling the GPU. Each launch has its own scratch (include/art.h).
-    if args.donate < 0:
-        # tail donation only pays when another pass in flight can take the freed CU slots:
-        # 1e6 rays on 3 streams +9%, 1.25e6 +6%; a lone pass loses 0.6-1.7% (its donated rays
-        # resume only after the pass; profiles/r02d_tail_donation.txt)
-        args.donate = 16 if args.streams > 1 else 0
-    eng.set_tail_donation(args.donate)
-    streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(args.streams - 1)]
-    outs = [eng.alloc_out(n, capacity=1) for _ in streams]
-    hists = [torch.zeros(2 * args.nbins, dtype=torch.float64, device=eng.device) for _ in streams]
-    for st_ in streams[1:]:
-        st_.wait_stream(streams[0])  # the sampled inputs and the outputs' initialisation
-    out, hist = outs[0], hists[0]
+    hist_dev = world > 1 and backend == "nccl"  # RCCL reduces device tensors, gloo host ones
 
-    def one_step(i):
-        k = i % len(streams)
-        with torch.cuda.stream(streams[k]):
-            eng.propagate(inp, outs[k], max_crossings=-1)
-            hists[k].zero_()
-            eng.flux_histogram(outs[k], inp["species"], None, args.nbins, hists[k])
-            allreduce_flux(hists[k], world)  # the only data-path collective: the binned flux (RCCL over xGMI)
+    def sync():
+        torch.cuda.synchronize()
 
-    for i in range(args.warmup):
-        one_step(i)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        one_step(args.warmup + i)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    # per-launch integrator durations (HIP events on each launch's own stream) and the
-    # launch's counters; every step integrates the same batch, so its accepted steps are
-    # the same each time (checked against the outputs)
+    # ---- the headline: BASELINE §2 / SURVEY §8(d)'s timed region, H2D + kernels + D2H ----
+    # One step = art_propagate_host_flux on this rank's pageable batch (inputs up, the init /
+    # integrator / finalize kernels, every output back into the caller's arrays, the batch's
+    # binned flux from the outputs while they are in HBM) and the all-reduce of that flux over
+    # the ranks (RCCL over xGMI; the path's only exchange, north_star).
+    h, hout = host_arrays(inp, n)
+    P = lambda a: a.ctypes.data_as(C.c_void_p)  # noqa: E731
+    so = SegmentOut(*[P(hout[k]) for k in ("x_end", "k_end", "u7_end", "tau_end", "status", "n_accept", "n_reject")])
+    xb = CrossingBuf(1, *[P(hout[k]) for k in ("n_cross", "xc_pos", "xc_k", "xc_t", "xc_dw", "xc_p")])
+    hflux = np.zeros(2 * args.nbins)
+    flux_red = {}
+
+    def host_step(i):
+        check(lib.art_propagate_host_flux(C.byref(eng.cp), n, *[P(h[k]) for k in ("x0", "k0", "erg", "dw", "ln_t0",
+                                                                                 "species")],
+                                          -1, C.byref(so), C.byref(xb), args.nbins, P(hflux)))
+        t = torch.from_numpy(hflux.copy())
+        flux_red["host"] = allreduce_flux(t.to(eng.device) if hist_dev else t, world)
+
+    A.raytracer.host_path_counters(reset=True)
+    for i in range(args.warmup):  # (the first call also allocates the pinned staging and streams)
+        host_step(i)
+    cnt_w = A.raytracer.host_path_counters(reset=True)
+    host_s = timed(host_step, args.steps, 0, world, sync)
+    cnt = A.raytracer.host_path_counters()
+    # every timed pass ran the path its size selects, and none gave up and ran twice
+    assert cnt["stream_giveups"] == 0, f"streamed host pipeline gave up inside the timed passes: {cnt}"
+    assert cnt["calls"] == args.steps, cnt
     kms_buf = (C.c_double * args.steps)()
-    got = A._lib.load().art_recent_kernel_ms(args.steps, kms_buf)
-    kernel_ms = list(kms_buf)[:max(0, got)]
-    eng.kernel_ms()  # latches the last launch's counters
-    stats_last = A.raytracer.last_stats()
-    k_last = (args.warmup + args.steps - 1) % len(streams)
-    out, hist = outs[k_last], hists[k_last]
-    assert int(out["n_accept"].sum().item()) == stats_last["accepted"]
-    accepted = stats_last["accepted"] * args.steps
-    # whole-job aggregates: Σ ray-steps over ranks / max wall time over ranks
-    total_steps, t_max, total_rays = reduce_totals(accepted, elapsed, n, world, device=eng.device)
+    got = lib.art_recent_kernel_ms(args.steps, kms_buf)
+    host_kms = list(kms_buf)[:max(0, got)]
+    host_stats = A.raytracer.last_stats()
+    assert int(hout["n_accept"].sum()) == host_stats["accepted"]
+    host_steps_total, host_t_max, total_rays = reduce_totals(host_stats["accepted"] * args.steps, host_s, n, world,
+                                                             device=eng.device if hist_dev else None)
+    host_status = hout["status"].copy()
+
+    # ---- side figure: the same passes on device-resident inputs (art_propagate_device) ----
+    dev = None
+    if not (args.no_device or args.no_pcie):
+        donate = args.donate if args.donate >= 0 else (16 if args.streams > 1 else 0)
+
+        def device_run(nstreams, donate_lanes, steps, warmup):
+            eng.set_tail_donation(donate_lanes)
+            streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(nstreams - 1)]
+            outs = [eng.alloc_out(n, capacity=1) for _ in streams]
+            hists = [torch.zeros(2 * args.nbins, dtype=torch.float64, device=eng.device) for _ in streams]
+            for st_ in streams[1:]:
+                st_.wait_stream(streams[0])  # the sampled inputs and the outputs' initialisation
+
+            def one_step(i):
+                k = i % len(streams)
+                with torch.cuda.stream(streams[k]):
+                    eng.propagate(inp, outs[k], max_crossings=-1)
+                    hists[k].zero_()
+                    eng.flux_histogram(outs[k], inp["species"], None, args.nbins, hists[k])
+                    allreduce_flux(hists[k], world)
+            el = timed(one_step, steps, warmup, world, sync)
+            kb = (C.c_double * steps)()
+            g = lib.art_recent_kernel_ms(steps, kb)
+            eng.kernel_ms()  # latches the last launch's counters
+            st = A.raytracer.last_stats()
+            k_last = (warmup + steps - 1) % len(streams)
+            assert int(outs[k_last]["n_accept"].sum().item()) == st["accepted"]
+            tot, tmax, _ = reduce_totals(st["accepted"] * steps, el, n, world, device=eng.device)
+            eng.set_tail_donation(0)
+            return {"value": tot / tmax, "ms_per_step": tmax / steps * 1e3, "kernel_ms": float(np.mean(list(kb)[:g])),
+                    "streams": nstreams, "tail_donation": donate_lanes, "elapsed_s": el, "stats": st,
+                    "hist": hists[k_last].cpu().numpy()}
+        dev = {"one": device_run(1, 0, args.steps, args.warmup)}
+        if args.streams > 1:
+            dev["many"] = device_run(args.streams, donate, args.steps * max(1, min(args.streams, 4)), args.warmup)
 
     if rank == 0:
         fl_all = json.load(open(os.path.join(HERE, "tools", "flops.json")))
         fl, fl_r1 = fl_all[args.config], fl_all[args.config + "_round1"]
-        kms = float(np.mean(kernel_ms))
-        fpl = flops_per_launch(stats_last, fl, args.integrator)
-        # with several passes in flight the launches overlap, so one launch's own duration
-        # covers the device only in part: the rate is then priced on the wall per launch
-        # (the overlapped launches back to back), and kernel_ms stays each launch's duration
-        basis_ms = kms if len(streams) == 1 else elapsed * 1e3 / args.steps
-        achieved = fpl / (basis_ms * 1e-3) / 1e12
-        st = out["status"].cpu().numpy()
-        traffic, traffic_src = None, None
+        import hashlib
+        sha = hashlib.sha256(open(lib._name, "rb").read()).hexdigest()
+        pm = {}
         pmc_path = os.path.join(HERE, "profiles", "pmc_summary.json")
         if os.path.exists(pmc_path):
             pm = json.load(open(pmc_path))
             # only a PMC pass of this very library build and workload counts
-            import hashlib
-            sha = hashlib.sha256(open(A._lib.load()._name, "rb").read()).hexdigest()
-            if pm.get("workload") == f"{args.config}:{n}" and pm.get("libart_sha256") == sha:
-                traffic = pm.get("hbm_bytes_per_launch")
-                traffic_src = ("stored PMC pass of this libart.so build (profiles/pmc_summary.json, sha "
-                               f"{sha[:12]}, tools/pmc_passes.sh: FETCH_SIZE/WRITE_SIZE in separate passes, "
-                               "calibrated by tools/calib_hbm.hip); not measured in this run")
-        ncross = int((out["n_cross"].clamp(max=out["capacity"])).sum().item())
-        att = (out["n_accept"] + out["n_reject"]).double()
-        q = torch.quantile(att[:min(n, 1 << 24)], torch.tensor([0.5, 0.99, 0.999], dtype=torch.float64,
-                                                               device=att.device)).tolist()
+            if not (pm.get("workload") == f"{args.config}:{n}" and pm.get("libart_sha256") == sha):
+                pm = {}
+
+        def traffic(kind):
+            k = pm.get("kernels", {}).get(kind)
+            return (k["hbm_bytes_per_launch"], ("stored PMC pass of this libart.so build (profiles/pmc_summary.json, "
+                                                f"sha {sha[:12]}, kernel {k['kernel']}, tools/pmc_passes.sh: FETCH_SIZE/"
+                                                "WRITE_SIZE in separate passes, calibrated by tools/calib_hbm.hip); not "
+                                                "measured in this run")) if k else (None, None)
+
+        kms = float(np.mean(host_kms))
+        fpl = flops_per_launch(host_stats, fl, args.integrator)
+        host_ms = host_t_max / args.steps * 1e3
+        ncross = int(np.minimum(hout["n_cross"], 1).sum())
+        att = (hout["n_accept"].astype(np.float64) + hout["n_reject"])
+        q = np.quantile(att, [0.5, 0.99, 0.999])
         attempt_dist = {"mean": float(att.mean()), "p50": q[0], "p99": q[1], "p999": q[2], "max": float(att.max())}
         alg_bytes = n * BYTES_PER_SEGMENT + ncross * BYTES_PER_CROSSING
+        streamed = cnt["streamed"] == args.steps
+        kname = (f"propagate_kernel<{'RK4' if args.integrator == 'rk4' else 'Vern6'}"
+                 f"{', streamed (DON=2)' if streamed else ''}>")
+        tr, tr_src = traffic("streamed" if streamed else "device")
+        in_b = sum(a.nbytes for a in h.values())
+        out_b = sum(a.nbytes for a in hout.values())
         line = {
             "metric": "ray-steps/sec (FP64), 10^7-ray GJ-dipole batch",
-            "value": total_steps / t_max,
+            "value": host_steps_total / host_t_max,
             "unit": "ray-steps/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": t_max / args.steps * 1e3,
+            "ms_per_step": host_ms,
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic: forward-tree roots sampled on the GPU by the restated find_samples_new (Philox seed 1769)",
+            "data": "synthetic: forward-tree roots sampled on the GPU by the restated find_samples_new (Philox seed "
+                    f"{args.seed}), handed over as pageable host arrays",
             "config": {"workload": f"{total_rays} photon segments, GJ dipole, "
-                                   f"{'flat space' if params.flat else 'Schwarzschild GR'}, {args.integrator}",
-                       "baseline_config": "configs[2] (1e7 rays, sharded over the GPUs)" if args.rays == 10_000_000
-                       else f"{args.rays} rays",
+                                   f"{'flat space' if params.flat else 'Schwarzschild GR'}, {args.integrator}; "
+                                   "one art_propagate_host call per rank per step (H2D + kernels + D2H, SURVEY 8(d))",
+                       "baseline_config": ("configs[2] (1e7 rays, sharded over the GPUs)" if args.rays == 10_000_000
+                                           else ("configs[3] (1e6 GR rays, one batch)" if gr and args.rays == 1_000_000
+                                                 else f"{args.rays} rays")),
                        "m_a_eV": params.mass_a, "theta_m": params.theta_m, "omega_pul": params.omega_pul,
                        "B0_G": params.B0, "rNS_km": params.rNS, "abstol": params.abstol, "reltol": params.reltol,
                        "interp_points": params.interp_points, "parallelism": f"rays sharded x{world}",
-                       "streams": args.streams, "tail_donation": args.donate},
-            "roofline": {"bound": "fp64-valu", "achieved": achieved, "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
-                         "frac": achieved / PEAK_FP64_TFLOPS, "traffic": traffic, "traffic_source": traffic_src,
-                         "kernel": f"propagate_kernel<{'RK4' if args.integrator == 'rk4' else 'Vern6'}>", "kernel_ms": kms,
-                         "flops_per_launch": fpl, "flops_per_ray_step": fpl / stats_last["accepted"],
-                         "time_basis": "launch duration (HIP events)" if len(streams) == 1
-                         else f"wall per launch ({len(streams)} overlapping passes)", "basis_ms": basis_ms,
-                         "frac_round1_flop_table": flops_per_launch(stats_last, fl_r1, args.integrator) / (basis_ms * 1e-3)
+                       "host_path": ("streamed pipeline" if streamed else
+                                     "single launch" if cnt["single"] == args.steps else str(cnt)),
+                       "host_path_counters": cnt, "host_path_counters_warmup": cnt_w},
+            "roofline": {"bound": "fp64-valu", "achieved": fpl / (kms * 1e-3) / 1e12, "peak": PEAK_FP64_TFLOPS,
+                         "unit": "TFLOP/s", "frac": fpl / (kms * 1e-3) / 1e12 / PEAK_FP64_TFLOPS,
+                         "traffic": tr, "traffic_source": tr_src, "kernel": kname, "kernel_ms": kms,
+                         "time_basis": "the integrator launch's own duration (HIP events on its stream), mean over "
+                                       "the timed passes",
+                         "achieved_wall": fpl / (host_ms * 1e-3) / 1e12,
+                         "frac_wall": fpl / (host_ms * 1e-3) / 1e12 / PEAK_FP64_TFLOPS,
+                         "wall_basis": "the whole host pass (ms_per_step: H2D + kernels + D2H)",
+                         "flops_per_launch": fpl, "flops_per_ray_step": fpl / host_stats["accepted"],
+                         "frac_round1_flop_table": flops_per_launch(host_stats, fl_r1, args.integrator) / (kms * 1e-3)
                                                    / 1e12 / PEAK_FP64_TFLOPS,
-                         "achieved_wall": fpl * args.steps / elapsed / 1e12,
                          "note": "FP64 VALU-bound (state in VGPRs, ~1 B of HBM per ray-step); peak = 78.6 TFLOP/s "
                                  "FP64 (vector = matrix dense peak). FLOPs from the kernel's counters x "
                                  "tools/flops.json (instrumented restatement).",
                          "hbm": {"algorithmic_bytes_per_launch": alg_bytes,
-                                 "achieved_GBs": alg_bytes / (basis_ms * 1e-3) / 1e9, "peak_GBs": PEAK_HBM_GBS,
-                                 "frac": alg_bytes / (basis_ms * 1e-3) / 1e9 / PEAK_HBM_GBS}},
-            "kernel_stats": stats_last,
-            "status_counts": np.bincount(st, minlength=5).tolist(),
+                                 "achieved_GBs": alg_bytes / (kms * 1e-3) / 1e9, "peak_GBs": PEAK_HBM_GBS,
+                                 "frac": alg_bytes / (kms * 1e-3) / 1e9 / PEAK_HBM_GBS},
+                         "pcie": {"h2d_bytes": in_b, "d2h_bytes": out_b,
+                                  "achieved_GBs": (in_b + out_b) / (host_ms * 1e-3) / 1e9}},
+            "kernel_stats": host_stats,
+            "status_counts": np.bincount(host_status, minlength=5).tolist(),
             "attempts_per_ray": attempt_dist,
+            "flux_hist_sum": float(flux_red["host"].sum()),
             "ic_sampling_s": sample_s,
         }
-        if not args.no_pcie:
-            line["pcie_inclusive"] = pcie_inclusive(eng, inp, n, stats_last["accepted"])
+        if dev:
+            def dev_obj(d, label):
+                fpl_d = flops_per_launch(d["stats"], fl, args.integrator)
+                basis = d["kernel_ms"] if d["streams"] == 1 else d["ms_per_step"]
+                trd, trd_src = traffic("device")
+                o = {"value": d["value"], "unit": "ray-steps/s", "ms_per_step": d["ms_per_step"],
+                     "workload": label, "streams": d["streams"], "tail_donation": d["tail_donation"],
+                     "roofline": {"achieved": fpl_d / (basis * 1e-3) / 1e12,
+                                  "frac": fpl_d / (basis * 1e-3) / 1e12 / PEAK_FP64_TFLOPS,
+                                  "kernel": "propagate_kernel<Vern6>" if args.integrator == "vern6" else
+                                            "propagate_kernel<RK4>", "kernel_ms": d["kernel_ms"],
+                                  "time_basis": ("launch duration (HIP events)" if d["streams"] == 1 else
+                                                 f"wall per launch ({d['streams']} overlapping passes)"),
+                                  "traffic": trd if d["streams"] == 1 else None,
+                                  "traffic_source": trd_src if d["streams"] == 1 else None,
+                                  "achieved_wall": fpl_d / (d["ms_per_step"] * 1e-3) / 1e12},
+                     "flux_equal_host": bool(np.array_equal(d["hist"], flux_red["host"].cpu().numpy()))}
+                return o
+            line["device_resident"] = dev_obj(dev["one"], "inputs already in HBM, one batch per step "
+                                                          "(art_propagate_device), outputs left in HBM")
+            if "many" in dev:
+                line["device_resident_in_flight"] = dev_obj(
+                    dev["many"], f"inputs in HBM, {dev['many']['streams']} batches in flight on as many HIP streams "
+                                 "(tail donation); a throughput figure, not one batch's latency")
         if world == 1 and not args.no_cpu_baseline:
             threads = int(os.environ.get("ART_CPU_THREADS", str(host_cores())))
 
             def sample(m):
-                xs = inp["x0"].view(3, n)[:, :m].cpu().numpy().reshape(-1)
-                ks = inp["k0"].view(3, n)[:, :m].cpu().numpy().reshape(-1)
-                return xs, ks, inp["erg"][:m].cpu().numpy()
+                xs = h["x0"].reshape(3, n)[:, :m].reshape(-1).copy()
+                ks = h["k0"].reshape(3, n)[:, :m].reshape(-1).copy()
+                return xs, ks, h["erg"][:m].copy()
             cfg = CONFIGS[args.config] | {"integrator": 0}
             m = min(args.cpu_rays, n)
             line["cpu_baseline"] = cpu_baseline(cfg, *sample(m), args.seed, threads)

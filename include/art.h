@@ -17,7 +17,9 @@
  *                                  RayTracer.jl:1480-1653, MainRunner.jl:463-529
  *   art_find_conversion_surface    RT.Find_Conversion_Surface RayTracer.jl:1250-1263
  *   art_flux_histogram_device      plot/flux.py:38-48 (binned flux of segment end states)
- *   art_flux_histogram_phi_device  plot/flux.py:38-48 (binned flux of the npy rows' φf)
+ *   art_flux_histogram_phi_device  plot/flux.py:38-48 (binned flux of the npy rows' φf;
+ *   art_flux_histogram_phi_range_device  _range: over flux.py's data-dependent bins)
+ *   art_propagate_host_flux        RT.propagate + the batch's binned flux (bench.py's step)
  *   art_comm_* / art_flux_allreduce  the reduction of the flux and counters over the GPUs of
  *                                  a node (the reference merges files instead,
  *                                  Combine_Files.py, Gen_Samples.jl:195-239)
@@ -139,6 +141,11 @@ const char* art_last_error(void);
 int art_device_count(int32_t* count);
 int art_set_device(int32_t device);
 int art_synchronize(void);
+/* Releases every device object the library holds (streams, events, pooled HBM and pinned
+ * staging, signal memory, the host copy threads) after draining its work; the next call
+ * re-creates what it needs. The library registers this to run at process exit, before the HIP
+ * runtime's own teardown; a host may also call it itself. */
+int art_shutdown(void);
 /* Duration [ms] of the last propagate kernel, from HIP events recorded on the stream
  * the kernel ran on. */
 double art_last_kernel_ms(void);
@@ -186,6 +193,24 @@ int art_propagate_device(const art_params* p, int64_t n, const double* x0, const
                          const double* erg, const double* dw, const double* ln_t0,
                          const int8_t* species, int32_t max_crossings,
                          art_segment_out* out, art_crossing_buf* xc, void* stream);
+/* art_propagate_host plus the batch's binned radiated flux (plot/flux.py:38-48, the quantity
+ * MainRunner.jl:749 normalises): hist[2*nbins] (host, overwritten; row 0 axions, row 1
+ * photons) counts the segments that end without a crossing beyond 1.1 rNS (MainRunner.jl:
+ * 203-209) by the azimuth atan2(k_y, k_x) of their final momentum, in nbins equal bins of
+ * [-pi, pi] with np.histogram's bin assignment. It is binned on the device while the outputs
+ * are still in HBM, so it costs no second pass over them; a multi-process run sums hist over
+ * its ranks (art_flux_allreduce_host). */
+int art_propagate_host_flux(const art_params* p, int64_t n, const double* x0, const double* k0,
+                            const double* erg, const double* dw, const double* ln_t0,
+                            const int8_t* species, int32_t max_crossings, art_segment_out* out,
+                            art_crossing_buf* xc, int32_t nbins, double* hist);
+/* What the art_propagate_host* calls of this process ran as, since load or the last reset:
+ * [0] calls, [1] streamed-pipeline completions, [2] streamed-pipeline give-ups (a wait
+ * outlasted its bound; the batch then ran again as one launch, same results), [3] chunked-
+ * pipeline calls, [4] single-launch calls (a give-up counts there too). Writes min(n, 5)
+ * counters (0 beyond), resets them when reset != 0, and returns 5. No reference counterpart
+ * (execution-path bookkeeping; bench.py asserts no give-up inside its timed passes). */
+int art_host_path_counters(uint64_t* counters, int32_t n, int32_t reset);
 
 /* ---- RT.propagate with its saved points (saveat, RayTracer.jl:176, 383, 427-444) ----
  * As art_propagate_*, plus up to ntimes (>= 2) saved points per ray: the start, the
@@ -332,6 +357,11 @@ int art_flux_histogram_device(const art_params* p, int64_t n, const double* x_en
  * flux is row 1 with w = weight * sln_prob (columns 9 and 8). */
 int art_flux_histogram_phi_device(int64_t n, const double* phi, const int8_t* species, const double* w,
                                   int32_t nbins, double* hist, void* stream);
+/* The same over [lo, hi] (finite, lo < hi): plot/flux.py:43-47 itself calls np.histogram(phif,
+ * bins=50) without a range, i.e. over [min φf, max φf] of the rows, and this reproduces those
+ * bins (edges linspace(lo, hi, nbins + 1), numpy's bin assignment). */
+int art_flux_histogram_phi_range_device(int64_t n, const double* phi, const int8_t* species, const double* w,
+                                        int32_t nbins, double lo, double hi, double* hist, void* stream);
 
 /* ---- reduction over the GPUs of a node (RCCL over xGMI) ----
  * One process per GPU. Rank 0 calls art_comm_unique_id and shares the 128 bytes with the

@@ -83,6 +83,17 @@ KEYS = ("x_end", "k_end", "u7_end", "tau_end", "status", "n_accept", "n_reject",
         "xc_dw", "xc_p")
 
 
+def host_flux(p, out, species, nbins):
+    """The binned radiated flux of plot/flux.py:38-48 over a batch's host outputs, in numpy:
+    segments that end without a crossing beyond 1.1 rNS (MainRunner.jl:203-209), binned by
+    atan2(k_y, k_x) over [-pi, pi], axions in row 0 and photons in row 1."""
+    n = species.size
+    x, k = out["x_end"].reshape(3, n), out["k_end"].reshape(3, n)
+    fin = (out["status"] != 1) & (np.sqrt((x * x).sum(0)) > 1.1 * p.rNS)
+    phi = np.arctan2(k[1], k[0])
+    return np.stack([np.histogram(phi[fin & (species == s)], nbins, range=(-np.pi, np.pi))[0] for s in (0, 1)]).astype(float)
+
+
 def _rows(r, idx, n):
     """Per-ray outputs of rays idx (numpy SoA layout [component][ray]) as one dict."""
     out = {}
@@ -240,12 +251,13 @@ def test_chunked_host_pipeline_is_bit_exact(cfg, species, cap, chunks, slots, mo
     q, k, mc = (p, s["k_init"], -1) if species == 1 else (replace(p, B0=-p.B0), -s["k_init"], 100000)
     args = (s["x"], k, s["erg"], -np.ones(n), np.full(n, -30.0), np.full(n, species, np.int8))
     monkeypatch.setenv("ART_HOST_MODE", "single")
-    ref = A.propagate_batch(q, *args, max_crossings=mc, capacity=cap)
+    ref = A.propagate_batch(q, *args, max_crossings=mc, capacity=cap, flux_nbins=50)
     monkeypatch.setenv("ART_HOST_MODE", "chunked")
     monkeypatch.setenv("ART_HOST_CHUNKS", str(chunks))
     monkeypatch.setenv("ART_HOST_SLOTS", str(slots))
     monkeypatch.setenv("ART_HOST_CHUNK_MIN", "1000")
-    got = A.propagate_batch(q, *args, max_crossings=mc, capacity=cap)
+    got = A.propagate_batch(q, *args, max_crossings=mc, capacity=cap, flux_nbins=50)
+    assert np.array_equal(got["flux"], host_flux(q, got, np.full(n, species, np.int8), 50))
     for key, v in ref.items():
         if isinstance(v, np.ndarray):
             assert np.array_equal(v, got[key], equal_nan=True), (cfg, key)
@@ -255,7 +267,37 @@ def test_chunked_host_pipeline_is_bit_exact(cfg, species, cap, chunks, slots, mo
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("cfg,species,cap,shift", [("flat", 1, 1, 11), ("flat", 0, 3, 12), ("gr", 1, 2, 11)])
+@pytest.mark.parametrize("slots", [1, 2])
+def test_chunked_host_pipeline_small_chunks(slots, monkeypatch):
+    """Chunks small enough for the tail kernel (<= ART_SMALL_TAIL rays, one record per ray in
+    the chunk's scratch) next to larger ones, with and without tail donation (ART_HOST_SLOTS 1:
+    donate = 0): the chunk's scratch slice is laid out with the launch's own small-batch
+    decision, so the results are the single launch's (slot 1 overran the slice)."""
+    import adiabatic_raytracer_amd as A
+    p = A.Params(**CONFIGS["flat"])
+    n = 3001  # chunks of ~300 (tail kernel) and ~1200 rays (persistent integrator)
+    s = A.sample_conversion_points(p, n, seed=1769)
+    args = (s["x"], s["k_init"], s["erg"], -np.ones(n), np.full(n, -30.0), np.ones(n, np.int8))
+    monkeypatch.setenv("ART_HOST_MODE", "single")
+    ref = A.propagate_batch(p, *args, capacity=2)
+    monkeypatch.setenv("ART_HOST_MODE", "chunked")
+    monkeypatch.setenv("ART_HOST_CHUNKS", "4")
+    monkeypatch.setenv("ART_HOST_SLOTS", str(slots))
+    monkeypatch.setenv("ART_HOST_CHUNK_MIN", "1000")
+    got = A.propagate_batch(p, *args, capacity=2)
+    for key, v in ref.items():
+        if isinstance(v, np.ndarray):
+            assert np.array_equal(v, got[key], equal_nan=True), key
+
+
+# the general-geometry instantiation (GEOM_ANY): boundary layer, isotropic plasma
+EXTRA = {"layer": dict(theta_m=0.2, mass_a=1e-5, flat=True, bndry_lyr=1.0),
+         "isotropic": dict(theta_m=0.2, mass_a=1e-5, flat=True, isotropic=True)}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg,species,cap,shift", [("flat", 1, 1, 11), ("flat", 0, 3, 12), ("gr", 1, 2, 11),
+                                                    ("layer", 1, 1, 11), ("isotropic", 1, 1, 12)])
 def test_streamed_host_pipeline_is_bit_exact(cfg, species, cap, shift, monkeypatch):
     """art_propagate_host's default for large batches is the streamed pipeline: one integrator
     launch over the whole batch while pieces of its inputs are still being uploaded and
@@ -265,23 +307,29 @@ def test_streamed_host_pipeline_is_bit_exact(cfg, species, cap, shift, monkeypat
     slot included, and the same statistics."""
     from dataclasses import replace
     import adiabatic_raytracer_amd as A
-    p = A.Params(**CONFIGS[cfg])
+    p = A.Params(**(CONFIGS[cfg] if cfg in CONFIGS else EXTRA[cfg]))
     n = 20011
     s = A.sample_conversion_points(p, n, seed=1769)
     q, k, mc = (p, s["k_init"], -1) if species == 1 else (replace(p, B0=-p.B0), -s["k_init"], 100000)
     args = (s["x"], k, s["erg"], -np.ones(n), np.full(n, -30.0), np.full(n, species, np.int8))
     monkeypatch.setenv("ART_HOST_MODE", "single")
-    ref = A.propagate_batch(q, *args, max_crossings=mc, capacity=cap)
+    ref = A.propagate_batch(q, *args, max_crossings=mc, capacity=cap, flux_nbins=50)
     monkeypatch.setenv("ART_HOST_MODE", "stream")
     monkeypatch.setenv("ART_HOST_PIECE_SHIFT", str(shift))
     monkeypatch.setenv("ART_HOST_CHUNK_MIN", "1000")
+    A.raytracer.host_path_counters(reset=True)
     for _ in range(2):  # the second call reuses the streams, signals and staging
-        got = A.propagate_batch(q, *args, max_crossings=mc, capacity=cap)
+        got = A.propagate_batch(q, *args, max_crossings=mc, capacity=cap, flux_nbins=50)
         for key, v in ref.items():
             if isinstance(v, np.ndarray):
                 assert np.array_equal(v, got[key], equal_nan=True), (cfg, key)
-        for key in ("attempts", "accepted", "root_steps", "scan_evals", "rays", "cert_steps"):
+        for key in ("attempts", "accepted", "root_steps", "scan_evals", "rays", "init_rhs", "cert_steps"):
             assert ref["stats"][key] == got["stats"][key], key
+    # both calls streamed (no give-up: a give-up would rerun as one launch with the same outputs)
+    assert A.raytracer.host_path_counters() == {"calls": 2, "streamed": 2, "stream_giveups": 0, "chunked": 0,
+                                                "single": 0}
+    # the device-binned flux (per piece in the streamed pipeline) is np.histogram of the outputs
+    assert np.array_equal(got["flux"], host_flux(q, got, np.full(n, species, np.int8), 50))
 
 
 @pytest.mark.gpu
@@ -299,12 +347,17 @@ def test_streamed_host_pipeline_gives_up_cleanly(monkeypatch):
     monkeypatch.setenv("ART_HOST_MODE", "stream")
     monkeypatch.setenv("ART_HOST_PIECE_SHIFT", "11")
     monkeypatch.setenv("ART_HOST_CHUNK_MIN", "1000")
-    for limit in ("0", "30000"):
+    A.raytracer.host_path_counters(reset=True)
+    for limit, want in (("0", {"streamed": 0, "stream_giveups": 1, "single": 1}),
+                        ("30000", {"streamed": 1, "stream_giveups": 1, "single": 1})):
         monkeypatch.setenv("ART_HOST_STREAM_TIMEOUT_MS", limit)
         got = A.propagate_batch(p, *args)
         for key, v in ref.items():
             if isinstance(v, np.ndarray):
                 assert np.array_equal(v, got[key], equal_nan=True), (limit, key)
+        # the give-up is visible to the caller (art_host_path_counters), not only on stderr
+        cnt = A.raytracer.host_path_counters()
+        assert {k: cnt[k] for k in want} == want, (limit, cnt)
 
 
 @pytest.mark.gpu

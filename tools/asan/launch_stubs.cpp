@@ -24,7 +24,7 @@ hipError_t launch_prob(const KParams&, int64_t, const double*, const double*, co
                        double*, hipStream_t) { return hipErrorNoDevice; }
 hipError_t launch_flux(const KParams&, int64_t, const double*, const double*, const int32_t*, const int8_t*,
                        const double*, int32_t, double*, hipStream_t) { return hipErrorNoDevice; }
-hipError_t launch_flux_phi(int64_t, const double*, const int8_t*, const double*, int32_t, double*, hipStream_t) {
+hipError_t launch_flux_phi(int64_t, const double*, const int8_t*, const double*, int32_t, double, double, double*, hipStream_t) {
   return hipErrorNoDevice;
 }
 hipError_t launch_eval_rhs(const KParams&, int64_t, const double*, const double*, const double*, const int8_t*, double*,

@@ -18,6 +18,11 @@ import adiabatic_raytracer_amd as A  # noqa: E402
 from adiabatic_raytracer_amd import Engine  # noqa: E402
 from adiabatic_raytracer_amd._lib import CrossingBuf, SegmentOut, check  # noqa: E402
 
+if os.environ.get("ART_MAPS_OUT"):  # the process's mappings at exit (resolving a crash PC)
+    import atexit
+    import shutil
+    atexit.register(lambda: shutil.copy("/proc/self/maps", os.environ["ART_MAPS_OUT"]))
+
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 10_000_000
 settings = sys.argv[2:] or ["stream", "single"]
 eng = Engine(A.Params(theta_m=0.2, mass_a=1e-5, flat=True))
