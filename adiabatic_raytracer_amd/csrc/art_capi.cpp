@@ -56,7 +56,7 @@ struct DeviceCtx {
   LaunchRec ring[RING];
   int next = 0, last = -1;       // next ring slot; the most recent propagate launch
   int64_t launches = 0;          // propagate launches issued so far
-  int32_t donate = 0;            // tail donation (art_set_tail_donation): lanes per wave, 0 = off
+  int32_t donate = -1;           // tail donation (art_set_tail_donation): lanes per wave, 0 = off, -1 = by geometry
   std::vector<std::pair<void*, size_t>> pool;  // host-entry staging buffers (grow-only, used under g_mu by the
                                                // synchronous *_host calls only)
   // the chunked host pipeline of art_propagate_host (propagate_host_chunked): its compute
@@ -390,7 +390,17 @@ struct LaunchOpts {
   hipStream_t finalize_stream = nullptr;  // finalize_kernel on this stream (after the integrator)
 };
 
-int launch_donate(DeviceCtx* c, const LaunchOpts& o) { return o.donate >= 0 ? o.donate : c->donate; }
+// Tail donation of a launch: the caller's choice, else the device's setting, else (-1, the
+// default) by geometry. A Schwarzschild batch is bound by its few longest rays (configs[3]: ray
+// 717277 takes 23 592 attempts), which a lone pass would run on one lane of a draining wave
+// (13.5 us per attempt); donated, they finish on the one-wave-per-ray tail kernel (7.7 us). A
+// flat lone pass has no such ray, and donation costs its drain 0.5-1.3%.
+int launch_donate(DeviceCtx* c, const LaunchOpts& o, const art_params* p, const TrajArgs& tr) {
+  if (o.donate >= 0) return o.donate;
+  if (c->donate >= 0) return c->donate;
+  const bool sch = !p->flat && !(p->bndry_lyr > 0.0) && !p->isotropic;
+  return (sch && p->integrator == ART_VERN6 && tr.ntimes == 0) ? 16 : 0;
+}
 
 // A small Vern6 batch without saveat runs every ray on a wave of its own (tail_kernel): the
 // latency of a Julia host's per-event calls (its rays run ~40% faster per attempt than a lone
@@ -441,7 +451,7 @@ int propagate_device_impl(const art_params* p, int64_t n, const double* x0, cons
   const art::KParams K = kparams(*p);
   const int cap = (xc && xc->count) ? xc->capacity : 0;
   const bool small_tail = use_small_tail(p, n, tr);
-  const int32_t donate = small_tail ? 0 : launch_donate(c, opt);
+  const int32_t donate = small_tail ? 0 : launch_donate(c, opt, p, tr);
   ScratchLayout SL;
   if ((rc = scratch_layout(c, n, cap, donate, &SL, small_tail))) return rc;
   if (opt.scratch && SL.total() > opt.scratch_bytes)
@@ -551,7 +561,7 @@ int art_set_device(int32_t device) {
 
 int art_set_tail_donation(int32_t lanes) {
   std::lock_guard<std::mutex> lk(g_mu);
-  if (lanes < 0 || lanes > 63) return fail(ART_E_INVALID, "tail donation lanes must be in [0, 63]");
+  if (lanes < -1 || lanes > 63) return fail(ART_E_INVALID, "tail donation lanes must be in [-1, 63]");
   DeviceCtx* c;
   int rc = current_ctx(&c);
   if (rc) return rc;

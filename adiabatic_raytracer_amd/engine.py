@@ -81,7 +81,8 @@ class Engine:
     def set_tail_donation(self, lanes: int) -> None:
         """Tail donation for launches pipelined with others on other streams
         (art_set_tail_donation, include/art.h): a drained wave with <= lanes live rays hands
-        them to a continuation launch and retires. Bit-identical results; 0 = off."""
+        them to a continuation launch and retires. Bit-identical results; 0 = off, -1 = the
+        library's default by geometry (16 for Schwarzschild batches, else 0)."""
         check(self.lib.art_set_tail_donation(int(lanes)))
 
     def kernel_ms(self) -> float:

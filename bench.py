@@ -266,11 +266,11 @@ def main():
             k_last = (warmup + steps - 1) % len(streams)
             assert int(outs[k_last]["n_accept"].sum().item()) == st["accepted"]
             tot, tmax, _ = reduce_totals(st["accepted"] * steps, el, n, world, device=eng.device)
-            eng.set_tail_donation(0)
+            eng.set_tail_donation(-1)
             return {"value": tot / tmax, "ms_per_step": tmax / steps * 1e3, "kernel_ms": float(np.mean(list(kb)[:g])),
                     "streams": nstreams, "tail_donation": donate_lanes, "elapsed_s": el, "stats": st,
                     "hist": hists[k_last].cpu().numpy()}
-        dev = {"one": device_run(1, 0, args.steps, args.warmup)}
+        dev = {"one": device_run(1, -1, args.steps, args.warmup)}  # (-1: the library default by geometry)
         if args.streams > 1:
             dev["many"] = device_run(args.streams, donate, args.steps * max(1, min(args.streams, 4)), args.warmup)
 

@@ -161,9 +161,12 @@ int art_recent_kernel_ms(int32_t n, double* ms);
  * flight on different streams): once a launch's work queue is drained, a wave with at most
  * `lanes` live rays (all between steps) hands them to a continuation launch on the same
  * stream and retires, so its CU slot goes to the next batch instead of idling behind one
- * long ray. The continuation launch integrates the donated rays packed into full waves;
- * results are bit-identical to lanes = 0 (the default: off). Applies to the current
- * device's subsequent launches. No reference counterpart (an execution policy). */
+ * long ray. The continuation launch integrates the donated rays packed into full waves, and
+ * its own last rays finish one per wave (the tail kernel); results are bit-identical to
+ * lanes = 0 (off). -1 (the default) chooses by geometry: 16 for Schwarzschild Vern6 batches,
+ * whose few longest rays set a lone batch's wall time (configs[3]), 0 otherwise. Applies to
+ * the current device's subsequent launches (the streamed host pipeline never donates). No
+ * reference counterpart (an execution policy). */
 int art_set_tail_donation(int32_t lanes);
 /* The Vern6 tableau the kernel uses: c[9], A[81] row-major, b[9], bhat[9]. */
 int art_vern6_tableau(double* c, double* A, double* b, double* bhat);

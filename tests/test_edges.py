@@ -220,7 +220,7 @@ print(json.dumps(out))
 
 @pytest.mark.gpu
 def test_small_batch_w1_first_launch_in_fresh_process():
-    """Round 2's reproducer (tools/exp_axn_case.py flat 1 2000 8): a fresh process samples 2000
+    """Round 2's reproducer (tools/exp_axn_case.py flat 1 2000 8, in the git history): a fresh process samples 2000
     flat roots and runs them, first as photons then as backtrace axions, with crossing capacity
     8 on the 1-wave/SIMD build. Both launches succeed, on the 1-wave grid (one block per CU)."""
     import json

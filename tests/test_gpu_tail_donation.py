@@ -22,7 +22,7 @@ def _run(eng, inp, lanes):
         eng.kernel_ms()
         st = dict(A.raytracer.last_stats())
     finally:
-        eng.set_tail_donation(0)
+        eng.set_tail_donation(-1)
     torch.cuda.synchronize()
     return {k: v.cpu().numpy() for k, v in out.items() if hasattr(v, "cpu")}, st
 
@@ -55,7 +55,7 @@ def test_tail_donation_rejects_bad_lane_counts():
     import adiabatic_raytracer_amd as A
     from adiabatic_raytracer_amd import Engine
     eng = Engine(A.Params(**CONFIGS["flat"]))
-    for bad in (-1, 64):
+    for bad in (-2, 64):
         with pytest.raises(A.ArtError):
             eng.set_tail_donation(bad)
 
@@ -67,7 +67,7 @@ def _host_run(p, args, lanes, **kw):
     try:
         return A.propagate_batch(p, *args, **kw)
     finally:
-        A._lib.check(lib.art_set_tail_donation(0))
+        A._lib.check(lib.art_set_tail_donation(-1))
 
 
 @pytest.mark.parametrize("cfg", ["flat", "gr"])
