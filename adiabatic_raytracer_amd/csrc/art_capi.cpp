@@ -899,7 +899,8 @@ constexpr int STREAM_FALLBACK = 1 << 20;
 int stream_setup(DeviceCtx* c, int reserve, int nsig) {
   int ncu = 0;
   HIP_OK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device));
-  if (reserve < 8 || reserve % 8 != 0 || reserve >= ncu / 2)
+  // (reserve = 0, dev only: the three streams CU-masked with every CU, to time the masked queue itself)
+  if (reserve != 0 && (reserve < 8 || reserve % 8 != 0 || reserve >= ncu / 2))
     return fail(ART_E_INVALID, "ART_HOST_RESERVE_CUS must be a multiple of 8 in [8, %s)", std::to_string(ncu / 2).c_str());
   const int key = reserve * 2 + (env_int("ART_HOST_RESERVE_XCD", 0) != 0 ? 1 : 0);
   if (!c->s_comp || c->reserve != key) {
@@ -919,6 +920,7 @@ int stream_setup(DeviceCtx* c, int reserve, int nsig) {
       const bool res = one_xcd ? (taken < reserve && i % 8 == 7) : i >= ncu - reserve;
       taken += res;
       (res ? mh : mc)[i / 32] |= 1u << (i % 32);
+      if (reserve == 0) mh[i / 32] |= 1u << (i % 32);
     }
     HIP_OK(hipExtStreamCreateWithCUMask(&c->s_comp, (uint32_t)words, mc.data()));
     HIP_OK(hipExtStreamCreateWithCUMask(&c->s_in, (uint32_t)words, mh.data()));
@@ -1233,8 +1235,8 @@ int propagate_host_impl(const art_params* p, int64_t n, const double* x0, const 
   if (cap && (rc = pool_get(c, 2, xc_bytes, &dxc))) return rc;
   double* di = (double*)din;
   hipStream_t s = c->stream;
-  if (const int r = env_int("ART_DEV_SINGLE_MASKED", 0)) {  // (dev: the single launch on a CU-masked stream)
-    if ((rc = stream_setup(c, r, 1))) return rc;
+  if (const int r = env_int("ART_DEV_SINGLE_MASKED", 0)) {  // (dev: the single launch on a CU-masked stream;
+    if ((rc = stream_setup(c, r < 0 ? 0 : r, 1))) return rc;  //  -1: masked with every CU)
     s = c->s_comp;
   }
   HIP_OK(hipMemcpyAsync(di, x0, nd * 3 * sizeof(double), hipMemcpyHostToDevice, s));

@@ -22,8 +22,8 @@ cfg = sys.argv[1] if len(sys.argv) > 1 else "flat"
 counts = [int(c) for c in (sys.argv[2] if len(sys.argv) > 2 else "1000,10000").split(",")]
 n_cpu = int(sys.argv[3]) if len(sys.argv) > 3 else 50
 p = A.Params(**CFG[cfg])
-DONATE = int(os.environ.get("ART_DONATE", "0"))  # tail donation of the forest's launches (art_set_tail_donation)
-if DONATE:
+DONATE = int(os.environ.get("ART_DONATE", "-1"))  # tail donation of the forest's launches (-1: the library default)
+if DONATE >= 0:
     import ctypes as C
     A._lib.load().art_set_tail_donation(C.c_int32(DONATE))
 
