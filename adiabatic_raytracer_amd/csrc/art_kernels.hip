@@ -749,9 +749,15 @@ __global__ __launch_bounds__(BLOCK, WPS) void propagate_kernel(const KParams P_i
       ART_SMARK(10)
     }
     ART_TMARK(1)  // step size and stage slots
-#ifdef ART_PRIO_PHASE
-    // (dev A/B) the latency-bound rest of the iteration at a higher issue priority than the
-    // partner wave's stage slots, so its short dependent chains issue as soon as they can
+#ifndef ART_NO_PRIO_PHASE
+    // The rest of the iteration -- error norm, controller, certificate, scan, walk, refill --
+    // is latency-bound (short dependent chains, LDS round trips, the loads of a refill), the
+    // stage slots issue-bound. At a higher issue priority than the partner wave's stage slots,
+    // its instructions issue as soon as they are ready and the slots fill the gaps, instead of
+    // the older wave's slots taking every issue cycle while this wave's chain waits behind
+    // them (the arbiter goes by priority, then age). The priority drops back to the slots' level
+    // at the top of the next iteration. 1e7 flat rays: 84.34 -> 82.53 ms, with the exp Horner
+    // 81.40 (profiles/r04b_ab.txt). ART_NO_PRIO_PHASE switches it off (A/B).
     if (outlier) __builtin_amdgcn_s_setprio(3);
     else __builtin_amdgcn_s_setprio(1);
 #endif
@@ -887,6 +893,10 @@ __global__ __launch_bounds__(BLOCK, WPS) void propagate_kernel(const KParams P_i
       const int tg = ns * nper, total = tg + nr;
       const int dj = ns ? 64 / ns : 0, dc = ns ? 64 % ns : 0;
       int c = ns ? lane % ns : 0, j = ns ? lane / ns + 1 : 0;
+#ifdef ART_PRIO_GRID0  // (dev A/B) the grid pass, dense VALU work, at the stage slots' priority
+      if (outlier) __builtin_amdgcn_s_setprio(2);
+      else __builtin_amdgcn_s_setprio(0);
+#endif
 #pragma unroll 1
       for (int w0 = 0; w0 < total; w0 += 64) {
         ART_PC(1)
@@ -920,6 +930,10 @@ __global__ __launch_bounds__(BLOCK, WPS) void propagate_kernel(const KParams P_i
           j += 1;
         }
       }
+#ifdef ART_PRIO_GRID0
+      if (outlier) __builtin_amdgcn_s_setprio(3);
+      else __builtin_amdgcn_s_setprio(1);
+#endif
       wave_lds_sync();
     }
 
@@ -2443,6 +2457,9 @@ __global__ __launch_bounds__(256, WPS) void sample_kernel(const KParams P, const
       // nonzero-ness of the next scan), so it keeps the value it had (round 3: until then
       // every certified lane evaluated its last point, 1 item per lane per step)
       const int totU = nU * nper, tot = totU;
+#ifdef ART_SAMPLER_PRIO  // (dev A/B) the dense grid pass at the low priority, the rest of a step at the high one
+      __builtin_amdgcn_s_setprio(0);
+#endif
       #pragma unroll 1
       for (int w0 = 0; w0 < tot; w0 += 64) {
         const int t = w0 + lane;
@@ -2462,6 +2479,9 @@ __global__ __launch_bounds__(256, WPS) void sample_kernel(const KParams P, const
           atomicOr(&snz[wb + src], (v != 0.0 ? 1u : 0u) << j);
         }
       }
+#ifdef ART_SAMPLER_PRIO
+      __builtin_amdgcn_s_setprio(1);
+#endif
       wave_lds_sync();
       // this lane's sign changes in (point j-1, point j]: signbits differ, both values nonzero
       unsigned br = 0u;

@@ -23,6 +23,8 @@ for name, kw in (("flat", dict(theta_m=0.2, mass_a=1e-5, flat=True)), ("gr", dic
     if only and name != only:
         continue
     eng = Engine(A.Params(**kw))
+    if "ART_AB_DONATE" in os.environ:  # tail donation lanes (default: the library's, by geometry)
+        eng.set_tail_donation(int(os.environ["ART_AB_DONATE"]))
     inp = eng.forward_roots(n, seed=1769)
     out = eng.alloc_out(n)
     ms = []
@@ -32,6 +34,7 @@ for name, kw in (("flat", dict(theta_m=0.2, mass_a=1e-5, flat=True)), ("gr", dic
     ms[-1] = min(ms[1:])
     st = A.raytracer.last_stats()
     att = (out["n_accept"] + out["n_reject"]).max().item()
-    print(json.dumps({"lib": os.environ.get("ART_LIB", "default"), "config": name, "kernel_ms": ms[-1],
+    print(json.dumps({"lib": os.environ.get("ART_LIB", "default"), "config": name, "n": n, "kernel_ms": ms[-1],
+                      "donate": os.environ.get("ART_AB_DONATE", "default"),
                       "accepted": st["accepted"], "scan_evals": st["scan_evals"], "interp_evals": st["interp_evals"],
                       "max_attempts": att, "ray_steps_per_s": st["accepted"] / ms[-1] * 1e3}), flush=True)
