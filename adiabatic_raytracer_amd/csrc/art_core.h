@@ -31,14 +31,13 @@
 #define ART_FP_FAST
 #endif
 
-// Three-operand FMA Horner steps in exp_fma and a one-instruction radius clamp (ART_EXP_ASM,
-// on unless ART_NO_EXP_ASM): the backend otherwise keeps the polynomial's coefficients in
-// VGPRs and copies one into the accumulator before every two-address v_fmac_f64 (a v_mov_b64 per
-// step). Measured on the 1e7 flat batch (profiles/r04b_ab.txt): 84.34 -> 83.37 ms. The same
-// code runs in every kernel, so a ray's arithmetic still does not depend on which one ran it.
-#if !defined(ART_NO_EXP_ASM) && !defined(ART_EXP_ASM)
-#define ART_EXP_ASM
-#endif
+// ART_EXP_ASM (off by default): three-operand FMA Horner steps in exp_fma and a
+// one-instruction radius clamp in inline asm. The backend otherwise keeps the polynomial's
+// coefficients in VGPRs and copies one into the accumulator before every two-address
+// v_fmac_f64. 1e7 flat rays: 84.34 -> 83.37 ms (profiles/r04b_ab.txt), but (1) the tail kernel
+// and the persistent integrator then no longer agree bit for bit (tests/test_edges.py,
+// test_gpu_tail_donation.py, profiles/r04d_bitexact.log) and (2) the streamed instantiation's
+// register allocation gets worse (100.8 -> 117.6 ms, profiles/r04d_stream_ab.jsonl). Not kept.
 
 namespace art {
 

@@ -695,6 +695,10 @@ __global__ __launch_bounds__(BLOCK, WPS) void propagate_kernel(const KParams P_i
     for (int i = 0; i < 7; ++i) kA[i] = 0.0;  // read (times a zero coefficient) before its first store
 #pragma unroll SUNROLL
     for (int s = 0; s < NSLOT; ++s) {
+#ifdef ART_PRIO_GLUE  // (dev A/B) the stage combination's LDS reads at the high priority
+      if (outlier) __builtin_amdgcn_s_setprio(3);
+      else __builtin_amdgcn_s_setprio(1);
+#endif
       const SlotRow R = T.row[s];
       const double cf = R.cf, cA = R.cA;
       double acc[7];
@@ -720,6 +724,10 @@ __global__ __launch_bounds__(BLOCK, WPS) void propagate_kernel(const KParams P_i
       for (int i = 0; i < 7; ++i) y[i] = u[i] + hs * acc[i];
       const double ty = tau + R.ct * hs;
       ART_SMARK(8)
+#ifdef ART_PRIO_GLUE
+      if (outlier) __builtin_amdgcn_s_setprio(2);
+      else __builtin_amdgcn_s_setprio(0);
+#endif
       // Every lane evaluates the photon RHS -- idle lanes (a draining wave) on stale state,
       // whose results nothing reads -- so the slot has no divergent control flow. Axion
       // segments (the tree driver's batches) take a wave-uniform detour and a select.
@@ -756,8 +764,9 @@ __global__ __launch_bounds__(BLOCK, WPS) void propagate_kernel(const KParams P_i
     // its instructions issue as soon as they are ready and the slots fill the gaps, instead of
     // the older wave's slots taking every issue cycle while this wave's chain waits behind
     // them (the arbiter goes by priority, then age). The priority drops back to the slots' level
-    // at the top of the next iteration. 1e7 flat rays: 84.34 -> 82.53 ms, with the exp Horner
-    // 81.40 (profiles/r04b_ab.txt). ART_NO_PRIO_PHASE switches it off (A/B).
+    // at the top of the next iteration. 1e7 flat rays: 84.34 -> 82.53 ms (profiles/r04b_ab.txt,
+    // 3 interleaved runs each); the grid pass at the slots' priority instead: 81.69 against
+    // 81.42 (profiles/r04c_ab_grid_prio.txt). ART_NO_PRIO_PHASE switches it off (A/B).
     if (outlier) __builtin_amdgcn_s_setprio(3);
     else __builtin_amdgcn_s_setprio(1);
 #endif
@@ -2457,9 +2466,9 @@ __global__ __launch_bounds__(256, WPS) void sample_kernel(const KParams P, const
       // nonzero-ness of the next scan), so it keeps the value it had (round 3: until then
       // every certified lane evaluated its last point, 1 item per lane per step)
       const int totU = nU * nper, tot = totU;
-#ifdef ART_SAMPLER_PRIO  // (dev A/B) the dense grid pass at the low priority, the rest of a step at the high one
-      __builtin_amdgcn_s_setprio(0);
-#endif
+#ifndef ART_NO_SAMPLER_PRIO  // the dense grid pass at the low issue priority, the rest of a step (certificate,
+      __builtin_amdgcn_s_setprio(0);  // brackets: short dependent chains) at the high one: 118.5 -> 117.1 ms
+#endif                                // per 1e7 samples (profiles/r04c_sampler_prio.jsonl)
       #pragma unroll 1
       for (int w0 = 0; w0 < tot; w0 += 64) {
         const int t = w0 + lane;
@@ -2479,7 +2488,7 @@ __global__ __launch_bounds__(256, WPS) void sample_kernel(const KParams P, const
           atomicOr(&snz[wb + src], (v != 0.0 ? 1u : 0u) << j);
         }
       }
-#ifdef ART_SAMPLER_PRIO
+#ifndef ART_NO_SAMPLER_PRIO
       __builtin_amdgcn_s_setprio(1);
 #endif
       wave_lds_sync();
