@@ -433,8 +433,8 @@ int scratch_layout(DeviceCtx* c, int64_t n, int cap, int32_t donate, ScratchLayo
     L->ncont = std::min(nd, (size_t)ncu * 32 * (size_t)donate);
   }
   // the second level (the packed continuation's own donations, resumed by the tail kernel):
-  // never more than the first level's
-  L->contb = 2 * L->ncont * art::CONT_REC * sizeof(double);
+  // never more than the first level's; then as many graduation records (SegOut::grad)
+  L->contb = (small_tail ? 2 : 3) * L->ncont * art::CONT_REC * sizeof(double);
   return ART_OK;
 }
 
@@ -489,6 +489,15 @@ int propagate_device_impl(const art_params* p, int64_t n, const double* x0, cons
     so.cont2 = so.cont + ncont * art::CONT_REC;
     so.cont2_count = words + 18;
     so.cont2_queue = words + 19;
+    if (!small_tail && tr.ntimes == 0 && p->integrator == ART_VERN6) {
+      // graduation of a pass's outlier rays to the tail kernel (ART_GRADUATE attempts, default
+      // 1024 -- about 12x the mean GR ray, never reached by a flat one; 0 = off)
+      so.grad = so.cont2 + ncont * art::CONT_REC;
+      so.grad_count = words + 20;
+      so.grad_queue = words + 21;
+      so.grad_cap = (int32_t)std::min(ncont, (size_t)INT32_MAX);
+      so.graduate = std::max(0, env_int("ART_GRADUATE", 1024));
+    }
     so.donate = donate;
     so.small_tail = small_tail ? 1 : 0;
   }

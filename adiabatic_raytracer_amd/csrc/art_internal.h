@@ -69,6 +69,14 @@ struct SegOut {
   // tail_kernel, one wave per ray (pack_fresh_kernel writes their CONT_REC records to cont),
   // instead of one lane per ray of the persistent integrator
   int32_t small_tail;
+  // Graduation (DON = 1 launches with tail_kernel): a ray that has taken `graduate` step
+  // attempts leaves its lane for the tail kernel at its next step boundary -- one wave per ray
+  // from then on -- without waiting for its wave to drain: CONT_REC records in grad[0, grad_cap)
+  // (count in *grad_count, which may pass grad_cap: a ray that finds no slot stays where it is),
+  // taken by tail_kernel ahead of the drained waves' records. 0 = off.
+  double* grad;
+  unsigned long long *grad_count, *grad_queue;
+  int32_t grad_cap, graduate;
 };
 constexpr unsigned long long STREAM_WAIT_TICKS = 200000000ull;  // 2 s at 100 MHz
 constexpr int END_REC = 16;

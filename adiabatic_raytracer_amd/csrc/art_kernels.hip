@@ -453,6 +453,23 @@ __device__ inline void stream_count(const SegOut& out, int64_t n, int p, unsigne
   }
 }
 
+// One ray's complete integrator state as a CONT_REC record (tail donation, graduation):
+// [u (7) | f (7) | τ, dt, qpow, cprev, bstart, erg | int4 {ray, n_acc, n_rej, ncross} |
+//  int4 {iter, sprev, flags, save_k}]
+__device__ inline void write_cont_rec(double* rec, const double* u, const double* f, double tau, double dt, double qpow,
+                                      double cprev, double bstart, double erg, int ray, int n_acc, int n_rej,
+                                      int ncross, int iter, int sprev, bool photon, bool cprev_ok, bool just_evented,
+                                      int save_k) {
+  double2* rq = reinterpret_cast<double2*>(rec);
+  const double v[20] = {u[0], u[1], u[2], u[3], u[4], u[5], u[6], f[0], f[1], f[2],
+                        f[3], f[4], f[5], f[6], tau, dt, qpow, cprev, bstart, erg};
+#pragma unroll
+  for (int i = 0; i < 10; ++i) rq[i] = make_double2(v[2 * i], v[2 * i + 1]);
+  int4* ri = reinterpret_cast<int4*>(rq + 10);
+  ri[0] = make_int4(ray, n_acc, n_rej, ncross);
+  ri[1] = make_int4(iter, sprev, (photon ? 1 : 0) | (cprev_ok ? 2 : 0) | (just_evented ? 4 : 0), save_k);
+}
+
 template <int GEOM>
 __device__ inline KParams specialize(const KParams& P) {
   KParams Q = P;
@@ -1369,6 +1386,27 @@ __global__ __launch_bounds__(BLOCK, WPS) void propagate_kernel(const KParams P_i
       }
     }
     ART_TMARK(0)  // saveat, reload, events, finish and the output stores (+ refill)
+    // graduation (SegOut::graduate): a ray past `graduate` attempts, at a step boundary, leaves
+    // for the tail kernel now instead of running on as one lane of this wave until the wave
+    // drains; its lane takes the next ray. The record is the donation record, so the ray's
+    // arithmetic does not change.
+    if (DON == 1 && out.graduate > 0) {
+      const bool g = mode == M_STEP && iter >= out.graduate;
+      const unsigned long long gm = __ballot(g);
+      if (gm != 0ull) {
+        const int leader = __ffsll((long long)gm) - 1;
+        unsigned long long base = 0;
+        if (lane == leader) base = atomicAdd(out.grad_count, (unsigned long long)__popcll(gm));
+        base = __shfl(base, leader);
+        const int64_t slot = (int64_t)base + __popcll(gm & ((1ull << lane) - 1ull));
+        if (g && slot < (int64_t)out.grad_cap) {  // (no slot left: the ray stays)
+          write_cont_rec(out.grad + slot * CONT_REC, u, f, tau, dt, qpow, cprev, bstart, erg, ray, n_acc, n_rej,
+                         ncross, iter, sprev, photon, cprev_ok, just_evented, save_k);
+          ray = -1;
+          mode = M_IDLE;
+        }
+      }
+    }
     // tail donation (SegOut::donate): the drained wave's last few rays, all at a step
     // boundary, leave for the continuation launch and the wave retires
     if (DON == 1 && exhausted && out.donate > 0) {
@@ -1380,14 +1418,8 @@ __global__ __launch_bounds__(BLOCK, WPS) void propagate_kernel(const KParams P_i
         base = __shfl(base, leader);
         if (mode != M_IDLE) {
           const int64_t slot = (int64_t)base + __popcll(live & ((1ull << lane) - 1ull));
-          double2* rq = reinterpret_cast<double2*>(out.cont + slot * CONT_REC);
-          const double v[20] = {u[0], u[1], u[2], u[3], u[4], u[5], u[6], f[0], f[1], f[2],
-                                f[3], f[4], f[5], f[6], tau, dt, qpow, cprev, bstart, erg};
-#pragma unroll
-          for (int i = 0; i < 10; ++i) rq[i] = make_double2(v[2 * i], v[2 * i + 1]);
-          int4* ri = reinterpret_cast<int4*>(rq + 10);
-          ri[0] = make_int4(ray, n_acc, n_rej, ncross);
-          ri[1] = make_int4(iter, sprev, (photon ? 1 : 0) | (cprev_ok ? 2 : 0) | (just_evented ? 4 : 0), save_k);
+          write_cont_rec(out.cont + slot * CONT_REC, u, f, tau, dt, qpow, cprev, bstart, erg, ray, n_acc, n_rej,
+                         ncross, iter, sprev, photon, cprev_ok, just_evented, save_k);
           ray = -1;
           mode = M_IDLE;
         }
@@ -1524,19 +1556,35 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
   const double my_ct = c_tail_ct[lane & 7];
   const double my_th = double(lane + 1) / double(npts - 1);  // grid point lane + 1 (Julia's range(0, 1, length = npts))
   unsigned s_att = 0, s_acc = 0, s_root = 0, s_scan = 0, s_interp = 0, s_cert = 0;
+  // the graduated rays (SegOut::grad, the pass's outliers) first, then the drained waves' records
+  const int64_t ng = out.grad ? ((int64_t)*out.grad_count < (int64_t)out.grad_cap ? (int64_t)*out.grad_count
+                                                                                   : (int64_t)out.grad_cap)
+                              : 0;
+  bool grads = ng > 0;
   while (true) {
-    unsigned long long ix = 0;
-    if (lane == 0) ix = atomicAdd(out.cont_queue, 1ull);
-    const int64_t rec = (int64_t)__builtin_amdgcn_readfirstlane((unsigned)ix) |
-                        ((int64_t)__builtin_amdgcn_readfirstlane((unsigned)(ix >> 32)) << 32);
-    if (rec >= nq) break;
+    const double* src = nullptr;
+    while (src == nullptr) {
+      unsigned long long* q = grads ? out.grad_queue : out.cont_queue;
+      unsigned long long ix = 0;
+      if (lane == 0) ix = atomicAdd(q, 1ull);
+      const int64_t rec = (int64_t)__builtin_amdgcn_readfirstlane((unsigned)ix) |
+                          ((int64_t)__builtin_amdgcn_readfirstlane((unsigned)(ix >> 32)) << 32);
+      if (grads) {
+        if (rec < ng) src = out.grad + rec * CONT_REC;
+        else grads = false;
+      } else {
+        if (rec >= nq) break;
+        src = out.cont + rec * CONT_REC;
+      }
+    }
+    if (src == nullptr) break;
     // ---- the donated ray's complete state (the bulk kernel's CONT_REC) ----
     double u[7], f[7];
     double tau, dt, qpow, cprev, bstart, erg;
     int ray, n_acc, n_rej, ncross, iter, sprev;
     bool photon, cprev_ok, just_evented;
     {
-      const double2* rq = reinterpret_cast<const double2*>(out.cont + rec * CONT_REC);
+      const double2* rq = reinterpret_cast<const double2*>(src);
       double v[20];
 #pragma unroll
       for (int i = 0; i < 10; ++i) {
@@ -2812,7 +2860,7 @@ static bool w1_builds() {
   return on;
 }
 
-hipError_t launch_propagate(const KParams& P, int64_t n, const SegIn& in, const SegOut& out, int32_t max_crossings,
+hipError_t launch_propagate(const KParams& P, int64_t n, const SegIn& in, const SegOut& out_arg, int32_t max_crossings,
                             unsigned long long* queue, unsigned long long* stats, hipStream_t s, int* grid_out,
                             hipEvent_t ev0, hipEvent_t ev1, hipStream_t fs) {
   const int64_t gr = (n + 255) / 256;
@@ -2838,6 +2886,13 @@ hipError_t launch_propagate(const KParams& P, int64_t n, const SegIn& in, const 
   const bool flat = P.rs_eff == 0.0 && !(P.bndry_lyr > 0.0) && !P.isotropic;
   const bool sch = P.rs_eff > 0.0 && !(P.bndry_lyr > 0.0) && !P.isotropic;
   const bool rk4 = P.integrator == ART_RK4;
+  // graduation (SegOut::grad) only where the tail kernel runs after the continuation to resume
+  // the graduated rays
+  SegOut out = out_arg;
+  if (out.small_tail || !(out.donate > 0 && tail_rays() != 0 && !rk4 && out.ntimes < 2 && out.cont2)) {
+    out.grad = nullptr;
+    out.graduate = 0;
+  }
   if (out.small_tail) {  // a small Vern6 batch: every ray on a wave of its own (tail_kernel)
     int dev = 0, ncu = 0;
     (void)hipGetDevice(&dev);
@@ -2915,7 +2970,7 @@ hipError_t launch_propagate(const KParams& P, int64_t n, const SegIn& in, const 
       (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
       // one wave per ray, at most one per SIMD of the device (ART_TAIL=k: k waves); more
       // second-level rays queue behind them
-      const int64_t maxc2 = (int64_t)cgrid * (BLOCK / 64) * oc.donate;
+      const int64_t maxc2 = (int64_t)cgrid * (BLOCK / 64) * oc.donate + (out.grad ? (int64_t)out.grad_cap : 0);
       const int waves = tail_rays() == 1 ? ncu * 4 : tail_rays();
       const int tgrid = (int)(maxc2 < waves ? maxc2 : waves);
       SegOut ot = out;

@@ -51,6 +51,30 @@ def test_tail_donation_is_bit_exact(cfg, tail, monkeypatch):
             assert sref[k] == sgot[k], (cfg, lanes, k, sref[k], sgot[k])
 
 
+@pytest.mark.parametrize("cfg", ["flat", "gr", "gr_oblique"])
+@pytest.mark.parametrize("graduate", ["1", "64", "1024"])
+def test_graduation_is_bit_exact(cfg, graduate, monkeypatch):
+    """ART_GRADUATE=k: a ray still stepping after k attempts leaves its wave for a wave of its own
+    (tail_kernel) without waiting for the wave to drain. k=1 graduates nearly every ray (and
+    overflows the graduation records, so the rest stay in place), k=64 a large share, 1024 (the
+    default) the outliers. Outputs and counters equal the undonated run bit for bit."""
+    monkeypatch.setenv("ART_GRADUATE", graduate)
+    import adiabatic_raytracer_amd as A
+    from adiabatic_raytracer_amd import Engine
+    eng = Engine(A.Params(**CONFIGS[cfg]))
+    inp = eng.forward_roots(N, seed=1769)
+    ref, sref = _run(eng, inp, 0)
+    has = ref["n_cross"] > 0
+    got, sgot = _run(eng, inp, 16)
+    for k in ref:
+        a, b = ref[k], got[k]
+        if k.startswith("xc_"):
+            a, b = a.reshape(-1, N)[:, has], b.reshape(-1, N)[:, has]
+        assert np.array_equal(a, b, equal_nan=True), (cfg, graduate, k)
+    for k in ("attempts", "accepted", "root_steps", "scan_evals", "rays", "cert_steps"):
+        assert sref[k] == sgot[k], (cfg, graduate, k, sref[k], sgot[k])
+
+
 def test_tail_donation_rejects_bad_lane_counts():
     import adiabatic_raytracer_amd as A
     from adiabatic_raytracer_amd import Engine
