@@ -911,7 +911,8 @@ int stream_setup(DeviceCtx* c, int reserve, int nsig) {
   // (reserve = 0, dev only: the three streams CU-masked with every CU, to time the masked queue itself)
   if (reserve != 0 && (reserve < 8 || reserve % 8 != 0 || reserve >= ncu / 2))
     return fail(ART_E_INVALID, "ART_HOST_RESERVE_CUS must be a multiple of 8 in [8, %s)", std::to_string(ncu / 2).c_str());
-  const int key = reserve * 2 + (env_int("ART_HOST_RESERVE_XCD", 0) != 0 ? 1 : 0);
+  const int key = (reserve * 2 + (env_int("ART_HOST_RESERVE_XCD", 0) != 0 ? 1 : 0)) * 1024 +
+                  env_int("ART_HOST_RESERVE_AT", ncu - reserve);
   if (!c->s_comp || c->reserve != key) {
     for (hipStream_t* st : {&c->s_comp, &c->s_in, &c->s_out})
       if (*st) {
@@ -926,7 +927,9 @@ int stream_setup(DeviceCtx* c, int reserve, int nsig) {
     const bool one_xcd = env_int("ART_HOST_RESERVE_XCD", 0) != 0;
     int taken = 0;
     for (int i = ncu - 1; i >= 0; --i) {
-      const bool res = one_xcd ? (taken < reserve && i % 8 == 7) : i >= ncu - reserve;
+      // (ART_HOST_RESERVE_AT=k, dev: the reserved CUs start at logical CU k instead of ncu - reserve)
+      const int at = env_int("ART_HOST_RESERVE_AT", ncu - reserve);
+      const bool res = one_xcd ? (taken < reserve && i % 8 == 7) : (i >= at && i < at + reserve);
       taken += res;
       (res ? mh : mc)[i / 32] |= 1u << (i % 32);
       if (reserve == 0) mh[i / 32] |= 1u << (i % 32);
@@ -1090,7 +1093,8 @@ int propagate_host_streamed(DeviceCtx* c, const art_params* p, int64_t n, const 
   so.abort_word = c->abort_dev;
   so.piece_shift = shift;
   HIP_OK(hipEventRecord(L->ev0, c->s_comp));
-  const int blocks = 2 * (ncu - reserve);  // persistent: 2 per CU of the integrator's mask
+  int blocks = 2 * (ncu - reserve);  // persistent: 2 per CU of the integrator's mask
+  if (const int b = env_int("ART_HOST_BLOCKS", 0)) blocks = std::max(1, b);  // (dev: grid A/B)
   HIP_OK(art::launch_integrator_streamed(K, n, in, so, max_crossings, words, words + 1, blocks, c->s_comp, &L->grid));
   HIP_OK(hipEventRecord(L->ev1, c->s_comp));
   HIP_OK(hipMemcpyAsync(L->host_stats, words + 1, sizeof(unsigned long long) * art::N_STATS, hipMemcpyDeviceToHost,
