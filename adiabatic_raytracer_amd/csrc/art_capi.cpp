@@ -83,6 +83,13 @@ struct DeviceCtx {
   unsigned long long** sig_dev = nullptr;
   unsigned int* abort_host = nullptr;
   unsigned int* abort_dev = nullptr;
+  // the maskless streamed pipeline (propagate_host_maskless): plain streams for the integrator
+  // and the two copy directions (the copies run on the DMA engines), a block of host memory the
+  // GPU reads and writes over PCIe -- [0] the ready counter, [8 + p] piece p's flag -- and the
+  // device array of the flags' addresses
+  hipStream_t m_comp = nullptr, m_up = nullptr, m_dn = nullptr, m_help = nullptr;
+  unsigned long long* hsig = nullptr;
+  unsigned long long* hsig_dev = nullptr;
 };
 std::vector<DeviceCtx> g_ctx;
 
@@ -284,8 +291,9 @@ void release_ctx(DeviceCtx& c) {
   for (hipEvent_t e : c.pev) (void)hipEventDestroy(e);
   for (hipStream_t s : c.pstreams)
     if (s && s != c.stream) (void)hipStreamDestroy(s);
-  for (hipStream_t s : {c.h2d, c.fin, c.s_comp, c.s_in, c.s_out})
+  for (hipStream_t s : {c.h2d, c.fin, c.s_comp, c.s_in, c.s_out, c.m_comp, c.m_up, c.m_dn, c.m_help})
     if (s) (void)hipStreamDestroy(s);
+  if (c.hsig) (void)hipHostFree(c.hsig);
   for (unsigned long long* w : c.sigs) (void)hipFree(w);
   if (c.sig_dev) (void)hipFree(c.sig_dev);
   if (c.abort_host) (void)hipHostFree(c.abort_host);
@@ -1200,6 +1208,353 @@ int propagate_host_streamed(DeviceCtx* c, const art_params* p, int64_t n, const 
   return finish_timing(c);
 }
 
+// art_propagate_host for large batches, streamed with no CU reserved (the default; SURVEY §8b,
+// the reference call site MainRunner.jl:179-190 hands over host arrays). ONE integrator launch
+// (propagate_kernel<..., DON = 3>) holds every CU for the whole batch; nothing else needs a CU
+// while it runs:
+//   * the host gathers piece k from the caller's arrays into pinned staging (copy pool) and
+//     copies it to HBM on the upload stream (DMA engines: tools/probe/copy_engine_probe.hip,
+//     profiles/r04k_probe_*.jsonl -- 64 MB copies finish at 56 GB/s under a kernel holding
+//     every CU); a host thread raises the ready counter (host memory) as each piece lands;
+//   * helper blocks of the same launch initialise 256-ray tiles whose inputs have landed
+//     (init_one, the init_kernel arithmetic) and flag their chunks; a wave that claims a
+//     chunk of 64 rays waits for its flag. Once every ray of a piece has finished, helpers
+//     finalize its tiles (finalize_one) into the piece's SoA blob in HBM, and the block that
+//     finalizes its last tile raises the piece's flag (host memory);
+//   * the host polls the flags, copies each finished blob to pinned memory (DMA engines) and
+//     scatters it into the caller's arrays.
+// Helper blocks (SegOut::helpers) do the init and finalize tiles while the rest integrate; the
+// blocks whose waves run out of rays join them (art_kernels.hip, s3_helper).
+// The CU-masked pipeline it replaces (propagate_host_streamed, ART_HOST_MODE=stream_masked) ran
+// the init and finalize kernels on 8 reserved CUs, which cost ~10% of the integrator
+// (profiles/r04g_stream_anatomy.jsonl). Per-ray results equal the single launch's bit for bit.
+int propagate_host_maskless(DeviceCtx* c, const art_params* p, int64_t n, const double* x0, const double* k0,
+                            const double* erg, const double* dw, const double* ln_t0, const int8_t* species,
+                            int32_t max_crossings, art_segment_out* out, art_crossing_buf* xc, const FluxArgs& fx) {
+  const int cap = (xc && xc->count) ? xc->capacity : 0;
+  const art::KParams K = kparams(*p);
+  int shift = 16;
+  while (((int64_t)1 << (shift + 1)) * 16 <= n) ++shift;  // 16..32 pieces (2^19 rays for 10^7)
+  if (const int e = env_int("ART_HOST_PIECE_SHIFT", 0)) shift = std::max(10, e);  // (tests: many small pieces)
+  while (((n + ((int64_t)1 << shift) - 1) >> shift) > 64) ++shift;  // 64 piece counters and flags
+  const int np = (int)((n + ((int64_t)1 << shift) - 1) >> shift);
+  constexpr int NFLAG = 64;
+  if (!c->m_comp) {
+    // the integrator's and the persistent helpers' streams each on a hardware queue of its own
+    // (a stream with a CU mask gets one; here the mask holds every CU): plain streams share the
+    // process's few queues (GPU_MAX_HW_QUEUES), and a stream queued behind a persistent kernel
+    // waits for that kernel to end -- the integrator behind the helpers never started
+    // (profiles/r04p_maskless_hwqueue.txt)
+    int ncu_all = 0;
+    HIP_OK(hipDeviceGetAttribute(&ncu_all, hipDeviceAttributeMultiprocessorCount, c->device));
+    std::vector<uint32_t> all((ncu_all + 31) / 32, 0u);
+    for (int i = 0; i < ncu_all; ++i) all[i / 32] |= 1u << (i % 32);
+    HIP_OK(hipExtStreamCreateWithCUMask(&c->m_comp, (uint32_t)all.size(), all.data()));
+    HIP_OK(hipExtStreamCreateWithCUMask(&c->m_help, (uint32_t)all.size(), all.data()));
+    HIP_OK(hipStreamCreateWithFlags(&c->m_up, hipStreamNonBlocking));
+    HIP_OK(hipStreamCreateWithFlags(&c->m_dn, hipStreamNonBlocking));
+  }
+  if (!c->hsig) {
+    // [0] ready | [8, 8 + 64) piece flags | [72] helper blocks started
+    HIP_OK(hipHostMalloc((void**)&c->hsig, sizeof(unsigned long long) * (16 + NFLAG), hipHostMallocCoherent | hipHostMallocMapped));
+    HIP_OK(hipHostGetDevicePointer((void**)&c->hsig_dev, c->hsig, 0));
+  }
+  if (!c->abort_host) {
+    HIP_OK(hipHostMalloc((void**)&c->abort_host, 64, hipHostMallocCoherent | hipHostMallocMapped));
+    HIP_OK(hipHostGetDevicePointer((void**)&c->abort_dev, c->abort_host, 0));
+  }
+  const size_t nd = (size_t)n;
+  auto up = [](size_t b) { return (b + 255) & ~size_t(255); };
+  const size_t in_bytes = nd * 9 * sizeof(double) + nd;  // x0 (3n) k0 (3n) erg dw lnt0 | species
+  // per-piece SoA output blobs, pinned and in HBM: the layout piece_blob (art_kernels.hip) computes
+  auto piece_lo = [&](int k) { return std::min((int64_t)k << shift, n); };
+  auto cnt_off = [&](int64_t m) { return up((size_t)m * 8 * sizeof(double) + (size_t)m * 3 * sizeof(int32_t)); };
+  auto xd_off = [&](int64_t m) { return cnt_off(m) + up((size_t)m * sizeof(int32_t)); };
+  auto out_bytes = [&](int64_t m) { return cap ? xd_off(m) + (size_t)cap * m * 9 * sizeof(double) : cnt_off(m); };
+  const size_t stride = up(out_bytes((int64_t)1 << shift));
+  // scratch: head [queue | stats (8) | init_next (16) fin_next (17) chunk misses (18) | finished rays per piece from
+  // word 32 | finalized tiles per piece from word 96] | chunk flags | u0 16n | rec 16n | xrec
+  const size_t nchunk = (nd + art::CHUNK - 1) / art::CHUNK;
+  const size_t head = 2048, ccb = up(nchunk * sizeof(unsigned)), u0b = nd * 16 * sizeof(double),
+               recb = nd * art::END_REC * sizeof(double);
+  const size_t xrb = (size_t)cap * nd * art::X_REC * sizeof(double);
+  void *pi, *po, *din, *dout, *dsc;
+  int rc;
+  if ((rc = pinned_get(c, 2, in_bytes, &pi)) || (rc = pinned_get(c, 3, stride * np, &po)) ||
+      (rc = pool_get(c, 20, in_bytes, &din)) || (rc = pool_get(c, 21, stride * np, &dout)) ||
+      (rc = pool_get(c, 22, head + ccb + u0b + recb + xrb, &dsc)))
+    return rc;
+  double* pin = (double*)pi;
+  double* di = (double*)din;
+  unsigned long long* words = (unsigned long long*)dsc;
+  unsigned* ccnt = (unsigned*)((char*)dsc + head);
+  double* u0 = (double*)((char*)dsc + head + ccb);
+  double* rec = (double*)((char*)dsc + head + ccb + u0b);
+  double* xrec = cap ? (double*)((char*)dsc + head + ccb + u0b + recb) : nullptr;
+  const art::SegIn in{di, di + 3 * nd, di + 6 * nd, di + 7 * nd, di + 8 * nd, (const int8_t*)(di + 9 * nd), u0};
+  // upload units: the first piece in four parts (the integrator starts on the first quarter),
+  // then one unit per piece
+  std::vector<int64_t> ulo;
+  for (int q = 0; q < 4; ++q) ulo.push_back(piece_lo(1) * q / 4 / art::CHUNK * art::CHUNK);
+  for (int k = 1; k <= np; ++k) ulo.push_back(piece_lo(k));
+  ulo.erase(std::unique(ulo.begin(), ulo.end()), ulo.end());
+  const int nu = (int)ulo.size() - 1;
+  while ((int64_t)c->pev.size() < nu + np + 2) {
+    hipEvent_t ev;
+    HIP_OK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    c->pev.push_back(ev);
+  }
+  hipEvent_t* ev_up = c->pev.data();
+  hipEvent_t* ev_dn = c->pev.data() + nu;
+  const bool trace = env_int("ART_HOST_TRACE", 0) != 0;
+  auto clk = [] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
+  const double t_start = clk();
+  unsigned long long* hready = c->hsig;
+  unsigned long long* hflag = c->hsig + 8;
+  __atomic_store_n(hready, 0ull, __ATOMIC_RELEASE);
+  for (int k = 0; k <= NFLAG; ++k) __atomic_store_n(hflag + k, 0ull, __ATOMIC_RELEASE);  // (+ the started count)
+  __atomic_store_n(c->abort_host, 0u, __ATOMIC_RELEASE);
+  HIP_OK(hipMemsetAsync(words, 0, head + ccb, c->m_comp));
+  double* hist_dev = nullptr;
+  if (fx.nbins) {
+    if ((rc = pool_get(c, 23, 2 * (size_t)fx.nbins * sizeof(double), (void**)&hist_dev))) return rc;
+    HIP_OK(hipMemsetAsync(hist_dev, 0, 2 * (size_t)fx.nbins * sizeof(double), c->m_comp));
+  }
+  // the integrator, first: its waves wait for the first piece
+  LaunchRec* L;
+  if ((rc = take_slot(c, &L))) return rc;
+  art::SegOut so{};
+  so.rec = rec;
+  so.cap = cap;
+  so.xrec = xrec;
+  so.xcount = cap ? (int32_t*)((char*)dout + cnt_off(piece_lo(1) - piece_lo(0))) : nullptr;  // (tested for null only)
+  so.piece_cnt = words + 32;
+  so.abort_word = c->abort_dev;
+  so.piece_shift = shift;
+  so.host_ready = c->hsig_dev;
+  so.host_flags = c->hsig_dev + 8;
+  so.init_next = words + 16;
+  so.fin_next = words + 17;
+  so.piece_fin = words + 96;
+  so.chunk_ready = ccnt;
+  so.blob = (char*)dout;
+  so.blob_stride = (int64_t)stride;
+  int ncu = 0;
+  HIP_OK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device));
+  const int slots = std::max(2, env_int("ART_HOST_BLOCKS", 2 * ncu));  // block slots: 2 per CU
+  // helper blocks beside the integrator (ART_HOST_HELPERS, default 16): launched first, and the
+  // integrator only once every one of them is resident, so it cannot take their slots
+  const int helpers = std::min(slots - 1, std::max(1, env_int("ART_HOST_HELPERS", 8)));
+  so.helpers = helpers;
+  hipEvent_t ev_zero = c->pev[nu + np];  // (the helpers start on zeroed counters)
+  HIP_OK(hipEventRecord(ev_zero, c->m_comp));
+  HIP_OK(hipStreamWaitEvent(c->m_help, ev_zero, 0));
+  HIP_OK(art::launch_helpers(K, n, in, so, helpers, -1, 1, words + 1, c->m_help));
+  {
+    const double tw = clk();
+    while (__atomic_load_n(hflag + NFLAG, __ATOMIC_ACQUIRE) < (unsigned long long)helpers) {
+      if (clk() - tw > 5000.0) {  // (never seen: the device is shared or wedged) -- let them go, fall back
+        __atomic_store_n(c->abort_host, 1u, __ATOMIC_RELEASE);
+        (void)hipStreamSynchronize(c->m_help);
+        std::fprintf(stderr, "[art] maskless streamed pipeline: helper blocks did not start; running the batch again\n");
+        return STREAM_FALLBACK;
+      }
+      std::this_thread::sleep_for(std::chrono::microseconds(5));
+    }
+  }
+  // every block slot initialises the first piece, then the integrator, then every slot helps
+  // finalize what is left
+  // the first upload unit by every block slot, then the helpers keep ahead (ART_HOST_INIT_RAYS:
+  // dev, another amount)
+  const int64_t first = std::min(n, (int64_t)std::max(1, env_int("ART_HOST_INIT_RAYS", (int)ulo[1])));
+  if (env_int("ART_HOST_INITPASS", 1))  // (dev: 0 leaves the first piece to the helpers)
+    HIP_OK(art::launch_helpers(K, n, in, so, slots - helpers, first, 0, words + 1, c->m_comp));
+  HIP_OK(hipEventRecord(L->ev0, c->m_comp));
+  HIP_OK(art::launch_integrator_streamed(K, n, in, so, max_crossings, words, words + 1, slots - helpers, c->m_comp,
+                                         &L->grid, true));
+  HIP_OK(hipEventRecord(L->ev1, c->m_comp));
+  HIP_OK(art::launch_helpers(K, n, in, so, slots, -1, 0, words + 1, c->m_comp));
+  hipEvent_t ev_help = c->pev[nu + np + 1];  // (the persistent helpers' init counts, in the statistics)
+  HIP_OK(hipEventRecord(ev_help, c->m_help));
+  HIP_OK(hipStreamWaitEvent(c->m_comp, ev_help, 0));
+  HIP_OK(hipMemcpyAsync(L->host_stats, words + 1, sizeof(unsigned long long) * art::N_STATS, hipMemcpyDeviceToHost,
+                        c->m_comp));
+  HIP_OK(hipEventRecord(L->done, c->m_comp));
+  L->pending = true;
+  c->last = c->next;
+  c->next = (c->next + 1) % RING;
+  c->launches += 1;
+  // a host thread raises the ready counter as each piece's copies land
+  std::atomic<int> recorded{0};
+  std::atomic<bool> stop{false};
+  std::atomic<int> ready_err{0};
+  std::thread readier([&] {
+    for (int u = 0; u < nu && !stop.load(); ++u) {
+      while (recorded.load(std::memory_order_acquire) <= u && !stop.load()) std::this_thread::sleep_for(std::chrono::microseconds(5));
+      if (stop.load()) break;
+      if (hipEventSynchronize(ev_up[u]) != hipSuccess) {
+        ready_err = 1;
+        break;
+      }
+      __atomic_store_n(hready, (unsigned long long)ulo[u + 1], __ATOMIC_RELEASE);
+      if (trace) std::fprintf(stderr, "[art-host] t=%.2f unit %d ready\n", clk() - t_start, u);
+    }
+  });
+  using Seg = CopyPool::Seg;
+  int dk = 0, sk = 0;  // pieces whose download is queued / scattered
+  auto scatter = [&](int k) {
+    const int64_t lo = piece_lo(k), m = piece_lo(k + 1) - lo;
+    const char* bo = (const char*)po + stride * k;
+    const double* d = (const double*)bo;
+    const int32_t* i32 = (const int32_t*)(d + 8 * m);
+    std::vector<Seg> g;
+    for (int q = 0; q < 3; ++q) {
+      g.push_back({out->x_end + q * n + lo, d + q * m, m * sizeof(double)});
+      g.push_back({out->k_end + q * n + lo, d + (3 + q) * m, m * sizeof(double)});
+    }
+    g.push_back({out->u7_end + lo, d + 6 * m, m * sizeof(double)});
+    g.push_back({out->tau_end + lo, d + 7 * m, m * sizeof(double)});
+    g.push_back({out->status + lo, i32, m * sizeof(int32_t)});
+    g.push_back({out->n_accept + lo, i32 + m, m * sizeof(int32_t)});
+    g.push_back({out->n_reject + lo, i32 + 2 * m, m * sizeof(int32_t)});
+    if (cap) {
+      g.push_back({xc->count + lo, bo + cnt_off(m), m * sizeof(int32_t)});
+      const double* x = (const double*)(bo + xd_off(m));
+      for (int r = 0; r < 3 * cap; ++r) {
+        g.push_back({xc->pos + r * n + lo, x + r * m, m * sizeof(double)});
+        g.push_back({xc->k + r * n + lo, x + (3 * cap + r) * m, m * sizeof(double)});
+      }
+      for (int r = 0; r < cap; ++r) {
+        g.push_back({xc->t + r * n + lo, x + (6 * cap + r) * m, m * sizeof(double)});
+        g.push_back({xc->dw + r * n + lo, x + (7 * cap + r) * m, m * sizeof(double)});
+        g.push_back({xc->p_nonad + r * n + lo, x + (8 * cap + r) * m, m * sizeof(double)});
+      }
+    }
+    copy_pool().run(g);
+  };
+  // downloads of the finished pieces, in order; scatters of the landed ones
+  auto progress = [&]() -> int {
+    int moved = 0;
+    while (dk < np && __atomic_load_n(hflag + dk, __ATOMIC_ACQUIRE) != 0ull) {
+      const int64_t m = piece_lo(dk + 1) - piece_lo(dk);
+      if (hipMemcpyAsync((char*)po + stride * dk, (char*)dout + stride * dk, out_bytes(m), hipMemcpyDeviceToHost,
+                         c->m_dn) != hipSuccess ||
+          hipEventRecord(ev_dn[dk], c->m_dn) != hipSuccess)
+        return -1;
+      if (trace) std::fprintf(stderr, "[art-host] t=%.2f piece %d done\n", clk() - t_start, dk);
+      ++dk;
+      ++moved;
+    }
+    while (sk < dk) {
+      const hipError_t q = hipEventQuery(ev_dn[sk]);
+      if (q == hipErrorNotReady) break;
+      if (q != hipSuccess) return -1;
+      const double t0 = clk();
+      scatter(sk);
+      if (trace) std::fprintf(stderr, "[art-host] t=%.2f piece %d scattered (%.2f ms)\n", t0 - t_start, sk, clk() - t0);
+      ++sk;
+      ++moved;
+    }
+    return moved;
+  };
+  int perr = 0;
+  for (int u = 0; u < nu && !perr; ++u) {
+    const int64_t lo = ulo[u], m = ulo[u + 1] - lo;
+    const double* src[9] = {x0, x0 + n, x0 + 2 * n, k0, k0 + n, k0 + 2 * n, erg, dw, ln_t0};
+    std::vector<Seg> g;
+    for (int r = 0; r < 9; ++r) g.push_back({pin + r * nd + lo, src[r] + lo, (size_t)m * sizeof(double)});
+    g.push_back({(int8_t*)(pin + 9 * nd) + lo, species + lo, (size_t)m});
+    const double tg0 = clk();
+    copy_pool().run(g);
+    for (int r = 0; r < 9 && !perr; ++r)
+      perr |= hipMemcpyAsync(di + r * nd + lo, pin + r * nd + lo, (size_t)m * sizeof(double), hipMemcpyHostToDevice,
+                             c->m_up) != hipSuccess;
+    perr |= hipMemcpyAsync((int8_t*)(di + 9 * nd) + lo, (int8_t*)(pin + 9 * nd) + lo, (size_t)m, hipMemcpyHostToDevice,
+                           c->m_up) != hipSuccess;
+    perr |= hipEventRecord(ev_up[u], c->m_up) != hipSuccess;
+    recorded.store(u + 1, std::memory_order_release);
+    if (trace) std::fprintf(stderr, "[art-host] t=%.2f unit %d gathered in %.2f ms\n", tg0 - t_start, u, clk() - tg0);
+    if (!perr && progress() < 0) perr = 1;
+  }
+  const double limit_ms = (double)env_int("ART_HOST_STREAM_TIMEOUT_MS", 30000);
+  double t_last = clk(), t_peek = clk();
+  bool gave_up = perr != 0;
+  unsigned long long* peek = nullptr;  // (trace) the device counters, copied out every 100 ms
+  if (trace) HIP_OK(hipHostMalloc((void**)&peek, 160 * sizeof(unsigned long long), hipHostMallocDefault));
+  while (!gave_up && sk < np) {
+    if (trace && clk() - t_peek > (double)env_int("ART_HOST_PEEK_MS", 100)) {
+      t_peek = clk();
+      if (hipMemcpyAsync(peek, words, 160 * sizeof(unsigned long long), hipMemcpyDeviceToHost, c->m_dn) == hipSuccess &&
+          hipStreamSynchronize(c->m_dn) == hipSuccess) {
+        unsigned long long fin = 0, tiles = 0;
+        for (int k = 0; k < np; ++k) {
+          fin += peek[32 + k];
+          tiles += peek[96 + k];
+        }
+        std::fprintf(stderr, "[art-host] t=%.1f queue %llu init_next %llu fin_next %llu misses %llu finished %llu tiles %llu flags:",
+                     clk() - t_start, peek[0], peek[16], peek[17], peek[18], fin, tiles);
+        for (int k = 0; k < np; ++k) std::fprintf(stderr, "%llu", hflag[k]);
+        std::fprintf(stderr, " ready %llu started %llu abort %u init-pass %s integrator %s\n", *hready, hflag[NFLAG],
+                     *c->abort_host, hipEventQuery(L->ev0) == hipSuccess ? "done" : "running",
+                     hipEventQuery(L->ev1) == hipSuccess ? "done" : "running");
+      }
+    }
+    const int mv = progress();
+    if (mv < 0 || ready_err.load()) {
+      gave_up = true;
+      break;
+    }
+    if (mv > 0) {
+      t_last = clk();
+      continue;
+    }
+    if (__atomic_load_n(c->abort_host, __ATOMIC_ACQUIRE) != 0u || clk() - t_last > limit_ms) {
+      gave_up = true;
+      break;
+    }
+    std::this_thread::sleep_for(std::chrono::microseconds(20));
+  }
+  stop = true;
+  if (peek) (void)hipHostFree(peek);
+  if (gave_up) {
+    // let the integrator run out (waves waiting for inputs stop on their own bound), then leave
+    // the batch to another path
+    __atomic_store_n(c->abort_host, 1u, __ATOMIC_RELEASE);
+    __atomic_store_n(hready, (unsigned long long)n, __ATOMIC_RELEASE);
+    readier.join();
+    (void)hipStreamSynchronize(c->m_up);
+    (void)hipStreamSynchronize(c->m_comp);
+    (void)hipStreamSynchronize(c->m_help);
+    (void)hipStreamSynchronize(c->m_dn);
+    (void)hipGetLastError();
+    if (trace) {  // the device counters at the give-up
+      std::vector<unsigned long long> w(160);
+      if (hipMemcpy(w.data(), words, w.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost) == hipSuccess) {
+        std::fprintf(stderr, "[art-host] queue %llu init_next %llu fin_next %llu\n", w[0], w[16], w[17]);
+        for (int k = 0; k < np; ++k)
+          std::fprintf(stderr, "[art-host] piece %d finished %llu finalized tiles %llu flag %llu\n", k, w[32 + k], w[96 + k],
+                       hflag[k]);
+      }
+    }
+    std::fprintf(stderr, "[art] maskless streamed pipeline gave up at piece %d of %d (abort=%u); running the batch again\n",
+                 sk, np, *c->abort_host);
+    return STREAM_FALLBACK;
+  }
+  readier.join();
+  if (trace) std::fprintf(stderr, "[art-host] maskless total %.2f ms (%d pieces of 2^%d)\n", clk() - t_start, np, shift);
+  if (fx.nbins) {  // the flux of every piece's blob, once the integrator is done (a few hundred µs)
+    for (int k = 0; k < np; ++k) {
+      const int64_t lo = piece_lo(k), m = piece_lo(k + 1) - lo;
+      double* dd = (double*)((char*)dout + stride * k);
+      const int32_t* st = (const int32_t*)(dd + 8 * m);
+      HIP_OK(art::launch_flux(K, m, dd, dd + 3 * m, st, in.species + lo, nullptr, fx.nbins, hist_dev, c->m_comp));
+    }
+    HIP_OK(hipMemcpyAsync(fx.hist, hist_dev, 2 * (size_t)fx.nbins * sizeof(double), hipMemcpyDeviceToHost, c->m_comp));
+    HIP_OK(hipStreamSynchronize(c->m_comp));
+  }
+  return finish_timing(c);
+}
+
 int propagate_host_impl(const art_params* p, int64_t n, const double* x0, const double* k0, const double* erg,
                         const double* dw, const double* ln_t0, const int8_t* species, int32_t max_crossings,
                         art_segment_out* out, art_crossing_buf* xc, const TrajArgs& htr,
@@ -1220,8 +1575,9 @@ int propagate_host_impl(const art_params* p, int64_t n, const double* x0, const 
   const char* mode_env = std::getenv("ART_HOST_MODE");
   const std::string mode = (mode_env && *mode_env) ? mode_env : "stream";
   if (htr.ntimes == 0 && n >= env_int("ART_HOST_CHUNK_MIN", 1 << 21)) {
-    if (mode == "stream" && p->integrator == ART_VERN6) {
-      rc = propagate_host_streamed(c, p, n, x0, k0, erg, dw, ln_t0, species, max_crossings, out, xc, fx);
+    if ((mode == "stream" || mode == "stream_masked") && p->integrator == ART_VERN6) {
+      rc = mode == "stream" ? propagate_host_maskless(c, p, n, x0, k0, erg, dw, ln_t0, species, max_crossings, out, xc, fx)
+                            : propagate_host_streamed(c, p, n, x0, k0, erg, dw, ln_t0, species, max_crossings, out, xc, fx);
       if (rc != STREAM_FALLBACK) {
         if (rc == ART_OK) g_host_cnt[HC_STREAMED] += 1;
         return rc;

@@ -65,6 +65,25 @@ struct SegOut {
   unsigned long long* const* piece_sig;
   unsigned int* abort_word;
   int32_t piece_shift;
+  // The maskless streamed pipeline (DON = 3, art_capi.cpp propagate_host_maskless): one launch
+  // over the whole batch holds every CU; its first `helpers` blocks are helpers, not
+  // integrators. *host_ready (host memory, raised by the host as each piece's copies land)
+  // counts rays whose inputs are in HBM. Helpers claim 256-ray tiles to initialise
+  // (*init_next, init_one) and set chunk_ready[c] for each 64-ray chunk they finish; an
+  // integrator wave that claims a chunk waits for its flag. Finished rays count into
+  // piece_cnt[p] as in DON = 2; once a piece is complete, helpers claim its tiles to finalize
+  // (*fin_next, finalize_one) into the piece's SoA blob (blob + p blob_stride, piece_blob), and
+  // the block that finalizes a piece's last tile sets host_flags[p] (host memory the host
+  // polls, then copies the blob out). Integrator blocks become helpers when their waves run out
+  // of rays; every block initialises tiles of the first piece before it integrates.
+  const unsigned long long* host_ready;
+  unsigned long long* host_flags;
+  unsigned long long *init_next, *fin_next;
+  unsigned long long* piece_fin;
+  unsigned* chunk_ready;
+  char* blob;
+  int64_t blob_stride;
+  int32_t helpers;
   // Small batches (art_capi.cpp, propagate_device_impl): 1 = every fresh ray goes straight to
   // tail_kernel, one wave per ray (pack_fresh_kernel writes their CONT_REC records to cont),
   // instead of one lane per ray of the persistent integrator
@@ -79,6 +98,7 @@ struct SegOut {
   int32_t grad_cap, graduate;
 };
 constexpr unsigned long long STREAM_WAIT_TICKS = 200000000ull;  // 2 s at 100 MHz
+constexpr int CHUNK = 64;  // rays a persistent wave claims from the queue at once
 constexpr int END_REC = 16;
 constexpr int X_REC = 8;
 constexpr int CONT_REC = 24;  // [u (7) | f (7) | τ, dt, qpow, cprev, bstart, erg | int4 {ray, n_acc, n_rej, ncross} | int4 {iter, sprev, flags, save_k}]
@@ -100,7 +120,12 @@ hipError_t launch_init_range(const KParams& P, int64_t n, int64_t i0, int64_t i1
                              unsigned long long* stats, hipStream_t s);
 hipError_t launch_integrator_streamed(const KParams& P, int64_t n, const SegIn& in, const SegOut& out,
                                       int32_t max_crossings, unsigned long long* queue, unsigned long long* stats,
-                                      int blocks, hipStream_t s, int* grid_out);
+                                      int blocks, hipStream_t s, int* grid_out, bool maskless = false);
+// The maskless streamed pipeline's helper duty (helper_kernel HK_TILES, SegOut::host_ready ...):
+// `blocks` blocks; init_limit >= 0 initialises only (tiles below it), -1 serves to the end;
+// announce counts each block into host_flags[64] as it starts.
+hipError_t launch_helpers(const KParams& P, int64_t n, const SegIn& in, const SegOut& out, int blocks, int64_t init_limit,
+                          int announce, unsigned long long* stats, hipStream_t s);
 hipError_t launch_finalize_range(const KParams& P, int64_t n, int64_t i0, int64_t m, const SegIn& in,
                                  const SegOut& ol, hipStream_t s);
 // The batch size up to which launch_propagate runs every ray on a wave of its own (tail_kernel):

@@ -27,8 +27,6 @@ namespace art {
 enum { ST_ATTEMPTS = 0, ST_ACCEPTED, ST_ROOT_STEPS, ST_SCAN_EVALS, ST_INTERP_EVALS, ST_RAYS, ST_INIT_RHS, ST_CERT,
        ST_NSTATS = 8 };
 
-constexpr int CHUNK = 64;
-
 #ifdef ART_TRACE
 // dev build: per-attempt state of ONE ray (g_trace_ray) from whichever kernel integrates it:
 // [kernel (0 bulk, 1 tail), mode, hs, tau, EEst2, y (7), kk (7)] per attempt
@@ -441,14 +439,37 @@ __device__ inline int stream_poll(const SegOut& out, int leader) {
 // the release stay rare.
 __device__ inline void stream_count(const SegOut& out, int64_t n, int p, unsigned long long c) {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the write-back done before the count, always)
   const int leader = __ffsll((long long)__ballot(1)) - 1;
   if ((int)(threadIdx.x & 63) == leader) {
     const unsigned long long old = __hip_atomic_fetch_add(out.piece_cnt + p, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int64_t lo = (int64_t)p << out.piece_shift;
     const int64_t hi = (lo + ((int64_t)1 << out.piece_shift)) < n ? lo + ((int64_t)1 << out.piece_shift) : n;
-    if ((int64_t)(old + c) == hi - lo) {  // the piece's last count: every wave's records are out
+    if ((int64_t)(old + c) == hi - lo && out.piece_sig) {  // the piece's last count: every wave's records are out
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       __hip_atomic_store(out.piece_sig[p], 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+}
+
+// (DON = 2, 3) a wave's LDS histogram of finished rays per piece (lane l: piece l) into the
+// pieces' global counts: the wave's end-record stores released once (agent scope), then one
+// atomic add per piece with a count; the add that completes a piece raises its signal
+// (piece_sig, when the pipeline has one: the DON = 3 helpers poll piece_cnt itself)
+__device__ inline void stream_flush(const SegOut& out, int64_t n, unsigned* hist, int lane) {
+  const unsigned c = hist[lane];
+  if (__ballot(c != 0u) == 0ull) return;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the write-back done before the counts, always)
+  if (c != 0u) {
+    hist[lane] = 0u;
+    const unsigned long long old =
+        __hip_atomic_fetch_add(out.piece_cnt + lane, (unsigned long long)c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int64_t lo = (int64_t)lane << out.piece_shift;
+    const int64_t hi = (lo + ((int64_t)1 << out.piece_shift)) < n ? lo + ((int64_t)1 << out.piece_shift) : n;
+    if ((int64_t)(old + c) == hi - lo && out.piece_sig) {  // the piece's last count: every wave's records are out
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      __hip_atomic_store(out.piece_sig[lane], 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
   }
 }
@@ -486,6 +507,190 @@ __device__ inline KParams specialize(const KParams& P) {
   return Q;
 }
 
+// Fresh state of ray i (init_kernel; the maskless streamed integrator, DON = 3, runs it for
+// each chunk it claims): u0 (RayTracer.jl:179-216: k_norm_Cart onto the axion shell, Cartesian
+// -> (r, θ, φ), covariant celerity), f(u0) with the hamiltonian's in-place clamp (:531), the
+// initial dt (ode_determine_initdt, order 6, with its probe RHS; RK4: the fixed step) and the
+// condition value that seeds the callback's sign memory, into in.u0 = 16n doubles
+// [u0 (7) | f0 (7) | dt | c0]. Returns the RHS evaluations it took.
+__device__ inline unsigned init_one(const KParams& P, int64_t n, int64_t i, const SegIn& in) {
+  const double xs[3] = {in.x0[i], in.x0[n + i], in.x0[2 * n + i]};
+  const double ks[3] = {in.k0[i], in.k0[n + i], in.k0[2 * n + i]};
+  const double erg = in.erg[i], tau = in.lnt0[i];
+  const bool photon = in.species[i] != ART_AXION;
+  double u[7], f[7];
+  initial_state(P, xs, ks, erg, in.dw[i], u);
+  rhs(P, photon, u, tau, erg, f);
+  unsigned nrhs = 1;
+  if (photon && u[0] < P.rNS) u[0] = P.rNS;  // hamiltonian's in-place clamp (:531)
+  double dt;
+  if (P.integrator == ART_RK4) {
+    dt = (P.ln_t_end - tau) / P.n_fixed;
+  } else {
+    int probe = 0;
+    dt = initdt(P, photon, erg, u, f, tau, P.ln_t_end - tau, probe);
+    nrhs += probe;
+  }
+  const double c0 = condition_t(P, u, fexp(tau));
+#pragma unroll
+  for (int c = 0; c < 7; ++c) {
+    in.u0[c * n + i] = u[c];
+    in.u0[(7 + c) * n + i] = f[c];
+  }
+  in.u0[14 * n + i] = dt;
+  in.u0[15 * n + i] = c0;
+  return nrhs;
+}
+
+// End state of ray i in Cartesian form (back-transform, RayTracer.jl:393-416) from the raw end
+// record the integrator left in out.rec, spread into the SoA outputs at o (row stride m), and
+// the conversion probability of every recorded crossing (get_Prob_nonAD with Nc = 1,
+// MainRunner.jl:265). finalize_kernel runs it one thread per ray; the maskless streamed
+// integrator (DON = 3) for each chunk whose rays have all finished.
+__device__ inline void finalize_one(const KParams& P, int64_t n, int64_t i, int64_t o, int64_t m, const SegIn& in,
+                                    const SegOut& out) {
+  const double erg = in.erg[i];
+  int ncross = 0;
+  {
+    const double2* rq = reinterpret_cast<const double2*>(out.rec + i * END_REC);
+    double u[7], xe[3], ke[3];
+    const double2 q0 = rq[0], q1 = rq[1], q2 = rq[2], q3 = rq[3];
+    const int4 ri = reinterpret_cast<const int4*>(rq + 4)[0];
+    u[0] = q0.x; u[1] = q0.y; u[2] = q1.x; u[3] = q1.y; u[4] = q2.x; u[5] = q2.y; u[6] = q3.x;
+    back_transform(P, u, erg, xe, ke);
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      out.x_end[c * m + o] = xe[c];
+      out.k_end[c * m + o] = ke[c];
+    }
+    out.u7_end[o] = u[6];
+    out.tau_end[o] = q3.y;
+    out.status[o] = ri.x;
+    out.n_acc[o] = ri.y;
+    out.n_rej[o] = ri.z;
+    ncross = ri.w;
+    if (out.xcount) out.xcount[o] = ncross;
+    if (out.ntimes >= 2) out.traj_n[o] = reinterpret_cast<const int4*>(rq + 4)[1].x;
+  }
+  if (out.ntimes >= 2) {  // saveat: start (u0 back-transformed), interior to Cartesian, end
+    double u0[7], xs[3], ks[3];
+#pragma unroll
+    for (int c = 0; c < 7; ++c) u0[c] = in.u0[c * n + i];
+    back_transform(P, u0, erg, xs, ks);
+    const int mt = out.traj_n[o];
+    for (int k = 0; k < mt; ++k) {
+      double x[3];
+      if (k == 0) {
+        x[0] = xs[0]; x[1] = xs[1]; x[2] = xs[2];
+        out.traj_t[o] = in.lnt0[i];
+      } else if (k == mt - 1) {
+        x[0] = out.x_end[o]; x[1] = out.x_end[m + o]; x[2] = out.x_end[2 * m + o];
+        out.traj_t[int64_t(k) * m + o] = out.tau_end[o];
+      } else {
+        const double r = out.traj[(int64_t(0) * out.ntimes + k) * m + o];
+        double st, ct, sp, cp;
+        msincos(out.traj[(int64_t(1) * out.ntimes + k) * m + o], st, ct);
+        msincos(out.traj[(int64_t(2) * out.ntimes + k) * m + o], sp, cp);
+        x[0] = r * st * cp; x[1] = r * st * sp; x[2] = r * ct;
+      }
+#pragma unroll
+      for (int c = 0; c < 3; ++c) out.traj[(int64_t(c) * out.ntimes + k) * m + o] = x[c];
+    }
+  }
+  if (!out.xcount) return;
+  const int mc = ncross < out.cap ? ncross : out.cap;
+  for (int j = 0; j < mc; ++j) {
+    const double2* rq = reinterpret_cast<const double2*>(out.xrec + (i * out.cap + j) * X_REC);
+    const double2 q0 = rq[0], q1 = rq[1], q2 = rq[2], q3 = rq[3];
+    const double x[3] = {q0.x, q0.y, q1.x}, k[3] = {q1.y, q2.x, q2.y};
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      out.xpos[(int64_t(c) * out.cap + j) * m + o] = x[c];
+      out.xk[(int64_t(c) * out.cap + j) * m + o] = k[c];
+    }
+    out.xt[int64_t(j) * m + o] = q3.x;
+    const double dwc = q3.y;
+    out.xdw[int64_t(j) * m + o] = dwc;
+    out.xp[int64_t(j) * m + o] = prob_nonad_single(P, x, k, erg * fabs(dwc));  // erg_inf_ini .* abs.(Δωc)
+  }
+  if (out.nan_fill) {
+    for (int j = mc; j < out.cap; ++j) {
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        out.xpos[(int64_t(c) * out.cap + j) * m + o] = NAN;
+        out.xk[(int64_t(c) * out.cap + j) * m + o] = NAN;
+      }
+      out.xt[int64_t(j) * m + o] = NAN;
+      out.xdw[int64_t(j) * m + o] = NAN;
+      out.xp[int64_t(j) * m + o] = NAN;
+    }
+  }
+}
+
+// (DON = 3) the SoA output blob of piece p (art_capi.cpp, propagate_host_streamed: the same
+// layout and 256-byte alignments), its rows m long
+__device__ inline SegOut piece_blob(const SegOut& out, int64_t n, int p, int64_t& m) {
+  const int64_t lo = (int64_t)p << out.piece_shift;
+  const int64_t full = (int64_t)1 << out.piece_shift;
+  m = (n - lo) < full ? n - lo : full;
+  auto up = [](int64_t b) { return (b + 255) & ~(int64_t)255; };
+  char* db = out.blob + (int64_t)p * out.blob_stride;
+  double* dd = (double*)db;
+  int32_t* di32 = (int32_t*)(dd + 8 * m);
+  SegOut ol{};
+  ol.x_end = dd; ol.k_end = dd + 3 * m; ol.u7_end = dd + 6 * m; ol.tau_end = dd + 7 * m;
+  ol.status = di32; ol.n_acc = di32 + m; ol.n_rej = di32 + 2 * m;
+  ol.rec = out.rec;
+  if (out.cap) {
+    const int64_t cnt = up(m * 8 * 8 + m * 3 * 4);
+    double* x = (double*)(db + cnt + up(m * 4));
+    ol.cap = out.cap;
+    ol.xcount = (int32_t*)(db + cnt);
+    ol.xpos = x; ol.xk = x + 3 * out.cap * m; ol.xt = x + 6 * out.cap * m; ol.xdw = x + 7 * out.cap * m;
+    ol.xp = x + 8 * out.cap * m;
+    ol.xrec = out.xrec;
+    ol.nan_fill = 1;
+  }
+  return ol;
+}
+
+// ---- the maskless streamed pipeline's helper duty (DON = 3, SegOut::helpers) ----
+constexpr int S3_TILE = 1024;  // rays a helper block initialises or finalizes per claim (4 per thread: the claim,
+                               // the barriers and the L2 write-back of the hand-off amortised over 4 rays)
+constexpr unsigned long long S3_WAIT_TICKS = 2000000000ull;  // 20 s of s_memrealtime without progress: give up
+
+__device__ inline unsigned long long ld_sys(const unsigned long long* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ inline unsigned long long ld_agent(const unsigned long long* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// (DON = 3) the claimed chunk's fresh state: its flag as the leader lane reads it now, or after
+// a bounded wait (false: the wait timed out or another wave gave up; the wave stops taking rays)
+__device__ inline bool chunk_flag(const SegOut& out, int wnext, int leader) {
+  unsigned v = 0;
+  if ((int)(threadIdx.x & 63) == leader)
+    v = __hip_atomic_load(out.chunk_ready + wnext / CHUNK, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return __builtin_amdgcn_readlane((int)v, leader) != 0;
+}
+__device__ inline bool chunk_wait(const SegOut& out, int wnext, int leader) {
+  int ok = 1;
+  if ((int)(threadIdx.x & 63) == leader) {
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    while (__hip_atomic_load(out.chunk_ready + wnext / CHUNK, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
+      if (__hip_atomic_load(out.abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u ||
+          __builtin_amdgcn_s_memrealtime() - t0 > STREAM_WAIT_TICKS) {
+        __hip_atomic_store(out.abort_word, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        ok = 0;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(32);
+    }
+  }
+  return __shfl(ok, leader) != 0;
+}
+
 // DON: the tail-donation instantiations (SegOut::donate / cont_mode honoured); the others
 // carry none of that code, so a lone pass pays nothing for it
 // WPS: waves per SIMD the registers are budgeted for (the default 2; the GR continuation
@@ -513,12 +718,14 @@ __global__ __launch_bounds__(BLOCK, WPS) void propagate_kernel(const KParams P_i
   __shared__ double lastt[BLOCK];                 // t at the step's end (the scan certificate)
   __shared__ unsigned char srcl[BLOCK];           // compact list of the wave's scanning lanes
   __shared__ double thgrid[SCAN_WORDS * 16 + 1];  // Θs = j/(npts-1): range(0, 1, length = npts)
+  __shared__ unsigned pend_lds[BLOCK / 64][64];  // (DON = 2, 3) per wave: finished rays per piece, not yet counted
   double* const L = lds + threadIdx.x;
   const int wbase = threadIdx.x & ~63;
   const int lane = threadIdx.x & 63;
   const double tend = P.ln_t_end;
   const int npts = P.interp_points;
   for (int j = threadIdx.x; j < npts; j += BLOCK) thgrid[j] = double(j) / double(npts - 1);
+  if constexpr (DON >= 2) pend_lds[threadIdx.x >> 6][threadIdx.x & 63] = 0u;
   __syncthreads();
 
   int mode = M_IDLE;
@@ -538,8 +745,8 @@ __global__ __launch_bounds__(BLOCK, WPS) void propagate_kernel(const KParams P_i
   int post_s = 0, r_side = 0, r_it = 0;
   int wnext = 0, wend = 0;
   int rdy = 0;                           // (DON = 2) the ready counter as last read
-  int pend_p = -1, tick = 0;             // (DON = 2) the piece whose finished rays are being counted
-  unsigned long long pend_c = 0;         //           and their count (per wave; in LDS: 1.5% slower)
+  int tick = 0;                          // (DON = 2, 3) iterations, for the flushes of the piece counts
+  bool cready = false;                   // (DON = 3) the claimed chunk's fresh state is in
   int save_k = 1;  // SAVE: the next interior saveat index
   bool exhausted = false;
   unsigned s_att = 0, s_acc = 0, s_root = 0, s_scan = 0, s_interp = 0, s_rays = 0, s_cert = 0;
@@ -603,8 +810,27 @@ __global__ __launch_bounds__(BLOCK, WPS) void propagate_kernel(const KParams P_i
           if ((int64_t)base >= nq) { exhausted = true; break; }
           wnext = __builtin_amdgcn_readfirstlane((int)base);
           wend = __builtin_amdgcn_readfirstlane((int)((int64_t)base + CHUNK < nq ? (int64_t)base + CHUNK : nq));
+          cready = false;
         }
         int lim = wend;
+#ifndef ART_S_NOCHUNK  // (dev A/B: no chunk flags polled)
+        if constexpr (DON == 3) {
+#else
+        if constexpr (DON == 99) {
+#endif
+          // the chunk's fresh state (the helpers' chunk flag); while it is not in, a wave with
+          // other rays goes on integrating them, and an empty wave waits (bounded)
+          if (!cready) {
+            const int leader = __ffsll((long long)need) - 1;
+            if (!chunk_flag(out, wnext, leader)) {
+              if (lane == leader) atomicAdd(out.init_next + 2, 1ull);  // (the misses, for the host's trace)
+              if (__ballot(mode != M_IDLE) != 0ull) break;
+              if (!chunk_wait(out, wnext, leader)) { exhausted = true; break; }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            cready = true;
+          }
+        }
         if constexpr (DON == 2) {
           // only rays whose fresh state has arrived; while none of the chunk has, a wave with
           // other rays goes on integrating them, and an empty wave waits (bounded)
@@ -1353,7 +1579,7 @@ __global__ __launch_bounds__(BLOCK, WPS) void propagate_kernel(const KParams P_i
 
     int fin_piece = -1;  // (DON = 2) the piece of a ray finishing now
     if (finish >= 0) {  // the raw end record; finalize_kernel back-transforms it (RayTracer.jl:393-416)
-      if constexpr (DON == 2) fin_piece = ray >> out.piece_shift;
+      if constexpr (DON >= 2) fin_piece = ray >> out.piece_shift;
       double2* rq = reinterpret_cast<double2*>(out.rec + (int64_t)ray * END_REC);
       rq[0] = make_double2(u[0], u[1]);
       rq[1] = make_double2(u[2], u[3]);
@@ -1365,25 +1591,19 @@ __global__ __launch_bounds__(BLOCK, WPS) void propagate_kernel(const KParams P_i
       ray = -1;
       mode = M_IDLE;
     }
-    if constexpr (DON == 2) {
-      // the streamed host pipeline: count the rays finishing now into their pieces (batched,
-      // stream_count)
-      unsigned long long fm = __ballot(fin_piece >= 0);
-      while (fm != 0ull) {
-        const int pc = __builtin_amdgcn_readlane(fin_piece, __ffsll((long long)fm) - 1);
-        const unsigned long long same = __ballot(fin_piece == pc);
-        if (pc != pend_p) {
-          if (pend_c != 0ull) stream_count(out, n, pend_p, pend_c);
-          pend_p = pc;
-          pend_c = 0ull;
-        }
-        pend_c += (unsigned long long)__popcll(same);
-        fm &= ~same;
-      }
-      if (pend_c != 0ull && ((++tick & ART_STREAM_FLUSH) == 0 || exhausted)) {
-        stream_count(out, n, pend_p, pend_c);
-        pend_c = 0ull;
-      }
+#ifndef ART_S_NOCOUNT  // (dev A/B: no piece counts)
+    if constexpr (DON >= 2) {
+#else
+    if constexpr (DON >= 99) {
+#endif
+      // the streamed host pipelines: each finishing lane counts its ray into its wave's LDS
+      // histogram over the pieces; every ART_STREAM_FLUSH + 1 iterations (and once the queue is
+      // drained) the wave releases its stores and adds the histogram to the pieces' global
+      // counts, one lane per piece (stream_flush). Kept out of registers: a per-wave pending
+      // count held across the loop cost the integrator 7.5% in spills
+      // (profiles/r04s2_streamed_kernel_ab.jsonl)
+      if (fin_piece >= 0) atomicAdd(&pend_lds[threadIdx.x >> 6][fin_piece], 1u);
+      if ((++tick & ART_STREAM_FLUSH) == 0 || exhausted) stream_flush(out, n, pend_lds[threadIdx.x >> 6], lane);
     }
     ART_TMARK(0)  // saveat, reload, events, finish and the output stores (+ refill)
     // graduation (SegOut::graduate): a ray past `graduate` attempts, at a step boundary, leaves
@@ -1427,9 +1647,8 @@ __global__ __launch_bounds__(BLOCK, WPS) void propagate_kernel(const KParams P_i
     }
   }
 
-  if constexpr (DON == 2) {
-    if (pend_c != 0ull) stream_count(out, n, pend_p, pend_c);
-  }
+  if constexpr (DON >= 2) stream_flush(out, n, pend_lds[threadIdx.x >> 6], lane);
+
   // wave-reduce the statistics and add them once per wave
 #if defined(ART_SLOT_TIMING)
   if (lane == 0) {  // [refill etc, combination, RHS, slot rest, norm..park, grid, fast+walk+coop, fallback]
@@ -2097,134 +2316,159 @@ __global__ __launch_bounds__(256) void pack_fresh_kernel(const int64_t n, const 
   ri[1] = make_int4(0, sprev, photon | 2 /* cprev_ok */, 1 /* save_k */);
 }
 
-// Fresh state of every segment, one thread per ray: u0 (RayTracer.jl:179-216: k_norm_Cart
-// onto the axion shell, Cartesian -> (r, θ, φ), covariant celerity), f(u0) with the
-// hamiltonian's in-place clamp (:531), the initial dt (ode_determine_initdt, order 6, with
-// its probe RHS; RK4: the fixed step) and the condition value that seeds the callback's
-// sign memory. Kept out of the persistent integrator, whose registers it would otherwise
-// crowd. Out: in.u0 = 16n doubles [u0 (7) | f0 (7) | dt | c0].
-// Rays [i0, i1) of the n (the streamed host pipeline initialises the batch piece by piece).
-__global__ __launch_bounds__(256) void init_kernel(const KParams P, const int64_t n, const int64_t i0, const int64_t i1,
-                                                   const SegIn in, unsigned long long* __restrict__ stats) {
-  unsigned nrhs = 0;  // grid-stride over the rays: one stats atomic per wave
-  for (int64_t i = i0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < i1; i += (int64_t)gridDim.x * blockDim.x) {
-    const double xs[3] = {in.x0[i], in.x0[n + i], in.x0[2 * n + i]};
-    const double ks[3] = {in.k0[i], in.k0[n + i], in.k0[2 * n + i]};
-    const double erg = in.erg[i], tau = in.lnt0[i];
-    const bool photon = in.species[i] != ART_AXION;
-    double u[7], f[7];
-    initial_state(P, xs, ks, erg, in.dw[i], u);
-    rhs(P, photon, u, tau, erg, f);
-    nrhs += 1;
-    if (photon && u[0] < P.rNS) u[0] = P.rNS;  // hamiltonian's in-place clamp (:531)
-    double dt;
-    if (P.integrator == ART_RK4) {
-      dt = (P.ln_t_end - tau) / P.n_fixed;
+// Every initialisation and finalization of the library runs in helper_kernel, through ONE call
+// site of init_one and ONE of finalize_one: their arithmetic (the right-hand side's "fast"
+// contraction included) is then the same machine code for every path -- the single launch, the
+// chunked and CU-masked pipelines and the maskless streamed one -- so their outputs agree bit
+// for bit (tests/test_edges.py). (Inlined into two kernels, the photon RHS of init_one had
+// contracted differently: profiles/r04m_pytest.log.)
+//   HK_INIT  rays [i0, i1): fresh state into in.u0 (grid-stride over 256-ray tiles);
+//   HK_FIN   rays [i0, i1): the end state into `out` at o = i - i0, row stride i1 - i0;
+//   HK_TILES the maskless streamed pipeline's helper duty (SegOut::host_ready ...): claim
+//            256-ray tiles to initialise once the host's copies of their inputs have landed,
+//            and tiles of each finished piece to finalize into its blob; flag each initialised
+//            chunk (chunk_ready, which the integrator's waves poll) and each finalized piece
+//            (host_flags, which the host polls). init_limit >= 0: initialise only, until every
+//            tile below it is claimed (the pass that starts the launch); -1: serve until every
+//            tile is initialised and finalized. announce: count this block into *host_started
+//            (the host launches the integrator once every persistent helper block is resident).
+//            Each hand-off: the block's stores, s_waitcnt, barrier, one agent-scope release,
+//            then the flag (MI355X_MICROARCH.md, inter-workgroup visibility); readers poll the
+//            flag and take one agent-scope acquire.
+enum { HK_INIT = 0, HK_FIN = 1, HK_TILES = 2 };
+__global__ __launch_bounds__(256) void helper_kernel(const KParams P, const int64_t n, const SegIn in, const SegOut out,
+                                                     const int mode, const int64_t i0, const int64_t i1,
+                                                     const int64_t init_limit, const int announce,
+                                                     unsigned long long* __restrict__ stats) {
+  __shared__ long long cmd[2];  // HK_TILES: [what, tile]: 0 nothing now, 1 initialise, 2 finalize, 3 done
+  const int tid = threadIdx.x;
+  const int64_t full = (int64_t)1 << out.piece_shift;
+  auto piece_rays = [&](int p) {
+    const int64_t lo = (int64_t)p << out.piece_shift;
+    return (n - lo) < full ? n - lo : full;
+  };
+  const int64_t TS = mode == HK_TILES ? S3_TILE : 256;  // rays per tile
+  int64_t tile = blockIdx.x;
+  unsigned long long hr = 0;  // (HK_TILES, thread 0) host_ready as last read: it only grows
+  long long pend = -1;  // (HK_TILES, thread 0) a claimed finalize tile whose piece is still running
+  unsigned long long t_idle = __builtin_amdgcn_s_memrealtime();
+  unsigned nrhs = 0;
+  if (mode == HK_TILES && announce && tid == 0)
+    __hip_atomic_fetch_add(out.host_flags + 64, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  while (true) {
+    long long what = 0, t = -1;
+    if (mode != HK_TILES) {
+      t = (long long)(i0 + tile * TS);
+      if (t >= i1) break;
+      what = mode == HK_INIT ? 1 : 2;
+      tile += gridDim.x;
     } else {
-      int probe = 0;
-      dt = initdt(P, photon, erg, u, f, tau, P.ln_t_end - tau, probe);
-      nrhs += probe;
+      if (tid == 0) {
+        const unsigned long long inext = ld_agent(out.init_next);
+        if (init_limit >= 0 && (int64_t)inext >= init_limit) what = 3;
+        if (what == 0 && (int64_t)inext < n && inext >= hr) hr = ld_sys(out.host_ready);
+        if (what == 0 && (int64_t)inext < n && inext < hr) {
+          const unsigned long long c = atomicAdd(out.init_next, (unsigned long long)S3_TILE);
+          if ((int64_t)c < n) {  // (a tile past the landed inputs waits for them below)
+            what = 1;
+            t = (long long)c;
+          }
+        }
+        if (what == 0 && init_limit < 0) {
+          if (pend < 0) {
+            const unsigned long long fnext = ld_agent(out.fin_next);
+            if ((int64_t)fnext < n) {
+              const int p = (int)(fnext >> out.piece_shift);
+              if ((int64_t)ld_agent(out.piece_cnt + p) == piece_rays(p)) {
+                const unsigned long long c = atomicAdd(out.fin_next, (unsigned long long)S3_TILE);
+                if ((int64_t)c < n) pend = (long long)c;
+              }
+            }
+          }
+          if (pend >= 0) {
+            const int p = (int)(pend >> out.piece_shift);
+            if ((int64_t)ld_agent(out.piece_cnt + p) == piece_rays(p)) {
+              what = 2;
+              t = pend;
+              pend = -1;
+            }
+          }
+          if (what == 0 && pend < 0 && (int64_t)inext >= n && (int64_t)ld_agent(out.fin_next) >= n) what = 3;
+        }
+        if (what == 1) {  // the tile's inputs (bounded wait)
+          const int64_t t1 = (int64_t)t + S3_TILE < n ? (int64_t)t + S3_TILE : n;
+          const unsigned long long w0 = __builtin_amdgcn_s_memrealtime();
+          while ((int64_t)ld_sys(out.host_ready) < t1) {
+            if (__hip_atomic_load(out.abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u ||
+                __builtin_amdgcn_s_memrealtime() - w0 > S3_WAIT_TICKS) {
+              __hip_atomic_store(out.abort_word, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+              what = 3;
+              break;
+            }
+            __builtin_amdgcn_s_sleep(32);
+          }
+        }
+        if (what == 0 && (__hip_atomic_load(out.abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u ||
+                          __builtin_amdgcn_s_memrealtime() - t_idle > S3_WAIT_TICKS)) {
+          __hip_atomic_store(out.abort_word, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          what = 3;
+        }
+        if (what == 1 || what == 2) {
+          t_idle = __builtin_amdgcn_s_memrealtime();
+          // the inputs the DMA engines wrote / the end records other CUs wrote
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        cmd[0] = what;
+        cmd[1] = t;
+      }
+      __syncthreads();
+      what = cmd[0];
+      t = cmd[1];
+      __syncthreads();
+      if (what == 3) break;
+      if (what == 0) {
+        __builtin_amdgcn_s_sleep(16);
+        continue;
+      }
     }
-    const double c0 = condition_t(P, u, fexp(tau));
-#pragma unroll
-    for (int c = 0; c < 7; ++c) {
-      in.u0[c * n + i] = u[c];
-      in.u0[(7 + c) * n + i] = f[c];
+    const int64_t t1 = t + TS < (mode == HK_TILES ? n : i1) ? t + TS : (mode == HK_TILES ? n : i1);
+    SegOut ol = out;
+    int64_t ob = i0, m = i1 - i0;
+    if (mode == HK_TILES && what == 2) {
+      const int p = (int)(t >> out.piece_shift);
+      ol = piece_blob(out, n, p, m);
+      ob = (int64_t)p << out.piece_shift;
     }
-    in.u0[14 * n + i] = dt;
-    in.u0[15 * n + i] = c0;
+    for (int64_t i = t + tid; i < t1; i += 256) {  // (one call site of each)
+      if (what == 1) nrhs += init_one(P, n, i, in);
+      else finalize_one(P, n, i, i - ob, m, in, ol);
+    }
+    if (mode == HK_TILES) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (what == 1) {
+          for (int64_t c = t / CHUNK; c * CHUNK < t1; ++c)
+            __hip_atomic_store(out.chunk_ready + c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+          const int p = (int)(t >> out.piece_shift);
+          const unsigned long long tiles = (unsigned long long)((piece_rays(p) + S3_TILE - 1) / S3_TILE);
+          const unsigned long long old =
+              __hip_atomic_fetch_add(out.piece_fin + p, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (old + 1ull == tiles) {  // the piece's last tile: its blob is complete in memory
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            __hip_atomic_store(out.host_flags + p, 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+          }
+        }
+      }
+    }
   }
   unsigned long long x = nrhs;  // init RHS evaluations -> stats[6]
   for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off);
-  if ((threadIdx.x & 63) == 0 && x) atomicAdd(&stats[6], x);
-}
-
-// End state in Cartesian form (back-transform, RayTracer.jl:393-416) from the raw end record
-// the integrator left in out.rec (spread into the SoA outputs here), and the conversion probability of every
-// recorded crossing (get_Prob_nonAD with Nc = 1, MainRunner.jl:265). One thread per ray.
-// Rays [i0, i0 + m) of the n; the outputs are indexed o = i - i0 with row stride m (the whole
-// batch: i0 = 0, m = n; the streamed host pipeline: one piece into its own SoA blob).
-__global__ __launch_bounds__(256) void finalize_kernel(const KParams P, const int64_t n, const int64_t i0,
-                                                       const int64_t m, const SegIn in, const SegOut out) {
-  const int64_t o = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (o >= m) return;
-  const int64_t i = i0 + o;
-  const double erg = in.erg[i];
-  int ncross = 0;
-  {
-    const double2* rq = reinterpret_cast<const double2*>(out.rec + i * END_REC);
-    double u[7], xe[3], ke[3];
-    const double2 q0 = rq[0], q1 = rq[1], q2 = rq[2], q3 = rq[3];
-    const int4 ri = reinterpret_cast<const int4*>(rq + 4)[0];
-    u[0] = q0.x; u[1] = q0.y; u[2] = q1.x; u[3] = q1.y; u[4] = q2.x; u[5] = q2.y; u[6] = q3.x;
-    back_transform(P, u, erg, xe, ke);
-#pragma unroll
-    for (int c = 0; c < 3; ++c) {
-      out.x_end[c * m + o] = xe[c];
-      out.k_end[c * m + o] = ke[c];
-    }
-    out.u7_end[o] = u[6];
-    out.tau_end[o] = q3.y;
-    out.status[o] = ri.x;
-    out.n_acc[o] = ri.y;
-    out.n_rej[o] = ri.z;
-    ncross = ri.w;
-    if (out.xcount) out.xcount[o] = ncross;
-    if (out.ntimes >= 2) out.traj_n[o] = reinterpret_cast<const int4*>(rq + 4)[1].x;
-  }
-  if (out.ntimes >= 2) {  // saveat: start (u0 back-transformed), interior to Cartesian, end
-    double u0[7], xs[3], ks[3];
-#pragma unroll
-    for (int c = 0; c < 7; ++c) u0[c] = in.u0[c * n + i];
-    back_transform(P, u0, erg, xs, ks);
-    const int mt = out.traj_n[o];
-    for (int k = 0; k < mt; ++k) {
-      double x[3];
-      if (k == 0) {
-        x[0] = xs[0]; x[1] = xs[1]; x[2] = xs[2];
-        out.traj_t[o] = in.lnt0[i];
-      } else if (k == mt - 1) {
-        x[0] = out.x_end[o]; x[1] = out.x_end[m + o]; x[2] = out.x_end[2 * m + o];
-        out.traj_t[int64_t(k) * m + o] = out.tau_end[o];
-      } else {
-        const double r = out.traj[(int64_t(0) * out.ntimes + k) * m + o];
-        double st, ct, sp, cp;
-        msincos(out.traj[(int64_t(1) * out.ntimes + k) * m + o], st, ct);
-        msincos(out.traj[(int64_t(2) * out.ntimes + k) * m + o], sp, cp);
-        x[0] = r * st * cp; x[1] = r * st * sp; x[2] = r * ct;
-      }
-#pragma unroll
-      for (int c = 0; c < 3; ++c) out.traj[(int64_t(c) * out.ntimes + k) * m + o] = x[c];
-    }
-  }
-  if (!out.xcount) return;
-  const int mc = ncross < out.cap ? ncross : out.cap;
-  for (int j = 0; j < mc; ++j) {
-    const double2* rq = reinterpret_cast<const double2*>(out.xrec + (i * out.cap + j) * X_REC);
-    const double2 q0 = rq[0], q1 = rq[1], q2 = rq[2], q3 = rq[3];
-    const double x[3] = {q0.x, q0.y, q1.x}, k[3] = {q1.y, q2.x, q2.y};
-#pragma unroll
-    for (int c = 0; c < 3; ++c) {
-      out.xpos[(int64_t(c) * out.cap + j) * m + o] = x[c];
-      out.xk[(int64_t(c) * out.cap + j) * m + o] = k[c];
-    }
-    out.xt[int64_t(j) * m + o] = q3.x;
-    const double dwc = q3.y;
-    out.xdw[int64_t(j) * m + o] = dwc;
-    out.xp[int64_t(j) * m + o] = prob_nonad_single(P, x, k, erg * fabs(dwc));  // erg_inf_ini .* abs.(Δωc)
-  }
-  if (out.nan_fill) {
-    for (int j = mc; j < out.cap; ++j) {
-#pragma unroll
-      for (int c = 0; c < 3; ++c) {
-        out.xpos[(int64_t(c) * out.cap + j) * m + o] = NAN;
-        out.xk[(int64_t(c) * out.cap + j) * m + o] = NAN;
-      }
-      out.xt[int64_t(j) * m + o] = NAN;
-      out.xdw[int64_t(j) * m + o] = NAN;
-      out.xp[int64_t(j) * m + o] = NAN;
-    }
-  }
+  if ((tid & 63) == 0 && x) atomicAdd(&stats[6], x);
 }
 
 // ---------------------------------------------------------------------------
@@ -2878,9 +3122,9 @@ hipError_t launch_propagate(const KParams& P, int64_t n, const SegIn& in, const 
 #else
 #define ART_DBG(stage)
 #endif
-  hipLaunchKernelGGL(init_kernel, dim3((unsigned)(gr < 2048 ? gr : 2048)), dim3(256), 0, s, P, n, (int64_t)0, n, in,
-                     stats);
-  ART_DBG("init_kernel")
+  hipLaunchKernelGGL(helper_kernel, dim3((unsigned)(gr < 2048 ? gr : 2048)), dim3(256), 0, s, P, n, in, out_arg, (int)HK_INIT,
+                     (int64_t)0, n, (int64_t)-1, 0, stats);
+  ART_DBG("helper_kernel (init)")
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   const bool flat = P.rs_eff == 0.0 && !(P.bndry_lyr > 0.0) && !P.isotropic;
@@ -2917,11 +3161,46 @@ hipError_t launch_propagate(const KParams& P, int64_t n, const SegIn& in, const 
       if ((e = hipStreamWaitEvent(fs, ev1, 0)) != hipSuccess) return e;
       sf = fs;
     }
-    hipLaunchKernelGGL(finalize_kernel, dim3(g1), dim3(256), 0, sf, P, n, (int64_t)0, n, in, out);
+    hipLaunchKernelGGL(helper_kernel, dim3(g1), dim3(256), 0, sf, P, n, in, out, (int)HK_FIN, (int64_t)0, n,
+                       (int64_t)-1, 0, stats);
     return hipGetLastError();
   }
   KFn fn = out.donate > 0 ? pick_propagate<1>(out.ntimes >= 2, rk4, flat, sch)
                            : pick_propagate<0>(out.ntimes >= 2, rk4, flat, sch);
+  // (dev A/B, ART_DEV_STREAMED_KERNEL=2|3: the streamed pipelines' integrator builds on a
+  // device-resident batch -- every chunk flagged in, every input ready -- to price their extra
+  // code against this launch's own)
+  if (const char* e = std::getenv("ART_DEV_STREAMED_KERNEL")) {
+    const int don = std::atoi(e);
+    if ((don == 2 || don == 3) && flat && !rk4 && out.ntimes < 2 && out.donate <= 0) {
+      static void* dbuf = nullptr;
+      static size_t dbytes = 0;
+      const size_t need = 4096 + ((size_t)n / CHUNK + 1) * sizeof(unsigned);
+      if (dbytes < need) {
+        if (dbuf) (void)hipFree(dbuf);
+        if (hipMalloc(&dbuf, need) != hipSuccess) return hipErrorOutOfMemory;
+        dbytes = need;
+      }
+      unsigned long long* w = (unsigned long long*)dbuf;
+      (void)hipMemsetAsync(w, 0, 4096, s);
+      (void)hipMemsetAsync((char*)dbuf + 4096, 1, need - 4096, s);
+      out.piece_cnt = w + 32;
+      out.piece_sig = nullptr;
+      out.piece_shift = 19;
+      out.chunk_ready = (unsigned*)((char*)dbuf + 4096);
+      out.init_next = w + 16;
+      static unsigned long long* rdy = nullptr;
+      if (!rdy) {
+        (void)hipMalloc((void**)&rdy, 8);
+      }
+      const unsigned long long big = ~0ull >> 1;
+      (void)hipMemcpyAsync(rdy, &big, 8, hipMemcpyHostToDevice, s);
+      (void)hipStreamSynchronize(s);
+      out.ready = rdy;
+      out.abort_word = (unsigned*)(w + 8 * 60);
+      fn = don == 2 ? propagate_kernel<ART_VERN6, GEOM_FLAT, false, 2> : propagate_kernel<ART_VERN6, GEOM_FLAT, false, 3>;
+    }
+  }
   // A batch that fits one ray per lane of 1 wave per SIMD runs the 1-wave/SIMD build, which
   // does not spill: lone GR tail ray -3%, flat -4.5% per attempt, bit-identical
   // (profiles/r02j_small_batch_w1_ab.txt, tests/test_edges.py). ART_W1=0 switches it off (A/B).
@@ -2991,8 +3270,9 @@ hipError_t launch_propagate(const KParams& P, int64_t n, const SegIn& in, const 
     if ((e = hipStreamWaitEvent(fs, ev1, 0)) != hipSuccess) return e;
     sf = fs;
   }
-  hipLaunchKernelGGL(finalize_kernel, dim3(g1), dim3(256), 0, sf, P, n, (int64_t)0, n, in, out);
-  ART_DBG("finalize_kernel")
+  hipLaunchKernelGGL(helper_kernel, dim3(g1), dim3(256), 0, sf, P, n, in, out, (int)HK_FIN, (int64_t)0, n, (int64_t)-1,
+                     0, stats);
+  ART_DBG("helper_kernel (finalize)")
   return hipGetLastError();
 }
 
@@ -3000,7 +3280,8 @@ hipError_t launch_init_range(const KParams& P, int64_t n, int64_t i0, int64_t i1
                              unsigned long long* stats, hipStream_t s) {
   const int64_t gr = (i1 - i0 + 255) / 256;
   if (gr <= 0) return hipSuccess;
-  hipLaunchKernelGGL(init_kernel, dim3((unsigned)(gr < 2048 ? gr : 2048)), dim3(256), 0, s, P, n, i0, i1, in, stats);
+  hipLaunchKernelGGL(helper_kernel, dim3((unsigned)(gr < 2048 ? gr : 2048)), dim3(256), 0, s, P, n, in, SegOut{},
+                     (int)HK_INIT, i0, i1, (int64_t)-1, 0, stats);
   return hipGetLastError();
 }
 
@@ -3009,11 +3290,15 @@ hipError_t launch_init_range(const KParams& P, int64_t n, int64_t i0, int64_t i1
 // finalize kernels of the pieces).
 hipError_t launch_integrator_streamed(const KParams& P, int64_t n, const SegIn& in, const SegOut& out,
                                       int32_t max_crossings, unsigned long long* queue, unsigned long long* stats,
-                                      int blocks, hipStream_t s, int* grid_out) {
+                                      int blocks, hipStream_t s, int* grid_out, bool maskless) {
   const bool flat = P.rs_eff == 0.0 && !(P.bndry_lyr > 0.0) && !P.isotropic;
   const bool sch = P.rs_eff > 0.0 && !(P.bndry_lyr > 0.0) && !P.isotropic;
-  const KFn fn = flat ? propagate_kernel<ART_VERN6, GEOM_FLAT, false, 2>
-                      : (sch ? propagate_kernel<ART_VERN6, GEOM_GR, false, 2> : propagate_kernel<ART_VERN6, GEOM_ANY, false, 2>);
+  const KFn fn = maskless ? (flat ? propagate_kernel<ART_VERN6, GEOM_FLAT, false, 3>
+                                  : (sch ? propagate_kernel<ART_VERN6, GEOM_GR, false, 3>
+                                         : propagate_kernel<ART_VERN6, GEOM_ANY, false, 3>))
+                          : (flat ? propagate_kernel<ART_VERN6, GEOM_FLAT, false, 2>
+                                  : (sch ? propagate_kernel<ART_VERN6, GEOM_GR, false, 2>
+                                         : propagate_kernel<ART_VERN6, GEOM_ANY, false, 2>));
   const int64_t need = (n + BLOCK - 1) / BLOCK;
   const int grid = (int)(need < (int64_t)blocks ? need : (int64_t)blocks);
   if (grid_out) *grid_out = grid;
@@ -3021,10 +3306,18 @@ hipError_t launch_integrator_streamed(const KParams& P, int64_t n, const SegIn& 
   return hipGetLastError();
 }
 
+hipError_t launch_helpers(const KParams& P, int64_t n, const SegIn& in, const SegOut& out, int blocks, int64_t init_limit,
+                          int announce, unsigned long long* stats, hipStream_t s) {
+  hipLaunchKernelGGL(helper_kernel, dim3((unsigned)blocks), dim3(256), 0, s, P, n, in, out, (int)HK_TILES, (int64_t)0, n,
+                     init_limit, announce, stats);
+  return hipGetLastError();
+}
+
 hipError_t launch_finalize_range(const KParams& P, int64_t n, int64_t i0, int64_t m, const SegIn& in,
                                  const SegOut& ol, hipStream_t s) {
   if (m <= 0) return hipSuccess;
-  hipLaunchKernelGGL(finalize_kernel, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, P, n, i0, m, in, ol);
+  hipLaunchKernelGGL(helper_kernel, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, P, n, in, ol, (int)HK_FIN, i0,
+                     i0 + m, (int64_t)-1, 0, nullptr);
   return hipGetLastError();
 }
 
