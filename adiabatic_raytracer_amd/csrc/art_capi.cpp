@@ -1346,11 +1346,15 @@ int propagate_host_maskless(DeviceCtx* c, const art_params* p, int64_t n, const 
   // integrator only once every one of them is resident, so it cannot take their slots
   const int helpers = std::min(slots - 1, std::max(1, env_int("ART_HOST_HELPERS", 8)));
   so.helpers = helpers;
+  // (dev, ART_HOST_STREAM_SERIAL=1: no persistent helpers -- every tile initialised before the
+  // integrator and finalized after it, kernel by kernel: for a counter-collection run, which
+  // serialises kernels; the integrator's code and traffic are the same)
+  const bool serial = env_int("ART_HOST_STREAM_SERIAL", 0) != 0;
   hipEvent_t ev_zero = c->pev[nu + np];  // (the helpers start on zeroed counters)
   HIP_OK(hipEventRecord(ev_zero, c->m_comp));
   HIP_OK(hipStreamWaitEvent(c->m_help, ev_zero, 0));
-  HIP_OK(art::launch_helpers(K, n, in, so, helpers, -1, 1, words + 1, c->m_help));
-  {
+  if (!serial) HIP_OK(art::launch_helpers(K, n, in, so, helpers, -1, 1, words + 1, c->m_help));
+  if (!serial) {
     const double tw = clk();
     while (__atomic_load_n(hflag + NFLAG, __ATOMIC_ACQUIRE) < (unsigned long long)helpers) {
       if (clk() - tw > 5000.0) {  // (never seen: the device is shared or wedged) -- let them go, fall back
@@ -1366,12 +1370,12 @@ int propagate_host_maskless(DeviceCtx* c, const art_params* p, int64_t n, const 
   // finalize what is left
   // the first upload unit by every block slot, then the helpers keep ahead (ART_HOST_INIT_RAYS:
   // dev, another amount)
-  const int64_t first = std::min(n, (int64_t)std::max(1, env_int("ART_HOST_INIT_RAYS", (int)ulo[1])));
+  const int64_t first = serial ? n : std::min(n, (int64_t)std::max(1, env_int("ART_HOST_INIT_RAYS", (int)ulo[1])));
   if (env_int("ART_HOST_INITPASS", 1))  // (dev: 0 leaves the first piece to the helpers)
-    HIP_OK(art::launch_helpers(K, n, in, so, slots - helpers, first, 0, words + 1, c->m_comp));
+    HIP_OK(art::launch_helpers(K, n, in, so, serial ? slots : slots - helpers, first, 0, words + 1, c->m_comp));
   HIP_OK(hipEventRecord(L->ev0, c->m_comp));
-  HIP_OK(art::launch_integrator_streamed(K, n, in, so, max_crossings, words, words + 1, slots - helpers, c->m_comp,
-                                         &L->grid, true));
+  HIP_OK(art::launch_integrator_streamed(K, n, in, so, max_crossings, words, words + 1, serial ? slots : slots - helpers,
+                                         c->m_comp, &L->grid, true));
   HIP_OK(hipEventRecord(L->ev1, c->m_comp));
   HIP_OK(art::launch_helpers(K, n, in, so, slots, -1, 0, words + 1, c->m_comp));
   hipEvent_t ev_help = c->pev[nu + np + 1];  // (the persistent helpers' init counts, in the statistics)

@@ -304,7 +304,7 @@ def main():
         alg_bytes = n * BYTES_PER_SEGMENT + ncross * BYTES_PER_CROSSING
         streamed = cnt["streamed"] == args.steps
         kname = (f"propagate_kernel<{'RK4' if args.integrator == 'rk4' else 'Vern6'}"
-                 f"{', streamed (DON=2)' if streamed else ''}>")
+                 f"{', streamed (DON=3)' if streamed else ''}>")
         tr, tr_src = traffic("streamed" if streamed else "device")
         in_b = sum(a.nbytes for a in h.values())
         out_b = sum(a.nbytes for a in hout.values())

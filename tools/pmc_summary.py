@@ -57,13 +57,13 @@ def main():
         return {"kernel": name, "hbm_bytes_per_launch": fetch * c_read + write * c_write,
                 "fetch_bytes_raw": fetch, "write_bytes_raw": write,
                 "other_counters_per_launch": {c: v[-1] for c, v in pc.items() if c not in ("FETCH_SIZE", "WRITE_SIZE")}}
-    # the Vern6 integrator's instantiations: <INTEG, GEOM, SAVE, DON, WPS>; DON = 2 is the
-    # streamed host pipeline's (bench.py's headline), DON = 0 the device-resident pass's
+    # the Vern6 integrator's instantiations: <INTEG, GEOM, SAVE, DON, WPS>; DON = 3 is the
+    # maskless streamed host pipeline's (bench.py's headline), DON = 0 the device-resident pass's
     kernels = {}
     for name, pc in k.items():
         m = re.search(r"propagate_kernel<0, \d, false, (\d),", name)
         if m and "FETCH_SIZE" in pc and "WRITE_SIZE" in pc:
-            kernels[{"2": "streamed", "0": "device"}.get(m.group(1), "don" + m.group(1))] = summary(name, pc)
+            kernels[{"3": "streamed", "0": "device"}.get(m.group(1), "don" + m.group(1))] = summary(name, pc)
     top = kernels.get("streamed") or kernels["device"]
     res = {
         "workload": workload,
