@@ -1572,13 +1572,15 @@ int propagate_host_impl(const art_params* p, int64_t n, const double* x0, const 
   DeviceCtx* c;
   if ((rc = current_ctx(&c))) return rc;
   g_host_cnt[HC_CALLS] += 1;
-  // large batches (ART_HOST_CHUNK_MIN rays and more, default 2^21; no saveat): the streamed
-  // pipeline (ART_HOST_MODE=stream, the default, Vern6) or the chunked one (=chunked); smaller
+  // large batches (ART_HOST_CHUNK_MIN rays and more, default 2^20, so the 1.25e6-ray shard of
+  // 8 GPUs streams: 18.3 ms against 20.0 in one launch, profiles/r04x_shard_sizes.jsonl; no
+  // saveat): the streamed pipeline (ART_HOST_MODE=stream, the default, Vern6) or the chunked
+  // one (=chunked); smaller
   // batches, RK4, saveat, ART_HOST_MODE=single and a streamed call that gave up take the single
   // launch below
   const char* mode_env = std::getenv("ART_HOST_MODE");
   const std::string mode = (mode_env && *mode_env) ? mode_env : "stream";
-  if (htr.ntimes == 0 && n >= env_int("ART_HOST_CHUNK_MIN", 1 << 21)) {
+  if (htr.ntimes == 0 && n >= env_int("ART_HOST_CHUNK_MIN", 1 << 20)) {
     if ((mode == "stream" || mode == "stream_masked") && p->integrator == ART_VERN6) {
       rc = mode == "stream" ? propagate_host_maskless(c, p, n, x0, k0, erg, dw, ln_t0, species, max_crossings, out, xc, fx)
                             : propagate_host_streamed(c, p, n, x0, k0, erg, dw, ln_t0, species, max_crossings, out, xc, fx);
