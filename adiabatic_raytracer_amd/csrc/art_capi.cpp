@@ -1462,8 +1462,12 @@ int propagate_host_maskless(DeviceCtx* c, const art_params* p, int64_t n, const 
     return moved;
   };
   int perr = 0;
+  // (tests: ART_HOST_UPLOAD_DELAY_MS holds back the second piece's upload, so the integrator's
+  // waves outwait their 2 s bound and the device side gives the call up)
+  const int delay_ms = env_int("ART_HOST_UPLOAD_DELAY_MS", 0);
   for (int u = 0; u < nu && !perr; ++u) {
     const int64_t lo = ulo[u], m = ulo[u + 1] - lo;
+    if (delay_ms > 0 && lo == piece_lo(1)) std::this_thread::sleep_for(std::chrono::milliseconds(delay_ms));
     const double* src[9] = {x0, x0 + n, x0 + 2 * n, k0, k0 + n, k0 + 2 * n, erg, dw, ln_t0};
     std::vector<Seg> g;
     for (int r = 0; r < 9; ++r) g.push_back({pin + r * nd + lo, src[r] + lo, (size_t)m * sizeof(double)});

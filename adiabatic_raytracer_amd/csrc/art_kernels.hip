@@ -1603,7 +1603,12 @@ __global__ __launch_bounds__(BLOCK, WPS) void propagate_kernel(const KParams P_i
       // count held across the loop cost the integrator 7.5% in spills
       // (profiles/r04s2_streamed_kernel_ab.jsonl)
       if (fin_piece >= 0) atomicAdd(&pend_lds[threadIdx.x >> 6][fin_piece], 1u);
-      if ((++tick & ART_STREAM_FLUSH) == 0 || exhausted) stream_flush(out, n, pend_lds[threadIdx.x >> 6], lane);
+#ifndef ART_DRAIN_FLUSH_MASK
+#define ART_DRAIN_FLUSH_MASK 7  // (once the queue is drained: every 8th iteration, so the drain pays few write-backs)
+#endif
+      ++tick;
+      if ((tick & ART_STREAM_FLUSH) == 0 || (exhausted && (tick & ART_DRAIN_FLUSH_MASK) == 0))
+        stream_flush(out, n, pend_lds[threadIdx.x >> 6], lane);
     }
     ART_TMARK(0)  // saveat, reload, events, finish and the output stores (+ refill)
     // graduation (SegOut::graduate): a ray past `graduate` attempts, at a step boundary, leaves

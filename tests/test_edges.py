@@ -361,6 +361,34 @@ def test_streamed_host_pipeline_gives_up_cleanly(monkeypatch):
 
 
 @pytest.mark.gpu
+def test_streamed_host_pipeline_device_give_up(monkeypatch):
+    """The device side's bound: with the second piece's upload held back 2.5 s, the integrator's
+    waves outwait their 2 s bound on a chunk flag, raise the abort word and stop; the host sees it,
+    lets the launch run out and runs the batch again as one launch. The results are the single
+    launch's, the give-up is counted, and the next streamed call works normally."""
+    import adiabatic_raytracer_amd as A
+    p = A.Params(**CONFIGS["flat"])
+    n = 20011
+    s = A.sample_conversion_points(p, n, seed=1769)
+    args = (s["x"], s["k_init"], s["erg"], -np.ones(n), np.full(n, -30.0), np.ones(n, np.int8))
+    monkeypatch.setenv("ART_HOST_MODE", "single")
+    ref = A.propagate_batch(p, *args)
+    monkeypatch.setenv("ART_HOST_MODE", "stream")
+    monkeypatch.setenv("ART_HOST_PIECE_SHIFT", "11")
+    monkeypatch.setenv("ART_HOST_CHUNK_MIN", "1000")
+    A.raytracer.host_path_counters(reset=True)
+    for delay, want in (("2500", {"streamed": 0, "stream_giveups": 1, "single": 1}),
+                        ("0", {"streamed": 1, "stream_giveups": 1, "single": 1})):
+        monkeypatch.setenv("ART_HOST_UPLOAD_DELAY_MS", delay)
+        got = A.propagate_batch(p, *args)
+        for key, v in ref.items():
+            if isinstance(v, np.ndarray):
+                assert np.array_equal(v, got[key], equal_nan=True), (delay, key)
+        cnt = A.raytracer.host_path_counters()
+        assert {k: cnt[k] for k in want} == want, (delay, cnt)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("cfg,species,cap", [("flat", 1, 1), ("gr", 1, 1), ("gr_oblique", 1, 2), ("flat", 0, 3)])
 def test_small_batch_tail_mode_is_bit_exact(cfg, species, cap, monkeypatch):
     """Batches of at most one ray per SIMD (ART_SMALL_TAIL, default 1024 on the MI355X) run every
