@@ -72,15 +72,7 @@ struct DeviceCtx {
   };
   std::vector<Pinned> pinned;
   std::vector<hipEvent_t> pev;
-  // the streamed host pipeline (propagate_host_streamed): three CU-masked streams (each its
-  // own hardware queue) -- the integrator on all CUs but `reserve` of them, the uploads with
-  // the pieces' init kernels and the pieces' waits, finalize kernels and downloads on those
-  // `reserve` CUs; signal memory for the ready counter and the pieces' signals, the device
-  // array of the signal pointers, and a pinned word a wave raises when it gives up
-  hipStream_t s_comp = nullptr, s_in = nullptr, s_out = nullptr;
-  int reserve = 0;
-  std::vector<unsigned long long*> sigs;
-  unsigned long long** sig_dev = nullptr;
+  // a pinned word the streamed pipeline's waves raise when they give up
   unsigned int* abort_host = nullptr;
   unsigned int* abort_dev = nullptr;
   // the maskless streamed pipeline (propagate_host_maskless): plain streams for the integrator
@@ -291,11 +283,9 @@ void release_ctx(DeviceCtx& c) {
   for (hipEvent_t e : c.pev) (void)hipEventDestroy(e);
   for (hipStream_t s : c.pstreams)
     if (s && s != c.stream) (void)hipStreamDestroy(s);
-  for (hipStream_t s : {c.h2d, c.fin, c.s_comp, c.s_in, c.s_out, c.m_comp, c.m_up, c.m_dn, c.m_help})
+  for (hipStream_t s : {c.h2d, c.fin, c.m_comp, c.m_up, c.m_dn, c.m_help})
     if (s) (void)hipStreamDestroy(s);
   if (c.hsig) (void)hipHostFree(c.hsig);
-  for (unsigned long long* w : c.sigs) (void)hipFree(w);
-  if (c.sig_dev) (void)hipFree(c.sig_dev);
   if (c.abort_host) (void)hipHostFree(c.abort_host);
   if (c.stream) (void)hipStreamDestroy(c.stream);
   c = DeviceCtx();
@@ -904,310 +894,6 @@ int propagate_host_chunked(DeviceCtx* c, const art_params* p, int64_t n, const d
 // signal): the call's results are discarded and the batch runs again on another path.
 constexpr int STREAM_FALLBACK = 1 << 20;
 
-// The streamed pipeline's three streams, each its own hardware queue (a CU-masked stream gets
-// one; a stream that shared a queue could sit behind another's wait): the integrator's on all
-// CUs but `reserve`, the uploads' (with the pieces' init kernels) and the downloads' (with the
-// finalize kernels) on those `reserve` CUs, the last logical CUs of the device -- one per XCD
-// for reserve = 8 (tools/probe_cumask.hip). A helper mask must reach every XCD: a kernel's
-// blocks are dealt to the XCDs round-robin, and blocks dealt to an XCD without a CU of the mask
-// never run (8 CUs from one XCD: every call gave up, profiles/r03zd_streamed_reserve.txt).
-// Tried: helpers in block slots the integrator's grid leaves free (no masks): they fit only
-// with 32 free slots and an init kernel bounded to 256 VGPRs (94 spilled), and were no faster.
-int stream_setup(DeviceCtx* c, int reserve, int nsig) {
-  int ncu = 0;
-  HIP_OK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device));
-  // (reserve = 0, dev only: the three streams CU-masked with every CU, to time the masked queue itself)
-  if (reserve != 0 && (reserve < 8 || reserve % 8 != 0 || reserve >= ncu / 2))
-    return fail(ART_E_INVALID, "ART_HOST_RESERVE_CUS must be a multiple of 8 in [8, %s)", std::to_string(ncu / 2).c_str());
-  const int key = (reserve * 2 + (env_int("ART_HOST_RESERVE_XCD", 0) != 0 ? 1 : 0)) * 1024 +
-                  env_int("ART_HOST_RESERVE_AT", ncu - reserve);
-  if (!c->s_comp || c->reserve != key) {
-    for (hipStream_t* st : {&c->s_comp, &c->s_in, &c->s_out})
-      if (*st) {
-        HIP_OK(hipStreamSynchronize(*st));
-        HIP_OK(hipStreamDestroy(*st));
-        *st = nullptr;
-      }
-    const int words = (ncu + 31) / 32;
-    std::vector<uint32_t> mc(words, 0u), mh(words, 0u);
-    // (ART_HOST_RESERVE_XCD=1, dev: the reserved CUs from the last XCD -- logical CU i sits on
-    // XCD i % 8 -- which starves the helpers, see above)
-    const bool one_xcd = env_int("ART_HOST_RESERVE_XCD", 0) != 0;
-    int taken = 0;
-    for (int i = ncu - 1; i >= 0; --i) {
-      // (ART_HOST_RESERVE_AT=k, dev: the reserved CUs start at logical CU k instead of ncu - reserve)
-      const int at = env_int("ART_HOST_RESERVE_AT", ncu - reserve);
-      const bool res = one_xcd ? (taken < reserve && i % 8 == 7) : (i >= at && i < at + reserve);
-      taken += res;
-      (res ? mh : mc)[i / 32] |= 1u << (i % 32);
-      if (reserve == 0) mh[i / 32] |= 1u << (i % 32);
-    }
-    HIP_OK(hipExtStreamCreateWithCUMask(&c->s_comp, (uint32_t)words, mc.data()));
-    HIP_OK(hipExtStreamCreateWithCUMask(&c->s_in, (uint32_t)words, mh.data()));
-    HIP_OK(hipExtStreamCreateWithCUMask(&c->s_out, (uint32_t)words, mh.data()));
-    c->reserve = key;
-  }
-  if ((int)c->sigs.size() < nsig) {
-    while ((int)c->sigs.size() < nsig) {
-      void* w = nullptr;
-      HIP_OK(hipExtMallocWithFlags(&w, sizeof(unsigned long long), hipMallocSignalMemory));
-      c->sigs.push_back((unsigned long long*)w);
-    }
-    if (c->sig_dev) HIP_OK(hipFree(c->sig_dev));
-    HIP_OK(hipMalloc((void**)&c->sig_dev, sizeof(unsigned long long*) * c->sigs.size()));
-    HIP_OK(hipMemcpy(c->sig_dev, c->sigs.data(), sizeof(unsigned long long*) * c->sigs.size(), hipMemcpyHostToDevice));
-  }
-  if (!c->abort_host) {
-    HIP_OK(hipHostMalloc((void**)&c->abort_host, 64, hipHostMallocCoherent | hipHostMallocMapped));
-    HIP_OK(hipHostGetDevicePointer((void**)&c->abort_dev, c->abort_host, 0));
-  }
-  return ART_OK;
-}
-
-// art_propagate_host for large batches, streamed (the reference call site
-// MainRunner.jl:179-190 hands over host arrays): ONE integrator launch over the whole batch --
-// no per-chunk drain tails -- while its inputs still arrive and its outputs already leave.
-//   * the batch is cut into pieces of 2^shift rays (16-32 of them). The host gathers piece k
-//     from the caller's arrays into pinned staging (copy pool), the upload stream copies it to
-//     HBM, runs the piece's init_kernel and raises the ready counter (a stream write). The
-//     first piece is initialised on the integrator's CUs, ahead of it, so the integrator starts
-//     after one small piece's gather and copy;
-//   * the integrator (propagate_kernel<..., DON = 2>) runs on all CUs but `reserve`; a wave
-//     that claims rays beyond the ready counter waits for them. Every finished ray counts into
-//     its piece, and the wave that completes a piece raises the piece's signal;
-//   * the download stream waits for each piece's signal (hipStreamWaitValue64), finalizes the
-//     piece into its own SoA blob in HBM and copies the blob to pinned memory (DMA engines);
-//   * the host scatters the pieces into the caller's arrays as they land.
-// The init and finalize kernels run on the `reserve` CUs the integrator's stream leaves out
-// (three CU-masked streams, each its own hardware queue, so no queue order can hold one stream
-// behind another, stream_setup). Per-ray results do not depend on the launch split (tests/test_edges.py), so
-// the outputs equal the single launch's bit for bit. Any wait that outlasts its bound makes
-// the call fall back (STREAM_FALLBACK) instead of hanging.
-int propagate_host_streamed(DeviceCtx* c, const art_params* p, int64_t n, const double* x0, const double* k0,
-                            const double* erg, const double* dw, const double* ln_t0, const int8_t* species,
-                            int32_t max_crossings, art_segment_out* out, art_crossing_buf* xc, const FluxArgs& fx) {
-  const int cap = (xc && xc->count) ? xc->capacity : 0;
-  const art::KParams K = kparams(*p);
-  int shift = 16;
-  while (((int64_t)1 << (shift + 1)) * 16 <= n) ++shift;  // 16..32 pieces (2^19 rays for 10^7)
-  if (const int e = env_int("ART_HOST_PIECE_SHIFT", 0)) shift = std::max(6, e);  // (tests: many small pieces)
-  while (((n + ((int64_t)1 << shift) - 1) >> shift) > 64) ++shift;  // the scratch head holds 64 piece counters
-  const int np = (int)((n + ((int64_t)1 << shift) - 1) >> shift);
-  int rc;
-  const int reserve = env_int("ART_HOST_RESERVE_CUS", 8);
-  if ((rc = stream_setup(c, reserve, np + 1))) return rc;
-  int ncu = 0;
-  HIP_OK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device));
-  const size_t nd = (size_t)n;
-  auto up = [](size_t b) { return (b + 255) & ~size_t(255); };
-  // inputs, pinned and in HBM, in the device entry points' layout: x0 (3n) k0 (3n) erg dw lnt0 | species
-  const size_t in_bytes = nd * 9 * sizeof(double) + nd;
-  // per-piece output blobs (pinned and in HBM) as the chunked pipeline's
-  auto piece_lo = [&](int k) { return std::min((int64_t)k << shift, n); };
-  auto cnt_off = [&](int64_t m) { return up((size_t)m * 8 * sizeof(double) + (size_t)m * 3 * sizeof(int32_t)); };
-  auto xd_off = [&](int64_t m) { return cnt_off(m) + up((size_t)m * sizeof(int32_t)); };
-  auto out_bytes = [&](int64_t m) { return cap ? xd_off(m) + (size_t)cap * m * 9 * sizeof(double) : cnt_off(m); };
-  std::vector<size_t> ooff(np + 1, 0);
-  for (int k = 0; k < np; ++k) ooff[k + 1] = ooff[k] + up(out_bytes(piece_lo(k + 1) - piece_lo(k)));
-  // scratch: head [queue | stats (8) | piece counters from word 32] | u0 16n | rec 16n | xrec 8 cap n
-  const size_t head = 1024, u0b = nd * 16 * sizeof(double), recb = nd * art::END_REC * sizeof(double);
-  const size_t xrb = (size_t)cap * nd * art::X_REC * sizeof(double);
-  void *pi, *po, *din, *dout, *dsc;
-  if ((rc = pinned_get(c, 2, in_bytes, &pi)) || (rc = pinned_get(c, 3, ooff[np], &po)) ||
-      (rc = pool_get(c, 20, in_bytes, &din)) || (rc = pool_get(c, 21, ooff[np], &dout)) ||
-      (rc = pool_get(c, 22, head + u0b + recb + xrb, &dsc)))
-    return rc;
-  double* pin = (double*)pi;
-  double* di = (double*)din;
-  unsigned long long* words = (unsigned long long*)dsc;
-  double* u0 = (double*)((char*)dsc + head);
-  double* rec = (double*)((char*)dsc + head + u0b);
-  double* xrec = cap ? (double*)((char*)dsc + head + u0b + recb) : nullptr;
-  const art::SegIn in{di, di + 3 * nd, di + 6 * nd, di + 7 * nd, di + 8 * nd, (const int8_t*)(di + 9 * nd), u0};
-  unsigned long long* ready = c->sigs[np];
-  *c->abort_host = 0u;
-  while ((int64_t)c->pev.size() < np + 3) {
-    hipEvent_t ev;
-    HIP_OK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-    c->pev.push_back(ev);
-  }
-  hipEvent_t* ev_out = c->pev.data();
-  hipEvent_t ev_reset = c->pev[np], ev_go = c->pev[np + 1], ev_first = c->pev[np + 2];
-  const bool trace = env_int("ART_HOST_TRACE", 0) != 0;
-  auto clk = [] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
-  const double t_start = clk();
-  // counters and signals to zero, ahead of everything that reads them
-  HIP_OK(hipMemsetAsync(words, 0, head, c->s_in));
-  double* hist_dev = nullptr;
-  if (fx.nbins) {
-    if ((rc = pool_get(c, 23, 2 * (size_t)fx.nbins * sizeof(double), (void**)&hist_dev))) return rc;
-    HIP_OK(hipMemsetAsync(hist_dev, 0, 2 * (size_t)fx.nbins * sizeof(double), c->s_in));
-  }
-  for (int k = 0; k <= np; ++k) HIP_OK(hipStreamWriteValue64(c->s_in, c->sigs[k], 0ull, 0));
-  HIP_OK(hipEventRecord(ev_reset, c->s_in));
-  HIP_OK(hipStreamWaitEvent(c->s_out, ev_reset, 0));
-  using Seg = CopyPool::Seg;
-  auto upload = [&](int k) -> int {
-    const int64_t lo = piece_lo(k), m = piece_lo(k + 1) - lo;
-    const double* src[9] = {x0, x0 + n, x0 + 2 * n, k0, k0 + n, k0 + 2 * n, erg, dw, ln_t0};
-    std::vector<Seg> g;
-    for (int r = 0; r < 9; ++r) g.push_back({pin + r * nd + lo, src[r] + lo, (size_t)m * sizeof(double)});
-    g.push_back({(int8_t*)(pin + 9 * nd) + lo, species + lo, (size_t)m});
-    const double tg0 = clk();
-    copy_pool().run(g);
-    const double tg1 = clk();
-    for (int r = 0; r < 9; ++r)
-      HIP_OK(hipMemcpyAsync(di + r * nd + lo, pin + r * nd + lo, (size_t)m * sizeof(double), hipMemcpyHostToDevice,
-                            c->s_in));
-    HIP_OK(hipMemcpyAsync((int8_t*)(di + 9 * nd) + lo, (int8_t*)(pin + 9 * nd) + lo, (size_t)m, hipMemcpyHostToDevice,
-                          c->s_in));
-    if (k == 0) {  // the first piece: init on the integrator's stream, right before it
-      HIP_OK(hipEventRecord(ev_go, c->s_in));
-      HIP_OK(hipStreamWaitEvent(c->s_comp, ev_go, 0));
-    }
-    hipStream_t si = k == 0 ? c->s_comp : c->s_in;
-    HIP_OK(art::launch_init_range(K, n, lo, lo + m, in, words + 1, si));
-    HIP_OK(hipStreamWriteValue64(si, ready, (uint64_t)(lo + m), 0));
-    if (k == 0) {  // (the later pieces' writes of the counter come after this one)
-      HIP_OK(hipEventRecord(ev_first, c->s_comp));
-      HIP_OK(hipStreamWaitEvent(c->s_in, ev_first, 0));
-    }
-    if (trace)
-      std::fprintf(stderr, "[art-host] t=%.2f piece %d upload m=%lld gather %.2f ms submit %.2f ms\n", tg0 - t_start, k,
-                   (long long)m, tg1 - tg0, clk() - tg1);
-    return ART_OK;
-  };
-  if ((rc = upload(0))) return rc;
-  // (dev, ART_HOST_STREAM_SERIAL=1: every piece in HBM before the integrator starts)
-  const bool serial = env_int("ART_HOST_STREAM_SERIAL", 0) != 0;
-  for (int k = 1; serial && k < np; ++k)
-    if ((rc = upload(k))) return rc;
-  if (serial) {
-    HIP_OK(hipEventRecord(ev_go, c->s_in));
-    HIP_OK(hipStreamWaitEvent(c->s_comp, ev_go, 0));
-  }
-  // the integrator
-  LaunchRec* L;
-  if ((rc = take_slot(c, &L))) return rc;
-  art::SegOut so{};
-  so.rec = rec;
-  so.cap = cap;
-  so.xrec = xrec;
-  // (the integrator only tests xcount for null: crossings are recorded; finalize writes the counts)
-  so.xcount = cap ? (int32_t*)((char*)dout + cnt_off(piece_lo(1) - piece_lo(0))) : nullptr;
-  so.ready = ready;
-  so.piece_cnt = words + 32;
-  so.piece_sig = c->sig_dev;
-  so.abort_word = c->abort_dev;
-  so.piece_shift = shift;
-  HIP_OK(hipEventRecord(L->ev0, c->s_comp));
-  int blocks = 2 * (ncu - reserve);  // persistent: 2 per CU of the integrator's mask
-  if (const int b = env_int("ART_HOST_BLOCKS", 0)) blocks = std::max(1, b);  // (dev: grid A/B)
-  HIP_OK(art::launch_integrator_streamed(K, n, in, so, max_crossings, words, words + 1, blocks, c->s_comp, &L->grid));
-  HIP_OK(hipEventRecord(L->ev1, c->s_comp));
-  HIP_OK(hipMemcpyAsync(L->host_stats, words + 1, sizeof(unsigned long long) * art::N_STATS, hipMemcpyDeviceToHost,
-                        c->s_comp));
-  HIP_OK(hipEventRecord(L->done, c->s_comp));
-  L->pending = true;
-  c->last = c->next;
-  c->next = (c->next + 1) % RING;
-  c->launches += 1;
-  for (int k = 1; !serial && k < np; ++k)
-    if ((rc = upload(k))) return rc;
-  // the download side: each piece once its signal is up
-  for (int k = 0; k < np; ++k) {
-    const int64_t lo = piece_lo(k), m = piece_lo(k + 1) - lo;
-    char* db = (char*)dout + ooff[k];
-    double* dd = (double*)db;
-    int32_t* di32 = (int32_t*)(dd + 8 * m);
-    art::SegOut ol{};
-    ol.x_end = dd; ol.k_end = dd + 3 * m; ol.u7_end = dd + 6 * m; ol.tau_end = dd + 7 * m;
-    ol.status = di32; ol.n_acc = di32 + m; ol.n_rej = di32 + 2 * m;
-    ol.rec = rec;
-    if (cap) {
-      double* x = (double*)(db + xd_off(m));
-      ol.cap = cap;
-      ol.xcount = (int32_t*)(db + cnt_off(m));
-      ol.xpos = x; ol.xk = x + 3 * cap * m; ol.xt = x + 6 * cap * m; ol.xdw = x + 7 * cap * m; ol.xp = x + 8 * cap * m;
-      ol.xrec = xrec;
-      ol.nan_fill = 1;
-    }
-    HIP_OK(hipStreamWaitValue64(c->s_out, c->sigs[k], 1ull, hipStreamWaitValueGte));
-    HIP_OK(art::launch_finalize_range(K, n, lo, m, in, ol, c->s_out));
-    HIP_OK(hipMemcpyAsync((char*)po + ooff[k], db, out_bytes(m), hipMemcpyDeviceToHost, c->s_out));
-    if (fx.nbins)  // the piece's flux from its SoA blob while it is still in HBM
-      HIP_OK(art::launch_flux(K, m, ol.x_end, ol.k_end, ol.status, in.species + lo, nullptr, fx.nbins, hist_dev, c->s_out));
-    HIP_OK(hipEventRecord(ev_out[k], c->s_out));
-  }
-  // drain: wait for each piece (bounded), scatter it into the caller's arrays
-  const double limit_ms = (double)env_int("ART_HOST_STREAM_TIMEOUT_MS", 30000);
-  for (int k = 0; k < np; ++k) {
-    const double tw0 = clk();
-    bool gave_up = false;
-    for (;;) {
-      const hipError_t q = hipEventQuery(ev_out[k]);
-      if (q == hipSuccess) break;
-      if (q != hipErrorNotReady) return fail(ART_E_HIP, "streamed pipeline: %s", hipGetErrorString(q));
-      if (__atomic_load_n(c->abort_host, __ATOMIC_ACQUIRE) != 0u || clk() - tw0 > limit_ms) {
-        gave_up = true;
-        break;
-      }
-      std::this_thread::sleep_for(std::chrono::microseconds(20));
-    }
-    if (gave_up) {
-      // release every wait this call queued, let the three streams run out, and leave the
-      // batch to another path
-      for (int j = 0; j < np; ++j) HIP_OK(hipStreamWriteValue64(c->stream, c->sigs[j], 1ull, 0));
-      HIP_OK(hipStreamWriteValue64(c->stream, ready, (uint64_t)n, 0));
-      HIP_OK(hipStreamSynchronize(c->stream));
-      HIP_OK(hipStreamSynchronize(c->s_comp));
-      HIP_OK(hipStreamSynchronize(c->s_in));
-      HIP_OK(hipStreamSynchronize(c->s_out));
-      std::fprintf(stderr, "[art] streamed host pipeline gave up at piece %d of %d (abort=%u); running the batch again\n",
-                   k, np, *c->abort_host);
-      return STREAM_FALLBACK;
-    }
-    const double tw1 = clk();
-    const int64_t lo = piece_lo(k), m = piece_lo(k + 1) - lo;
-    const char* bo = (const char*)po + ooff[k];
-    const double* d = (const double*)bo;
-    const int32_t* i32 = (const int32_t*)(d + 8 * m);
-    std::vector<Seg> g;
-    for (int q = 0; q < 3; ++q) {
-      g.push_back({out->x_end + q * n + lo, d + q * m, m * sizeof(double)});
-      g.push_back({out->k_end + q * n + lo, d + (3 + q) * m, m * sizeof(double)});
-    }
-    g.push_back({out->u7_end + lo, d + 6 * m, m * sizeof(double)});
-    g.push_back({out->tau_end + lo, d + 7 * m, m * sizeof(double)});
-    g.push_back({out->status + lo, i32, m * sizeof(int32_t)});
-    g.push_back({out->n_accept + lo, i32 + m, m * sizeof(int32_t)});
-    g.push_back({out->n_reject + lo, i32 + 2 * m, m * sizeof(int32_t)});
-    if (cap) {
-      g.push_back({xc->count + lo, bo + cnt_off(m), m * sizeof(int32_t)});
-      const double* x = (const double*)(bo + xd_off(m));
-      for (int r = 0; r < 3 * cap; ++r) {
-        g.push_back({xc->pos + r * n + lo, x + r * m, m * sizeof(double)});
-        g.push_back({xc->k + r * n + lo, x + (3 * cap + r) * m, m * sizeof(double)});
-      }
-      for (int r = 0; r < cap; ++r) {
-        g.push_back({xc->t + r * n + lo, x + (6 * cap + r) * m, m * sizeof(double)});
-        g.push_back({xc->dw + r * n + lo, x + (7 * cap + r) * m, m * sizeof(double)});
-        g.push_back({xc->p_nonad + r * n + lo, x + (8 * cap + r) * m, m * sizeof(double)});
-      }
-    }
-    copy_pool().run(g);
-    if (trace)
-      std::fprintf(stderr, "[art-host] t=%.2f piece %d drain wait %.2f ms scatter %.2f ms\n", tw0 - t_start, k,
-                   tw1 - tw0, clk() - tw1);
-  }
-  if (trace) std::fprintf(stderr, "[art-host] streamed total %.2f ms (%d pieces of 2^%d)\n", clk() - t_start, np, shift);
-  if (fx.nbins) {
-    HIP_OK(hipMemcpyAsync(fx.hist, hist_dev, 2 * (size_t)fx.nbins * sizeof(double), hipMemcpyDeviceToHost, c->s_out));
-    HIP_OK(hipStreamSynchronize(c->s_out));
-  }
-  return finish_timing(c);
-}
-
 // art_propagate_host for large batches, streamed with no CU reserved (the default; SURVEY §8b,
 // the reference call site MainRunner.jl:179-190 hands over host arrays). ONE integrator launch
 // (propagate_kernel<..., DON = 3>) holds every CU for the whole batch; nothing else needs a CU
@@ -1225,9 +911,9 @@ int propagate_host_streamed(DeviceCtx* c, const art_params* p, int64_t n, const 
 //     scatters it into the caller's arrays.
 // Helper blocks (SegOut::helpers) do the init and finalize tiles while the rest integrate; the
 // blocks whose waves run out of rays join them (art_kernels.hip, s3_helper).
-// The CU-masked pipeline it replaces (propagate_host_streamed, ART_HOST_MODE=stream_masked) ran
-// the init and finalize kernels on 8 reserved CUs, which cost ~10% of the integrator
-// (profiles/r04g_stream_anatomy.jsonl). Per-ray results equal the single launch's bit for bit.
+// Round 3's CU-masked pipeline ran the init and finalize kernels on 8 reserved CUs, which cost
+// ~10% of the integrator (profiles/r04g_stream_anatomy.jsonl); it is gone. Per-ray results
+// equal the single launch's bit for bit.
 int propagate_host_maskless(DeviceCtx* c, const art_params* p, int64_t n, const double* x0, const double* k0,
                             const double* erg, const double* dw, const double* ln_t0, const int8_t* species,
                             int32_t max_crossings, art_segment_out* out, art_crossing_buf* xc, const FluxArgs& fx) {
@@ -1375,7 +1061,7 @@ int propagate_host_maskless(DeviceCtx* c, const art_params* p, int64_t n, const 
     HIP_OK(art::launch_helpers(K, n, in, so, serial ? slots : slots - helpers, first, 0, words + 1, c->m_comp));
   HIP_OK(hipEventRecord(L->ev0, c->m_comp));
   HIP_OK(art::launch_integrator_streamed(K, n, in, so, max_crossings, words, words + 1, serial ? slots : slots - helpers,
-                                         c->m_comp, &L->grid, true));
+                                         c->m_comp, &L->grid));
   HIP_OK(hipEventRecord(L->ev1, c->m_comp));
   HIP_OK(art::launch_helpers(K, n, in, so, slots, -1, 0, words + 1, c->m_comp));
   hipEvent_t ev_help = c->pev[nu + np + 1];  // (the persistent helpers' init counts, in the statistics)
@@ -1585,9 +1271,8 @@ int propagate_host_impl(const art_params* p, int64_t n, const double* x0, const 
   const char* mode_env = std::getenv("ART_HOST_MODE");
   const std::string mode = (mode_env && *mode_env) ? mode_env : "stream";
   if (htr.ntimes == 0 && n >= env_int("ART_HOST_CHUNK_MIN", 1 << 20)) {
-    if ((mode == "stream" || mode == "stream_masked") && p->integrator == ART_VERN6) {
-      rc = mode == "stream" ? propagate_host_maskless(c, p, n, x0, k0, erg, dw, ln_t0, species, max_crossings, out, xc, fx)
-                            : propagate_host_streamed(c, p, n, x0, k0, erg, dw, ln_t0, species, max_crossings, out, xc, fx);
+    if (mode == "stream" && p->integrator == ART_VERN6) {
+      rc = propagate_host_maskless(c, p, n, x0, k0, erg, dw, ln_t0, species, max_crossings, out, xc, fx);
       if (rc != STREAM_FALLBACK) {
         if (rc == ART_OK) g_host_cnt[HC_STREAMED] += 1;
         return rc;
@@ -1614,10 +1299,6 @@ int propagate_host_impl(const art_params* p, int64_t n, const double* x0, const 
   if (cap && (rc = pool_get(c, 2, xc_bytes, &dxc))) return rc;
   double* di = (double*)din;
   hipStream_t s = c->stream;
-  if (const int r = env_int("ART_DEV_SINGLE_MASKED", 0)) {  // (dev: the single launch on a CU-masked stream;
-    if ((rc = stream_setup(c, r < 0 ? 0 : r, 1))) return rc;  //  -1: masked with every CU)
-    s = c->s_comp;
-  }
   HIP_OK(hipMemcpyAsync(di, x0, nd * 3 * sizeof(double), hipMemcpyHostToDevice, s));
   HIP_OK(hipMemcpyAsync(di + 3 * nd, k0, nd * 3 * sizeof(double), hipMemcpyHostToDevice, s));
   HIP_OK(hipMemcpyAsync(di + 6 * nd, erg, nd * sizeof(double), hipMemcpyHostToDevice, s));

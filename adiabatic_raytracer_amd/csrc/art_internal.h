@@ -53,16 +53,10 @@ struct SegOut {
   // 1: finalize_kernel writes NaN into the crossing slots j >= min(count, cap) (the *_host
   // entry points' contract, include/art.h), so no fill of the outputs is needed beforehand
   int32_t nan_fill;
-  // The streamed host pipeline (propagate_kernel<..., DON = 2>, art_propagate_host): one
-  // integrator launch over the whole batch while its inputs are still arriving and its
-  // outputs already leave. Rays [0, *ready) have their fresh state in HBM (a stream write
-  // raises *ready after each piece's init_kernel); a wave waits for its chunk (at most
-  // STREAM_WAIT_TICKS of s_memrealtime, then it sets *abort and stops: the host falls back).
-  // Piece p = ray >> piece_shift; every finished ray counts into piece_cnt[p], and the wave
-  // that completes a piece sets *piece_sig[p] = 1 (signal memory a finalize stream waits on).
-  const unsigned long long* ready;
+  // The streamed host pipeline (propagate_kernel<..., DON = 3>, art_propagate_host): piece
+  // p = ray >> piece_shift; every finished ray counts into piece_cnt[p]; a wave that waits too
+  // long (STREAM_WAIT_TICKS of s_memrealtime) raises *abort_word and stops taking rays.
   unsigned long long* piece_cnt;
-  unsigned long long* const* piece_sig;
   unsigned int* abort_word;
   int32_t piece_shift;
   // The maskless streamed pipeline (DON = 3, art_capi.cpp propagate_host_maskless): one launch
@@ -113,21 +107,15 @@ int persistent_blocks(const void* func, int64_t work, int block, int fallback_pe
 hipError_t launch_propagate(const KParams& P, int64_t n, const SegIn& in, const SegOut& out, int32_t max_crossings,
                             unsigned long long* queue, unsigned long long* stats, hipStream_t s, int* grid_out,
                             hipEvent_t ev0, hipEvent_t ev1, hipStream_t fs = nullptr);
-// The streamed host pipeline's launches (art_capi.cpp, propagate_host_streamed): init of rays
-// [i0, i1); the integrator (DON = 2) with at most `blocks` persistent blocks; finalize of rays
-// [i0, i0 + m) into piece-local SoA outputs `ol` (row stride m).
-hipError_t launch_init_range(const KParams& P, int64_t n, int64_t i0, int64_t i1, const SegIn& in,
-                             unsigned long long* stats, hipStream_t s);
+// The streamed host pipeline's integrator (DON = 3) with at most `blocks` persistent blocks.
 hipError_t launch_integrator_streamed(const KParams& P, int64_t n, const SegIn& in, const SegOut& out,
                                       int32_t max_crossings, unsigned long long* queue, unsigned long long* stats,
-                                      int blocks, hipStream_t s, int* grid_out, bool maskless = false);
+                                      int blocks, hipStream_t s, int* grid_out);
 // The maskless streamed pipeline's helper duty (helper_kernel HK_TILES, SegOut::host_ready ...):
 // `blocks` blocks; init_limit >= 0 initialises only (tiles below it), -1 serves to the end;
 // announce counts each block into host_flags[64] as it starts.
 hipError_t launch_helpers(const KParams& P, int64_t n, const SegIn& in, const SegOut& out, int blocks, int64_t init_limit,
                           int announce, unsigned long long* stats, hipStream_t s);
-hipError_t launch_finalize_range(const KParams& P, int64_t n, int64_t i0, int64_t m, const SegIn& in,
-                                 const SegOut& ol, hipStream_t s);
 // The batch size up to which launch_propagate runs every ray on a wave of its own (tail_kernel):
 // ART_SMALL_TAIL, default one ray per SIMD of the device; 0 switches it off.
 int64_t small_tail_limit();

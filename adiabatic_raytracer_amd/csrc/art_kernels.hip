@@ -383,7 +383,7 @@ constexpr int SCAN_WORDS = 4;  // 2-bit codes for up to 64 grid points (interp_p
 #define ART_WAVES_PER_SIMD 2
 #endif
 #ifndef ART_STREAM_FLUSH
-// (DON = 2) a wave's finished-ray counts go out every 128 iterations (~2.5 ms of a flat ray's
+// (DON = 3) a wave's finished-ray counts go out every 128 iterations (~2.5 ms of a flat ray's
 // steps; every 8: -3%, every 32: -1%, profiles/r03sg_flush.jsonl)
 #define ART_STREAM_FLUSH 127
 #endif
@@ -402,75 +402,17 @@ constexpr int SCAN_WORDS = 4;  // 2-bit codes for up to 64 grid points (interp_p
 // boundary-layer and isotropic branches fold away, and rs != 0 is assumed.
 enum { GEOM_ANY = 0, GEOM_FLAT = 1, GEOM_GR = 2 };
 
-// The streamed host pipeline (DON = 2): the fresh state of rays [0, need) is in HBM once
-// *out.ready >= need (a stream write after each piece's init_kernel). The leader lane polls it
-// (system scope: the command processor writes it), at most STREAM_WAIT_TICKS; on time-out, or
-// when another wave gave up, it raises *out.abort_word and the wave stops taking rays (the host
-// then discards the call's results and runs the batch again without streaming).
-__device__ inline bool stream_ready(const SegOut& out, int64_t need, int leader) {
-  int ok = 1;
-  if ((int)(threadIdx.x & 63) == leader) {  // (a wave with nothing else to integrate)
-    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-    while (__hip_atomic_load(out.ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < (unsigned long long)need) {
-      if (__hip_atomic_load(out.abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u ||
-          __builtin_amdgcn_s_memrealtime() - t0 > STREAM_WAIT_TICKS) {
-        __hip_atomic_store(out.abort_word, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        ok = 0;
-        break;
-      }
-      __builtin_amdgcn_s_sleep(64);
-    }
-  }
-  return __shfl(ok, leader) != 0;
-}
-
-// the ready counter as one lane reads it now, returned in a scalar register (ray indices are
-// 32-bit in the integrator; the streamed kernel is short of vector registers)
-__device__ inline int stream_poll(const SegOut& out, int leader) {
-  unsigned long long r = 0;
-  if ((int)(threadIdx.x & 63) == leader) r = __hip_atomic_load(out.ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
-  return __builtin_amdgcn_readlane((int)r, leader);
-}
-
-// A wave's finished rays of piece p, counted c at a time: the wave's record stores are released
-// first (agent scope: the end and crossing records reach memory every XCD reads), then the
-// count; the count that completes the piece raises the piece's signal. Waves batch their
-// counts (at most every 128 iterations, at a piece change and at exit), so the L2 write-backs of
-// the release stay rare.
-__device__ inline void stream_count(const SegOut& out, int64_t n, int p, unsigned long long c) {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the write-back done before the count, always)
-  const int leader = __ffsll((long long)__ballot(1)) - 1;
-  if ((int)(threadIdx.x & 63) == leader) {
-    const unsigned long long old = __hip_atomic_fetch_add(out.piece_cnt + p, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int64_t lo = (int64_t)p << out.piece_shift;
-    const int64_t hi = (lo + ((int64_t)1 << out.piece_shift)) < n ? lo + ((int64_t)1 << out.piece_shift) : n;
-    if ((int64_t)(old + c) == hi - lo && out.piece_sig) {  // the piece's last count: every wave's records are out
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      __hip_atomic_store(out.piece_sig[p], 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-  }
-}
-
-// (DON = 2, 3) a wave's LDS histogram of finished rays per piece (lane l: piece l) into the
+// (DON = 3) a wave's LDS histogram of finished rays per piece (lane l: piece l) into the
 // pieces' global counts: the wave's end-record stores released once (agent scope), then one
-// atomic add per piece with a count; the add that completes a piece raises its signal
-// (piece_sig, when the pipeline has one: the DON = 3 helpers poll piece_cnt itself)
-__device__ inline void stream_flush(const SegOut& out, int64_t n, unsigned* hist, int lane) {
+// atomic add per piece with a count (the helpers poll piece_cnt)
+__device__ inline void stream_flush(const SegOut& out, unsigned* hist, int lane) {
   const unsigned c = hist[lane];
   if (__ballot(c != 0u) == 0ull) return;
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the write-back done before the counts, always)
   if (c != 0u) {
     hist[lane] = 0u;
-    const unsigned long long old =
-        __hip_atomic_fetch_add(out.piece_cnt + lane, (unsigned long long)c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int64_t lo = (int64_t)lane << out.piece_shift;
-    const int64_t hi = (lo + ((int64_t)1 << out.piece_shift)) < n ? lo + ((int64_t)1 << out.piece_shift) : n;
-    if ((int64_t)(old + c) == hi - lo && out.piece_sig) {  // the piece's last count: every wave's records are out
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      __hip_atomic_store(out.piece_sig[lane], 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
+    __hip_atomic_fetch_add(out.piece_cnt + lane, (unsigned long long)c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -718,14 +660,14 @@ __global__ __launch_bounds__(BLOCK, WPS) void propagate_kernel(const KParams P_i
   __shared__ double lastt[BLOCK];                 // t at the step's end (the scan certificate)
   __shared__ unsigned char srcl[BLOCK];           // compact list of the wave's scanning lanes
   __shared__ double thgrid[SCAN_WORDS * 16 + 1];  // Θs = j/(npts-1): range(0, 1, length = npts)
-  __shared__ unsigned pend_lds[BLOCK / 64][64];  // (DON = 2, 3) per wave: finished rays per piece, not yet counted
+  __shared__ unsigned pend_lds[BLOCK / 64][64];  // (DON = 3) per wave: finished rays per piece, not yet counted
   double* const L = lds + threadIdx.x;
   const int wbase = threadIdx.x & ~63;
   const int lane = threadIdx.x & 63;
   const double tend = P.ln_t_end;
   const int npts = P.interp_points;
   for (int j = threadIdx.x; j < npts; j += BLOCK) thgrid[j] = double(j) / double(npts - 1);
-  if constexpr (DON >= 2) pend_lds[threadIdx.x >> 6][threadIdx.x & 63] = 0u;
+  if constexpr (DON == 3) pend_lds[threadIdx.x >> 6][threadIdx.x & 63] = 0u;
   __syncthreads();
 
   int mode = M_IDLE;
@@ -744,8 +686,7 @@ __global__ __launch_bounds__(BLOCK, WPS) void propagate_kernel(const KParams P_i
   double hroot = 0.0, r_tha = 0.0, r_ca = 0.0, r_thb = 0.0, r_cb = 0.0, r_t = 0.0, r_slope = 1.0, post_c = 0.0;
   int post_s = 0, r_side = 0, r_it = 0;
   int wnext = 0, wend = 0;
-  int rdy = 0;                           // (DON = 2) the ready counter as last read
-  int tick = 0;                          // (DON = 2, 3) iterations, for the flushes of the piece counts
+  int tick = 0;                          // (DON = 3) iterations, for the flushes of the piece counts
   bool cready = false;                   // (DON = 3) the claimed chunk's fresh state is in
   int save_k = 1;  // SAVE: the next interior saveat index
   bool exhausted = false;
@@ -830,18 +771,6 @@ __global__ __launch_bounds__(BLOCK, WPS) void propagate_kernel(const KParams P_i
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
             cready = true;
           }
-        }
-        if constexpr (DON == 2) {
-          // only rays whose fresh state has arrived; while none of the chunk has, a wave with
-          // other rays goes on integrating them, and an empty wave waits (bounded)
-          const int leader = __ffsll((long long)need) - 1;
-          if (rdy < wend) rdy = stream_poll(out, leader);
-          if (rdy <= wnext) {
-            if (__ballot(mode != M_IDLE) != 0ull) break;
-            if (!stream_ready(out, wnext + 1, leader)) { exhausted = true; break; }
-            rdy = stream_poll(out, leader);
-          }
-          lim = rdy < wend ? rdy : wend;
         }
         const int rank = __popcll(need & ((1ull << lane) - 1ull));
         const int cnt = __popcll(need);
@@ -1577,9 +1506,9 @@ __global__ __launch_bounds__(BLOCK, WPS) void propagate_kernel(const KParams P_i
       else if (iter >= P.maxiters) finish = ART_STATUS_MAXITERS;
     }
 
-    int fin_piece = -1;  // (DON = 2) the piece of a ray finishing now
+    int fin_piece = -1;  // (DON = 3) the piece of a ray finishing now
     if (finish >= 0) {  // the raw end record; finalize_kernel back-transforms it (RayTracer.jl:393-416)
-      if constexpr (DON >= 2) fin_piece = ray >> out.piece_shift;
+      if constexpr (DON == 3) fin_piece = ray >> out.piece_shift;
       double2* rq = reinterpret_cast<double2*>(out.rec + (int64_t)ray * END_REC);
       rq[0] = make_double2(u[0], u[1]);
       rq[1] = make_double2(u[2], u[3]);
@@ -1592,7 +1521,7 @@ __global__ __launch_bounds__(BLOCK, WPS) void propagate_kernel(const KParams P_i
       mode = M_IDLE;
     }
 #ifndef ART_S_NOCOUNT  // (dev A/B: no piece counts)
-    if constexpr (DON >= 2) {
+    if constexpr (DON == 3) {
 #else
     if constexpr (DON >= 99) {
 #endif
@@ -1608,7 +1537,7 @@ __global__ __launch_bounds__(BLOCK, WPS) void propagate_kernel(const KParams P_i
 #endif
       ++tick;
       if ((tick & ART_STREAM_FLUSH) == 0 || (exhausted && (tick & ART_DRAIN_FLUSH_MASK) == 0))
-        stream_flush(out, n, pend_lds[threadIdx.x >> 6], lane);
+        stream_flush(out, pend_lds[threadIdx.x >> 6], lane);
     }
     ART_TMARK(0)  // saveat, reload, events, finish and the output stores (+ refill)
     // graduation (SegOut::graduate): a ray past `graduate` attempts, at a step boundary, leaves
@@ -1652,7 +1581,7 @@ __global__ __launch_bounds__(BLOCK, WPS) void propagate_kernel(const KParams P_i
     }
   }
 
-  if constexpr (DON >= 2) stream_flush(out, n, pend_lds[threadIdx.x >> 6], lane);
+  if constexpr (DON == 3) stream_flush(out, pend_lds[threadIdx.x >> 6], lane);
 
   // wave-reduce the statistics and add them once per wave
 #if defined(ART_SLOT_TIMING)
@@ -3172,12 +3101,11 @@ hipError_t launch_propagate(const KParams& P, int64_t n, const SegIn& in, const 
   }
   KFn fn = out.donate > 0 ? pick_propagate<1>(out.ntimes >= 2, rk4, flat, sch)
                            : pick_propagate<0>(out.ntimes >= 2, rk4, flat, sch);
-  // (dev A/B, ART_DEV_STREAMED_KERNEL=2|3: the streamed pipelines' integrator builds on a
-  // device-resident batch -- every chunk flagged in, every input ready -- to price their extra
-  // code against this launch's own)
+  // (dev A/B, ART_DEV_STREAMED_KERNEL=3: the streamed pipeline's integrator build on a
+  // device-resident batch -- every chunk flagged in -- to price its extra code against this
+  // launch's own, profiles/r04s3_streamed_kernel_ab.jsonl)
   if (const char* e = std::getenv("ART_DEV_STREAMED_KERNEL")) {
-    const int don = std::atoi(e);
-    if ((don == 2 || don == 3) && flat && !rk4 && out.ntimes < 2 && out.donate <= 0) {
+    if (std::atoi(e) == 3 && flat && !rk4 && out.ntimes < 2 && out.donate <= 0) {
       static void* dbuf = nullptr;
       static size_t dbytes = 0;
       const size_t need = 4096 + ((size_t)n / CHUNK + 1) * sizeof(unsigned);
@@ -3190,20 +3118,11 @@ hipError_t launch_propagate(const KParams& P, int64_t n, const SegIn& in, const 
       (void)hipMemsetAsync(w, 0, 4096, s);
       (void)hipMemsetAsync((char*)dbuf + 4096, 1, need - 4096, s);
       out.piece_cnt = w + 32;
-      out.piece_sig = nullptr;
       out.piece_shift = 19;
       out.chunk_ready = (unsigned*)((char*)dbuf + 4096);
       out.init_next = w + 16;
-      static unsigned long long* rdy = nullptr;
-      if (!rdy) {
-        (void)hipMalloc((void**)&rdy, 8);
-      }
-      const unsigned long long big = ~0ull >> 1;
-      (void)hipMemcpyAsync(rdy, &big, 8, hipMemcpyHostToDevice, s);
-      (void)hipStreamSynchronize(s);
-      out.ready = rdy;
       out.abort_word = (unsigned*)(w + 8 * 60);
-      fn = don == 2 ? propagate_kernel<ART_VERN6, GEOM_FLAT, false, 2> : propagate_kernel<ART_VERN6, GEOM_FLAT, false, 3>;
+      fn = propagate_kernel<ART_VERN6, GEOM_FLAT, false, 3>;
     }
   }
   // A batch that fits one ray per lane of 1 wave per SIMD runs the 1-wave/SIMD build, which
@@ -3281,29 +3200,16 @@ hipError_t launch_propagate(const KParams& P, int64_t n, const SegIn& in, const 
   return hipGetLastError();
 }
 
-hipError_t launch_init_range(const KParams& P, int64_t n, int64_t i0, int64_t i1, const SegIn& in,
-                             unsigned long long* stats, hipStream_t s) {
-  const int64_t gr = (i1 - i0 + 255) / 256;
-  if (gr <= 0) return hipSuccess;
-  hipLaunchKernelGGL(helper_kernel, dim3((unsigned)(gr < 2048 ? gr : 2048)), dim3(256), 0, s, P, n, in, SegOut{},
-                     (int)HK_INIT, i0, i1, (int64_t)-1, 0, stats);
-  return hipGetLastError();
-}
-
 // The streamed pipeline's integrator: Vern6 (flat / GR / general geometry), no saveat, no
 // donation, at most `blocks` persistent blocks (the block slots it leaves free run the init and
 // finalize kernels of the pieces).
 hipError_t launch_integrator_streamed(const KParams& P, int64_t n, const SegIn& in, const SegOut& out,
                                       int32_t max_crossings, unsigned long long* queue, unsigned long long* stats,
-                                      int blocks, hipStream_t s, int* grid_out, bool maskless) {
+                                      int blocks, hipStream_t s, int* grid_out) {
   const bool flat = P.rs_eff == 0.0 && !(P.bndry_lyr > 0.0) && !P.isotropic;
   const bool sch = P.rs_eff > 0.0 && !(P.bndry_lyr > 0.0) && !P.isotropic;
-  const KFn fn = maskless ? (flat ? propagate_kernel<ART_VERN6, GEOM_FLAT, false, 3>
-                                  : (sch ? propagate_kernel<ART_VERN6, GEOM_GR, false, 3>
-                                         : propagate_kernel<ART_VERN6, GEOM_ANY, false, 3>))
-                          : (flat ? propagate_kernel<ART_VERN6, GEOM_FLAT, false, 2>
-                                  : (sch ? propagate_kernel<ART_VERN6, GEOM_GR, false, 2>
-                                         : propagate_kernel<ART_VERN6, GEOM_ANY, false, 2>));
+  const KFn fn = flat ? propagate_kernel<ART_VERN6, GEOM_FLAT, false, 3>
+                      : (sch ? propagate_kernel<ART_VERN6, GEOM_GR, false, 3> : propagate_kernel<ART_VERN6, GEOM_ANY, false, 3>);
   const int64_t need = (n + BLOCK - 1) / BLOCK;
   const int grid = (int)(need < (int64_t)blocks ? need : (int64_t)blocks);
   if (grid_out) *grid_out = grid;
@@ -3315,14 +3221,6 @@ hipError_t launch_helpers(const KParams& P, int64_t n, const SegIn& in, const Se
                           int announce, unsigned long long* stats, hipStream_t s) {
   hipLaunchKernelGGL(helper_kernel, dim3((unsigned)blocks), dim3(256), 0, s, P, n, in, out, (int)HK_TILES, (int64_t)0, n,
                      init_limit, announce, stats);
-  return hipGetLastError();
-}
-
-hipError_t launch_finalize_range(const KParams& P, int64_t n, int64_t i0, int64_t m, const SegIn& in,
-                                 const SegOut& ol, hipStream_t s) {
-  if (m <= 0) return hipSuccess;
-  hipLaunchKernelGGL(helper_kernel, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, P, n, in, ol, (int)HK_FIN, i0,
-                     i0 + m, (int64_t)-1, 0, nullptr);
   return hipGetLastError();
 }
 

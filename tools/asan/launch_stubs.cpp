@@ -9,16 +9,10 @@ hipError_t launch_propagate(const KParams&, int64_t, const SegIn&, const SegOut&
                             unsigned long long*, hipStream_t, int*, hipEvent_t, hipEvent_t, hipStream_t) {
   return hipErrorNoDevice;
 }
-hipError_t launch_init_range(const KParams&, int64_t, int64_t, int64_t, const SegIn&, unsigned long long*, hipStream_t) {
-  return hipErrorNoDevice;
-}
 hipError_t launch_integrator_streamed(const KParams&, int64_t, const SegIn&, const SegOut&, int32_t, unsigned long long*,
-                                      unsigned long long*, int, hipStream_t, int*, bool) { return hipErrorNoDevice; }
+                                      unsigned long long*, int, hipStream_t, int*) { return hipErrorNoDevice; }
 hipError_t launch_helpers(const KParams&, int64_t, const SegIn&, const SegOut&, int, int64_t, int, unsigned long long*,
                           hipStream_t) {
-  return hipErrorNoDevice;
-}
-hipError_t launch_finalize_range(const KParams&, int64_t, int64_t, int64_t, const SegIn&, const SegOut&, hipStream_t) {
   return hipErrorNoDevice;
 }
 int64_t small_tail_limit() { return 0; }

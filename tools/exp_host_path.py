@@ -2,9 +2,8 @@
 batch, for several pipeline settings (ART_HOST_CHUNKS / ART_HOST_SLOTS / ART_HOST_THREADS are
 read per call). Prints one JSON line per setting; with ART_HOST_TRACE=1 the library also
 prints the host side of every chunk to stderr.
-Usage: exp_host_path.py [rays] [setting ...]; a setting is "stream" (the maskless streamed
-pipeline), "masked" or "masked:R" (the CU-masked one, R reserved CUs), "single", or
-"chunks,slots" (the chunked pipeline), e.g.
+Usage: exp_host_path.py [rays] [setting ...]; a setting is "stream" (the streamed pipeline),
+"single", or "chunks,slots" (the chunked pipeline), e.g.
 exp_host_path.py 10000000 stream single 4,2"""
 import ctypes as C
 import json
@@ -47,10 +46,8 @@ cp = eng.cp
 ref = None
 for setting in settings:
     chunks = slots = 0
-    if setting.startswith("stream") or setting.startswith("masked"):
-        # "stream": the maskless pipeline (the default); "masked[:R]": the CU-masked one, R reserved CUs
-        os.environ["ART_HOST_MODE"] = "stream" if setting.startswith("stream") else "stream_masked"
-        os.environ["ART_HOST_RESERVE_CUS"] = setting.split(":")[1] if ":" in setting else "8"
+    if setting == "stream":
+        os.environ["ART_HOST_MODE"] = "stream"
     elif setting == "single":
         os.environ["ART_HOST_MODE"] = "single"
     else:

@@ -18,9 +18,10 @@ for grp in "FETCH_SIZE" "WRITE_SIZE" \
            "SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_TRANS_F64" \
            "SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_INST_ANY SQ_WAIT_ANY"; do
   i=$((i+1))
-  # (counter collection serialises the kernels, so the streamed host pipeline's integrator must
-  # not wait for another kernel: ART_HOST_STREAM_SERIAL=1 puts every piece in HBM first; its
-  # code and its traffic are the streamed instantiation's all the same)
+  # (counter collection serialises the kernels, so the streamed host pipeline must not hand off
+  # between concurrent kernels: ART_HOST_STREAM_SERIAL=1 initialises every tile before the
+  # integrator and finalizes after it, with no persistent helpers; the integrator's code and
+  # traffic are the streamed instantiation's all the same)
   ART_HOST_STREAM_SERIAL=1 timeout -k 10 300 rocprofv3 --kernel-trace --pmc $grp -d "$OUT/kernel/pass$i" -o pass$i \
     --output-format csv -- python3 bench.py --rays "$RAYS" --steps 1 --warmup 0 --no-cpu-baseline > "$OUT/pass$i.log" 2>&1 \
     || { echo "pass $i ($grp) failed"; exit 1; }
