@@ -978,12 +978,17 @@ int propagate_host_maskless(DeviceCtx* c, const art_params* p, int64_t n, const 
   double* rec = (double*)((char*)dsc + head + ccb + u0b);
   double* xrec = cap ? (double*)((char*)dsc + head + ccb + u0b + recb) : nullptr;
   const art::SegIn in{di, di + 3 * nd, di + 6 * nd, di + 7 * nd, di + 8 * nd, (const int8_t*)(di + 9 * nd), u0};
-  // upload units: the first piece in four parts (the integrator starts on the first quarter),
-  // then one unit per piece
-  std::vector<int64_t> ulo;
-  for (int q = 0; q < 4; ++q) ulo.push_back(piece_lo(1) * q / 4 / art::CHUNK * art::CHUNK);
-  for (int k = 1; k <= np; ++k) ulo.push_back(piece_lo(k));
-  ulo.erase(std::unique(ulo.begin(), ulo.end()), ulo.end());
+  // upload units (independent of the output pieces): a small first one (2^16 rays, the
+  // integrator starts soon), then units of max(2^18 rays, a piece) -- each unit costs ~0.2 ms of
+  // host-side submission, which small pieces made the bound of a 1.25e6-ray call's uploads
+  // (ART_HOST_FIRST_UNIT / ART_HOST_UNIT: tests, other sizes in rays)
+  std::vector<int64_t> ulo{0};
+  const int64_t ustep = std::max(1, env_int("ART_HOST_UNIT", (int)std::max((int64_t)1 << 18, (int64_t)1 << shift)));
+  for (int64_t lo = std::min(n, (int64_t)std::max(1, env_int("ART_HOST_FIRST_UNIT", 1 << 16))); ;
+       lo = std::min(n, lo + ustep)) {
+    ulo.push_back(lo);
+    if (lo >= n) break;
+  }
   const int nu = (int)ulo.size() - 1;
   while ((int64_t)c->pev.size() < nu + np + 2) {
     hipEvent_t ev;
@@ -1016,6 +1021,9 @@ int propagate_host_maskless(DeviceCtx* c, const art_params* p, int64_t n, const 
   so.xcount = cap ? (int32_t*)((char*)dout + cnt_off(piece_lo(1) - piece_lo(0))) : nullptr;  // (tested for null only)
   so.piece_cnt = words + 32;
   so.abort_word = c->abort_dev;
+  // (tests: ART_HOST_WAVE_WAIT_MS shortens a wave's bound on its chunk, s_memrealtime at 100 MHz)
+  so.wait_ticks = env_int("ART_HOST_WAVE_WAIT_MS", 0) > 0 ? (unsigned long long)env_int("ART_HOST_WAVE_WAIT_MS", 0) * 100000ull
+                                                         : art::STREAM_WAIT_TICKS;
   so.piece_shift = shift;
   so.host_ready = c->hsig_dev;
   so.host_flags = c->hsig_dev + 8;
@@ -1054,9 +1062,13 @@ int propagate_host_maskless(DeviceCtx* c, const art_params* p, int64_t n, const 
   }
   // every block slot initialises the first piece, then the integrator, then every slot helps
   // finalize what is left
-  // the first upload unit by every block slot, then the helpers keep ahead (ART_HOST_INIT_RAYS:
-  // dev, another amount)
-  const int64_t first = serial ? n : std::min(n, (int64_t)std::max(1, env_int("ART_HOST_INIT_RAYS", (int)ulo[1])));
+  // every block slot initialises two rays per integrator lane before the integrator starts (258k
+  // rays; the first unit alone left the integrator's first waves waiting on 8 helpers: 33 ms
+  // against 18 per 1.25e6-ray call), then the helpers keep ahead (ART_HOST_INIT_RAYS: tests and
+  // A/B, another amount)
+  const int64_t first =
+      serial ? n
+             : std::min(n, (int64_t)std::max(1, env_int("ART_HOST_INIT_RAYS", (slots - helpers) * 4 * 64 * 2)));
   if (env_int("ART_HOST_INITPASS", 1))  // (dev: 0 leaves the first piece to the helpers)
     HIP_OK(art::launch_helpers(K, n, in, so, serial ? slots : slots - helpers, first, 0, words + 1, c->m_comp));
   HIP_OK(hipEventRecord(L->ev0, c->m_comp));
@@ -1148,12 +1160,12 @@ int propagate_host_maskless(DeviceCtx* c, const art_params* p, int64_t n, const 
     return moved;
   };
   int perr = 0;
-  // (tests: ART_HOST_UPLOAD_DELAY_MS holds back the second piece's upload, so the integrator's
+  // (tests: ART_HOST_UPLOAD_DELAY_MS holds back the second upload unit, so the integrator's
   // waves outwait their 2 s bound and the device side gives the call up)
   const int delay_ms = env_int("ART_HOST_UPLOAD_DELAY_MS", 0);
   for (int u = 0; u < nu && !perr; ++u) {
     const int64_t lo = ulo[u], m = ulo[u + 1] - lo;
-    if (delay_ms > 0 && lo == piece_lo(1)) std::this_thread::sleep_for(std::chrono::milliseconds(delay_ms));
+    if (delay_ms > 0 && u == 1) std::this_thread::sleep_for(std::chrono::milliseconds(delay_ms));
     const double* src[9] = {x0, x0 + n, x0 + 2 * n, k0, k0 + n, k0 + 2 * n, erg, dw, ln_t0};
     std::vector<Seg> g;
     for (int r = 0; r < 9; ++r) g.push_back({pin + r * nd + lo, src[r] + lo, (size_t)m * sizeof(double)});

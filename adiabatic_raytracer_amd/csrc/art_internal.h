@@ -58,6 +58,7 @@ struct SegOut {
   // long (STREAM_WAIT_TICKS of s_memrealtime) raises *abort_word and stops taking rays.
   unsigned long long* piece_cnt;
   unsigned int* abort_word;
+  unsigned long long wait_ticks;  // a wave's bound on a chunk flag (STREAM_WAIT_TICKS; tests set less)
   int32_t piece_shift;
   // The maskless streamed pipeline (DON = 3, art_capi.cpp propagate_host_maskless): one launch
   // over the whole batch holds every CU; its first `helpers` blocks are helpers, not
@@ -93,6 +94,7 @@ struct SegOut {
 };
 constexpr unsigned long long STREAM_WAIT_TICKS = 200000000ull;  // 2 s at 100 MHz
 constexpr int CHUNK = 64;  // rays a persistent wave claims from the queue at once
+constexpr int HELPER_TILE = 1024;  // rays a helper block initialises or finalizes per claim
 constexpr int END_REC = 16;
 constexpr int X_REC = 8;
 constexpr int CONT_REC = 24;  // [u (7) | f (7) | τ, dt, qpow, cprev, bstart, erg | int4 {ray, n_acc, n_rej, ncross} | int4 {iter, sprev, flags, save_k}]

@@ -597,8 +597,8 @@ __device__ inline SegOut piece_blob(const SegOut& out, int64_t n, int p, int64_t
 }
 
 // ---- the maskless streamed pipeline's helper duty (DON = 3, SegOut::helpers) ----
-constexpr int S3_TILE = 1024;  // rays a helper block initialises or finalizes per claim (4 per thread: the claim,
-                               // the barriers and the L2 write-back of the hand-off amortised over 4 rays)
+constexpr int S3_TILE = HELPER_TILE;  // (4 rays per thread: the claim, the barriers and the L2 write-back of
+                                     // the hand-off amortised over 4 rays)
 constexpr unsigned long long S3_WAIT_TICKS = 2000000000ull;  // 20 s of s_memrealtime without progress: give up
 
 __device__ inline unsigned long long ld_sys(const unsigned long long* p) {
@@ -622,7 +622,7 @@ __device__ inline bool chunk_wait(const SegOut& out, int wnext, int leader) {
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
     while (__hip_atomic_load(out.chunk_ready + wnext / CHUNK, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
       if (__hip_atomic_load(out.abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u ||
-          __builtin_amdgcn_s_memrealtime() - t0 > STREAM_WAIT_TICKS) {
+          __builtin_amdgcn_s_memrealtime() - t0 > out.wait_ticks) {
         __hip_atomic_store(out.abort_word, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         ok = 0;
         break;
@@ -2302,10 +2302,27 @@ __global__ __launch_bounds__(256) void helper_kernel(const KParams P, const int6
         if (init_limit >= 0 && (int64_t)inext >= init_limit) what = 3;
         if (what == 0 && (int64_t)inext < n && inext >= hr) hr = ld_sys(out.host_ready);
         if (what == 0 && (int64_t)inext < n && inext < hr) {
-          const unsigned long long c = atomicAdd(out.init_next, (unsigned long long)S3_TILE);
-          if ((int64_t)c < n) {  // (a tile past the landed inputs waits for them below)
-            what = 1;
-            t = (long long)c;
+          if (init_limit >= 0) {
+            // the pass that starts the launch claims tiles below init_limit only (compare-and-
+            // swap: with a blind add, every block that saw init_next below the limit claimed a
+            // tile, far past the landed inputs, and the integrator behind this pass waited for them)
+            unsigned long long cur = inext;
+            while ((int64_t)cur < init_limit && (int64_t)cur < n) {
+              const unsigned long long seen = atomicCAS(out.init_next, cur, cur + (unsigned long long)S3_TILE);
+              if (seen == cur) {
+                what = 1;
+                t = (long long)cur;
+                break;
+              }
+              cur = seen;
+            }
+            if (what == 0) what = 3;
+          } else {
+            const unsigned long long c = atomicAdd(out.init_next, (unsigned long long)S3_TILE);
+            if ((int64_t)c < n) {  // (a tile past the landed inputs waits for them below)
+              what = 1;
+              t = (long long)c;
+            }
           }
         }
         if (what == 0 && init_limit < 0) {
@@ -3122,6 +3139,7 @@ hipError_t launch_propagate(const KParams& P, int64_t n, const SegIn& in, const 
       out.chunk_ready = (unsigned*)((char*)dbuf + 4096);
       out.init_next = w + 16;
       out.abort_word = (unsigned*)(w + 8 * 60);
+      out.wait_ticks = STREAM_WAIT_TICKS;
       fn = propagate_kernel<ART_VERN6, GEOM_FLAT, false, 3>;
     }
   }

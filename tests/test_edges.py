@@ -362,8 +362,9 @@ def test_streamed_host_pipeline_gives_up_cleanly(monkeypatch):
 
 @pytest.mark.gpu
 def test_streamed_host_pipeline_device_give_up(monkeypatch):
-    """The device side's bound: with the second piece's upload held back 2.5 s, the integrator's
-    waves outwait their 2 s bound on a chunk flag, raise the abort word and stop; the host sees it,
+    """The device side's bound: with the second upload unit held back 1.5 s and the waves' bound
+    on a chunk flag at 0.2 s, the integrator's waves outwait it, raise the abort word and stop;
+    the host sees it,
     lets the launch run out and runs the batch again as one launch. The results are the single
     launch's, the give-up is counted, and the next streamed call works normally."""
     import adiabatic_raytracer_amd as A
@@ -377,7 +378,11 @@ def test_streamed_host_pipeline_device_give_up(monkeypatch):
     monkeypatch.setenv("ART_HOST_PIECE_SHIFT", "11")
     monkeypatch.setenv("ART_HOST_CHUNK_MIN", "1000")
     A.raytracer.host_path_counters(reset=True)
-    for delay, want in (("2500", {"streamed": 0, "stream_giveups": 1, "single": 1}),
+    monkeypatch.setenv("ART_HOST_WAVE_WAIT_MS", "200")
+    monkeypatch.setenv("ART_HOST_INIT_RAYS", "512")  # (the integrator starts before the held-back unit)
+    monkeypatch.setenv("ART_HOST_FIRST_UNIT", "1024")
+    monkeypatch.setenv("ART_HOST_UNIT", "4096")
+    for delay, want in (("1500", {"streamed": 0, "stream_giveups": 1, "single": 1}),
                         ("0", {"streamed": 1, "stream_giveups": 1, "single": 1})):
         monkeypatch.setenv("ART_HOST_UPLOAD_DELAY_MS", delay)
         got = A.propagate_batch(p, *args)
