@@ -920,7 +920,9 @@ int propagate_host_maskless(DeviceCtx* c, const art_params* p, int64_t n, const 
   const int cap = (xc && xc->count) ? xc->capacity : 0;
   const art::KParams K = kparams(*p);
   int shift = 16;
-  while (((int64_t)1 << (shift + 1)) * 16 <= n) ++shift;  // 16..32 pieces (2^19 rays for 10^7)
+  while (((int64_t)1 << (shift + 1)) * 32 <= n) ++shift;  // 32..64 pieces (2^18 rays for 10^7: the last
+  // piece's finalize, copy and scatter are the call's tail, 95.3-96.5 ms against 98.4-101 with 2^19,
+  // profiles/r04ag_piece_shift.jsonl)
   if (const int e = env_int("ART_HOST_PIECE_SHIFT", 0)) shift = std::max(10, e);  // (tests: many small pieces)
   while (((n + ((int64_t)1 << shift) - 1) >> shift) > 64) ++shift;  // 64 piece counters and flags
   const int np = (int)((n + ((int64_t)1 << shift) - 1) >> shift);
