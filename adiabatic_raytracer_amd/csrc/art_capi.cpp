@@ -1188,9 +1188,10 @@ int propagate_host_maskless(DeviceCtx* c, const art_params* p, int64_t n, const 
   double t_last = clk(), t_peek = clk();
   bool gave_up = perr != 0;
   unsigned long long* peek = nullptr;  // (trace) the device counters, copied out every 100 ms
-  if (trace) HIP_OK(hipHostMalloc((void**)&peek, 160 * sizeof(unsigned long long), hipHostMallocDefault));
+  if (trace && hipHostMalloc((void**)&peek, 160 * sizeof(unsigned long long), hipHostMallocDefault) != hipSuccess)
+    peek = nullptr;  // (no HIP_OK between the readier thread's start and its join)
   while (!gave_up && sk < np) {
-    if (trace && clk() - t_peek > (double)env_int("ART_HOST_PEEK_MS", 100)) {
+    if (peek && clk() - t_peek > (double)env_int("ART_HOST_PEEK_MS", 100)) {
       t_peek = clk();
       if (hipMemcpyAsync(peek, words, 160 * sizeof(unsigned long long), hipMemcpyDeviceToHost, c->m_dn) == hipSuccess &&
           hipStreamSynchronize(c->m_dn) == hipSuccess) {
