@@ -142,8 +142,8 @@ int art_device_count(int32_t* count);
 int art_set_device(int32_t device);
 int art_synchronize(void);
 /* Releases every device object the library holds (streams, events, pooled HBM and pinned
- * staging, signal memory, the host copy threads) after draining its work; the next call
- * re-creates what it needs. The library registers this to run at process exit, before the HIP
+ * staging, the host-mapped flags of the streamed pipeline, the host copy threads) after
+ * draining its work; the next call re-creates what it needs. The library registers this to run at process exit, before the HIP
  * runtime's own teardown; a host may also call it itself. */
 int art_shutdown(void);
 /* Duration [ms] of the last propagate kernel, from HIP events recorded on the stream
@@ -187,7 +187,11 @@ double art_find_conversion_surface(const art_params* p);
  *            plain ODE with no callbacks, as the reference does for make_tree = false
  *            (RayTracer.jl:361-377): no crossing is recorded and photons are not stopped
  *            at 1.01 rNS.
- * xc may be NULL when crossings are not wanted (the segment still stops on them). */
+ * xc may be NULL when crossings are not wanted (the segment still stops on them).
+ * art_propagate_host streams Vern6 batches of 2^20 rays and more: one
+ * integrator launch while the inputs are still being copied in and finished pieces already
+ * copied out; the outputs are those of one launch bit for bit, and a streamed call that outlasts
+ * its bounds runs again as one launch (counted by art_host_path_counters). */
 int art_propagate_host(const art_params* p, int64_t n, const double* x0, const double* k0,
                        const double* erg, const double* dw, const double* ln_t0,
                        const int8_t* species, int32_t max_crossings,
