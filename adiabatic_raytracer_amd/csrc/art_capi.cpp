@@ -47,6 +47,7 @@ struct LaunchRec {
   hipEvent_t ev0 = nullptr, ev1 = nullptr, done = nullptr;
   unsigned long long* host_stats = nullptr;  // N_STATS words (pinned)
   int grid = 0;
+  hipStream_t stream = nullptr;
   bool pending = false;
 };
 
@@ -149,6 +150,22 @@ int take_slot(DeviceCtx* c, LaunchRec** out) {
   }
   *out = &L;
   return ART_OK;
+}
+
+// Whether a propagate launch of this context on a stream other than s is still running. With
+// other passes in flight, graduation only costs: a graduated ray holds a whole wave of the tail
+// kernel instead of one lane, and the other passes already fill the CUs its wave would free
+// (profiles/r04al_graduation_in_flight.txt: 16 GR passes in flight 4.9e8 with, 7.7e8 without).
+bool others_in_flight(DeviceCtx* c, hipStream_t s) {
+  for (LaunchRec& L : c->ring) {
+    if (!L.pending || L.stream == s) continue;
+    if (hipEventQuery(L.done) == hipErrorNotReady) {
+      // not an error: keep it out of the thread's last error, which the launches check
+      if (hipPeekAtLastError() == hipErrorNotReady) (void)hipGetLastError();
+      return true;
+    }
+  }
+  return false;
 }
 
 int pool_get(DeviceCtx* c, size_t slot, size_t bytes, void** p) {
@@ -494,7 +511,8 @@ int propagate_device_impl(const art_params* p, int64_t n, const double* x0, cons
       so.grad_count = words + 20;
       so.grad_queue = words + 21;
       so.grad_cap = (int32_t)std::min(ncont, (size_t)INT32_MAX);
-      so.graduate = std::max(0, env_int("ART_GRADUATE", 1024));
+      // (off while another pass of this context runs on another stream: others_in_flight)
+      so.graduate = others_in_flight(c, s) ? 0 : std::max(0, env_int("ART_GRADUATE", 1024));
     }
     so.donate = donate;
     so.small_tail = small_tail ? 1 : 0;
@@ -505,6 +523,7 @@ int propagate_device_impl(const art_params* p, int64_t n, const double* x0, cons
   HIP_OK(hipMemcpyAsync(L->host_stats, words + 1, sizeof(unsigned long long) * art::N_STATS, hipMemcpyDeviceToHost, s));
   HIP_OK(hipEventRecord(L->done, s));
   if (!opt.scratch) HIP_OK(hipFreeAsync(blk, s));
+  L->stream = s;
   L->pending = true;
   c->last = c->next;
   c->next = (c->next + 1) % RING;
@@ -1084,6 +1103,7 @@ int propagate_host_maskless(DeviceCtx* c, const art_params* p, int64_t n, const 
   HIP_OK(hipMemcpyAsync(L->host_stats, words + 1, sizeof(unsigned long long) * art::N_STATS, hipMemcpyDeviceToHost,
                         c->m_comp));
   HIP_OK(hipEventRecord(L->done, c->m_comp));
+  L->stream = c->m_comp;
   L->pending = true;
   c->last = c->next;
   c->next = (c->next + 1) % RING;
