@@ -33,7 +33,7 @@ def build(force=False, verbose=False):
         return LIB
     os.makedirs(LIB_DIR, exist_ok=True)
     # AMDGPU's own register-pressure trackers in the machine scheduler: fewer spills of the
-    # 256-VGPR integrator and 1% faster (A/B on the 1e7-ray flat batch, tools/ab_multi.sh)
+    # 256-VGPR integrator and 1% faster (A/B on the 1e7-ray flat batch, round 3)
     cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=on",
            "-mllvm", "-amdgpu-use-amdgpu-trackers=1",
            *[os.path.join(CSRC, s) for s in SOURCES], "-o", LIB + ".tmp"]
@@ -45,7 +45,7 @@ def build(force=False, verbose=False):
 
 
 def build_variant(out, defines=(), extra=()):
-    """Dev A/B builds (tools/ab_multi.sh): the same sources with extra -D defines / flags into
+    """Dev builds (tools/gpu_final.sh: the section-timing one): the same sources with extra -D defines / flags into
     `out` (e.g. tools/build/libart_x.so, loaded with ART_LIB)."""
     os.makedirs(os.path.dirname(os.path.abspath(out)), exist_ok=True)
     cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=on",

@@ -918,7 +918,7 @@ constexpr int STREAM_FALLBACK = 1 << 20;
 // (propagate_kernel<..., DON = 3>) holds every CU for the whole batch; nothing else needs a CU
 // while it runs:
 //   * the host gathers piece k from the caller's arrays into pinned staging (copy pool) and
-//     copies it to HBM on the upload stream (DMA engines: tools/probe/copy_engine_probe.hip,
+//     copies it to HBM on the upload stream (DMA engines:
 //     profiles/r04k_probe_*.jsonl -- 64 MB copies finish at 56 GB/s under a kernel holding
 //     every CU); a host thread raises the ready counter (host memory) as each piece lands;
 //   * helper blocks of the same launch initialise 256-ray tiles whose inputs have landed

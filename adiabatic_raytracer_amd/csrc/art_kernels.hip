@@ -2662,7 +2662,7 @@ __global__ __launch_bounds__(256, WPS) void sample_kernel(const KParams P, const
       // |b| <= min(2, max(|b_a|, |b_b|) + 0.75 α²), and where b_a, b_b share a sign,
       // |b| >= min(|b_a|, |b_b|) - 0.75 α². (Until round 3 the bound was the first-order
       // |b_a| ± (3 + 3|sinθm|) α, about 100x wider at 0.5 km steps: the uncertified steps
-      // drop by a third, tools/sampler_steps.cpp.)
+      // drop by a third)
       //  * negative: ωp² <= wp2n |b|max / r_min³ < m_a² (see above);
       //  * positive (the point before positive too): outside g_schwartz's interior patch
       //    (r > 10 km), g^rr g^tt = -1, so Cauchy-Schwarz on k∥ with w on the axion shell gives
