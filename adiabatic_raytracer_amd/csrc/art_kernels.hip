@@ -2467,7 +2467,6 @@ __global__ __launch_bounds__(256, WPS) void sample_kernel(const KParams P, const
   // loop: the kernel fits 2 waves/SIMD without spills)
   __shared__ double sline[14 * 256];
   __shared__ double slast[256];           // value at the step's last point
-  __shared__ unsigned ssb[256], snz[256];  // bit j: signbit / nonzero of point j (bit 0: the step start)
   __shared__ unsigned char ssrc[2 * 256];  // compact lists: uncertified lanes, certified lanes
   __shared__ double sqa[4 * SQCAP], sqb[4 * SQCAP];  // bracket queue: ends -> root
   __shared__ unsigned char sqsrc[4 * SQCAP], sqok[4 * SQCAP];
@@ -2699,25 +2698,32 @@ __global__ __launch_bounds__(256, WPS) void sample_kernel(const KParams P, const
       const unsigned long long mU = __ballot(unc);
       const int nU = __popcll(mU);
       if (nU == 0) continue;  // all certified: no point, no bracket, c_prev unchanged
-      if (unc) ssrc[wb + __popcll(mU & lt)] = (unsigned char)lane;
-      ssb[threadIdx.x] = signbit(c_prev) ? 1u : 0u;
-      snz[threadIdx.x] = (c_prev != 0.0) ? 1u : 0u;
+      const int uix = __popcll(mU & lt);  // this lane's rank among the uncertified ones
+      if (unc) ssrc[wb + uix] = (unsigned char)lane;
+      // bit j: signbit / nonzero-ness of point j (bit 0: the step start)
+      unsigned sb = signbit(c_prev) ? 1u : 0u, nz = (c_prev != 0.0) ? 1u : 0u;
       wave_lds_sync();
-      // items: (uncertified lane, point 1..nper) point-major. A certified step needs no point at
-      // all: its last point -- the next step's bracket start -- has the certified sign, and
-      // c_prev is only ever read for its sign (the next certificate, the bit-0 sign and
-      // nonzero-ness of the next scan), so it keeps the value it had (round 3: until then
-      // every certified lane evaluated its last point, 1 item per lane per step)
-      const int totU = nU * nper, tot = totU;
+      // items: (uncertified lane u, point j = 1..nper) lane-major, t = u nper + j - 1. A certified
+      // step needs no point at all: its last point -- the next step's bracket start -- has the
+      // certified sign, and c_prev is only ever read for its sign (the next certificate, the
+      // bit-0 sign and nonzero-ness of the next scan), so it keeps the value it had. Each pass's
+      // signs come back as two ballots, from which every owner takes the run of its own items'
+      // bits (round 4: until then point-major items ORed their bits into LDS words with two LDS
+      // atomics each, ~13 lanes deep on one word, and divided by the variable nU: 3.3 LDS
+      // bank-conflict cycles per LDS instruction. Samples bit-identical, time unchanged: the
+      // kernel is VALU-bound, profiles/r04aq_sampler_pmc.txt).
+      const int tot = nU * nper;
 #ifndef ART_NO_SAMPLER_PRIO  // the dense grid pass at the low issue priority, the rest of a step (certificate,
       __builtin_amdgcn_s_setprio(0);  // brackets: short dependent chains) at the high one: 118.5 -> 117.1 ms
 #endif                                // per 1e7 samples (profiles/r04c_sampler_prio.jsonl)
       #pragma unroll 1
       for (int w0 = 0; w0 < tot; w0 += 64) {
         const int t = w0 + lane;
+        bool neg = false, nonz = false;
         if (t < tot) {
-          const int j = t / nU + 1;
-          const int src = ssrc[wb + t % nU];
+          const int u = t / nper;
+          const int j = t - u * nper + 1;
+          const int src = ssrc[wb + u];
           const double* S = sline + wb + src;
           // (s1 - s0) j / 19: from the table for a full 0.5 km step (wave-uniform), else divided
           const double sc = s0 + (s1 - s0 == 0.5 ? sgrid[j] : (s1 - s0) * double(j) / double(np - 1));
@@ -2727,8 +2733,19 @@ __global__ __launch_bounds__(256, WPS) void sample_kernel(const KParams P, const
           const double VL[3] = {S[6 * 256], S[7 * 256], S[8 * 256]};
           const double v = sampler_condition_e(P, xl, VL, S[9 * 256], S[10 * 256]);
           if (j == nper) slast[wb + src] = v;
-          atomicOr(&ssb[wb + src], (signbit(v) ? 1u : 0u) << j);
-          atomicOr(&snz[wb + src], (v != 0.0 ? 1u : 0u) << j);
+          neg = signbit(v);
+          nonz = v != 0.0;
+        }
+        const unsigned long long mneg = __ballot(neg), mnz = __ballot(nonz);
+        if (unc) {
+          const int a = uix * nper;
+          const int lo = max(a, w0), hi = min(a + nper, w0 + 64);
+          if (lo < hi) {
+            const unsigned long long run = (1ull << (hi - lo)) - 1ull;
+            const int at = lo - a + 1;
+            sb |= (unsigned)((mneg >> (lo - w0)) & run) << at;
+            nz |= (unsigned)((mnz >> (lo - w0)) & run) << at;
+          }
         }
       }
 #ifndef ART_NO_SAMPLER_PRIO
@@ -2738,7 +2755,6 @@ __global__ __launch_bounds__(256, WPS) void sample_kernel(const KParams P, const
       // this lane's sign changes in (point j-1, point j]: signbits differ, both values nonzero
       unsigned br = 0u;
       if (unc) {
-        const unsigned sb = ssb[threadIdx.x], nz = snz[threadIdx.x];
         br = (sb ^ (sb << 1)) & nz & (nz << 1) & (((1u << np) - 1u) & ~1u);
         c_prev = slast[threadIdx.x];
       }
