@@ -506,13 +506,14 @@ int propagate_device_impl(const art_params* p, int64_t n, const double* x0, cons
     so.cont2_queue = words + 19;
     if (!small_tail && tr.ntimes == 0 && p->integrator == ART_VERN6) {
       // graduation of a pass's outlier rays to the tail kernel (ART_GRADUATE attempts, default
-      // 1024 -- about 12x the mean GR ray, never reached by a flat one; 0 = off)
+      // 2048 -- about 23x the mean GR ray, never reached by a flat one; 0 = off;
+      // profiles/r04av_graduation_threshold.txt)
       so.grad = so.cont2 + ncont * art::CONT_REC;
       so.grad_count = words + 20;
       so.grad_queue = words + 21;
       so.grad_cap = (int32_t)std::min(ncont, (size_t)INT32_MAX);
       // (off while another pass of this context runs on another stream: others_in_flight)
-      so.graduate = others_in_flight(c, s) ? 0 : std::max(0, env_int("ART_GRADUATE", 1024));
+      so.graduate = others_in_flight(c, s) ? 0 : std::max(0, env_int("ART_GRADUATE", 2048));
     }
     so.donate = donate;
     so.small_tail = small_tail ? 1 : 0;

@@ -52,11 +52,11 @@ def test_tail_donation_is_bit_exact(cfg, tail, monkeypatch):
 
 
 @pytest.mark.parametrize("cfg", ["flat", "gr", "gr_oblique"])
-@pytest.mark.parametrize("graduate", ["1", "64", "1024"])
+@pytest.mark.parametrize("graduate", ["1", "64", "2048"])
 def test_graduation_is_bit_exact(cfg, graduate, monkeypatch):
     """ART_GRADUATE=k: a ray still stepping after k attempts leaves its wave for a wave of its own
     (tail_kernel) without waiting for the wave to drain. k=1 graduates nearly every ray (and
-    overflows the graduation records, so the rest stay in place), k=64 a large share, 1024 (the
+    overflows the graduation records, so the rest stay in place), k=64 a large share, 2048 (the
     default) the outliers. Outputs and counters equal the undonated run bit for bit."""
     monkeypatch.setenv("ART_GRADUATE", graduate)
     import adiabatic_raytracer_amd as A
