@@ -62,6 +62,9 @@ SIGNATURES = {
                                        C.POINTER(CrossingBuf), _v]),
     "art_propagate_host_flux": (C.c_int, [_P, _i64, _v, _v, _v, _v, _v, _v, _i32, C.POINTER(SegmentOut),
                                           C.POINTER(CrossingBuf), _i32, _v]),
+    "art_propagate_host_flux_async": (C.c_int, [_P, _i64, _v, _v, _v, _v, _v, _v, _i32, C.POINTER(SegmentOut),
+                                                C.POINTER(CrossingBuf), _i32, _v, C.POINTER(C.c_int64)]),
+    "art_host_wait": (C.c_int, [C.c_int64]),
     "art_host_path_counters": (C.c_int, [_v, _i32, _i32]),
     "art_propagate_traj_host": (C.c_int, [_P, _i64, _v, _v, _v, _v, _v, _v, _i32, C.POINTER(SegmentOut),
                                           C.POINTER(CrossingBuf), _i32, _v, _v, _v]),
@@ -78,6 +81,7 @@ SIGNATURES = {
     "art_event_weight_host": (C.c_int, [_P, _d, _d, _d, _i64, _v, _v, _v, _v]),
     "art_event_weight_device": (C.c_int, [_P, _d, _d, _d, _i64, _v, _v, _v, _v, _v]),
     "art_recent_kernel_ms": (C.c_int, [_i32, _v]),
+    "art_recent_kernel_span_ms": (C.c_int, [_i32, _v]),
     "art_set_tail_donation": (C.c_int, [_i32]),
     "art_flux_histogram_phi_device": (C.c_int, [_i64, _v, _v, _v, _i32, _v, _v]),
     "art_flux_histogram_phi_range_device": (C.c_int, [_i64, _v, _v, _v, _i32, _d, _d, _v, _v]),

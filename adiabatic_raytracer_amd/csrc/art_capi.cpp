@@ -15,7 +15,12 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
+#include <functional>
+#include <map>
+#include <memory>
 #include <mutex>
+#include <set>
 #include <string>
 #include <thread>
 #include <vector>
@@ -27,7 +32,10 @@
 
 namespace {
 
-std::mutex g_mu;
+// g_mu: every entry point (the calls of one process are serialised); g_ring_mu: the launch ring
+// and the latched statistics, which the asynchronous host calls' worker threads also touch
+// (they never take g_mu, so a caller holding it may wait for them)
+std::mutex g_mu, g_ring_mu;
 thread_local std::string g_err;
 double g_last_ms = 0.0;
 unsigned long long g_last_stats[art::N_STATS] = {0};
@@ -36,7 +44,7 @@ int g_last_grid = 0;
 // pipeline completions, streamed give-ups (each batch then ran again as one launch), chunked
 // pipeline calls, single-launch calls
 enum { HC_CALLS, HC_STREAMED, HC_GIVEUPS, HC_CHUNKED, HC_SINGLE, HC_N };
-uint64_t g_host_cnt[HC_N] = {0};
+std::atomic<uint64_t> g_host_cnt[HC_N] = {};
 
 // One propagate launch's bookkeeping: the HIP events around the integrator kernel, an event
 // after its statistics were copied to pinned host memory, and that memory. A ring of them per
@@ -45,10 +53,41 @@ uint64_t g_host_cnt[HC_N] = {0};
 constexpr int RING = 64;
 struct LaunchRec {
   hipEvent_t ev0 = nullptr, ev1 = nullptr, done = nullptr;
-  unsigned long long* host_stats = nullptr;  // N_STATS words (pinned)
+  unsigned long long* host_stats = nullptr;  // N_STATS_DEV words (pinned): statistics, then the clock stamps
   int grid = 0;
   hipStream_t stream = nullptr;
   bool pending = false;
+};
+
+struct Pinned {
+  void* p = nullptr;
+  size_t bytes = 0;
+  unsigned flags = 0;
+};
+using PoolVec = std::vector<std::pair<void*, size_t>>;
+
+// One set of the maskless streamed pipeline's resources (propagate_host_maskless): the
+// integrator's and the helpers' CU-masked streams (a hardware queue each), the two copy
+// streams, the host words the GPU polls and raises, the pinned and device staging and the
+// events. A context has HOST_LANES of them, so that many host calls can be in flight at once
+// (art_propagate_host_flux_async: the next batch's uploads and first rays overlap this one's
+// drain); lane 0 also serves the synchronous calls, which first wait for every async call.
+constexpr int HOST_LANES = 2;
+struct HostLane {
+  hipStream_t m_comp = nullptr, m_up = nullptr, m_dn = nullptr, m_help = nullptr;
+  unsigned long long* hsig = nullptr;  // [0] ready | [8, 8 + 64) piece flags | [72] helper blocks started
+  unsigned long long* hsig_dev = nullptr;
+  unsigned int* abort_host = nullptr;  // the word the waves and helpers raise (or read) when a call gives up
+  unsigned int* abort_dev = nullptr;
+  std::vector<hipEvent_t> pev;
+  std::vector<Pinned> pinned;  // [0] gathered inputs, [1] output blobs
+  PoolVec pool;                // [0] inputs, [1] output blobs, [2] scratch, [3] flux; [4..] the single-launch fallback
+  // the asynchronous calls' worker: one job at a time, results kept by ticket until waited for
+  std::thread worker;
+  std::mutex m;
+  std::condition_variable cv;
+  std::function<int()> job;
+  bool busy = false, stop = false;
 };
 
 struct DeviceCtx {
@@ -66,25 +105,20 @@ struct DeviceCtx {
   // pinned memory)
   std::vector<hipStream_t> pstreams;
   hipStream_t h2d = nullptr, fin = nullptr;
-  struct Pinned {
-    void* p = nullptr;
-    size_t bytes = 0;
-    unsigned flags = 0;
-  };
   std::vector<Pinned> pinned;
   std::vector<hipEvent_t> pev;
-  // a pinned word the streamed pipeline's waves raise when they give up
-  unsigned int* abort_host = nullptr;
-  unsigned int* abort_dev = nullptr;
-  // the maskless streamed pipeline (propagate_host_maskless): plain streams for the integrator
-  // and the two copy directions (the copies run on the DMA engines), a block of host memory the
-  // GPU reads and writes over PCIe -- [0] the ready counter, [8 + p] piece p's flag -- and the
-  // device array of the flags' addresses
-  hipStream_t m_comp = nullptr, m_up = nullptr, m_dn = nullptr, m_help = nullptr;
-  unsigned long long* hsig = nullptr;
-  unsigned long long* hsig_dev = nullptr;
+  HostLane lanes[HOST_LANES];
+  // asynchronous host calls: tickets in submission order (ticket t runs on lane t % HOST_LANES);
+  // finished calls' results until art_host_wait takes them
+  std::atomic<int64_t> next_ticket{0};
+  std::mutex res_m;
+  std::condition_variable res_cv;
+  std::set<int64_t> pending;  // submitted, not yet waited for
+  std::map<int64_t, std::pair<int, std::string>> results;
 };
-std::vector<DeviceCtx> g_ctx;
+// (pointers: a context never moves, so a worker thread may hold one while another device's is created)
+std::vector<std::unique_ptr<DeviceCtx>> g_ctx;
+std::mutex g_ctx_mu;
 
 int fail(int code, const char* fmt, const char* a = "", const char* b = "") {
   char buf[512];
@@ -116,17 +150,23 @@ int current_ctx(DeviceCtx** out) {
   }
   int dev = 0;
   HIP_OK(hipGetDevice(&dev));
-  if ((int)g_ctx.size() <= dev) g_ctx.resize(dev + 1);
-  DeviceCtx& c = g_ctx[dev];
+  DeviceCtx* cp = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(g_ctx_mu);
+    if ((int)g_ctx.size() <= dev) g_ctx.resize(dev + 1);
+    if (!g_ctx[dev]) g_ctx[dev].reset(new DeviceCtx());
+    cp = g_ctx[dev].get();
+  }
+  DeviceCtx& c = *cp;
   if (c.device < 0) {
     HIP_OK(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking));
     unsigned long long* hs = nullptr;
-    HIP_OK(hipHostMalloc((void**)&hs, sizeof(unsigned long long) * art::N_STATS * RING, hipHostMallocDefault));
+    HIP_OK(hipHostMalloc((void**)&hs, sizeof(unsigned long long) * art::N_STATS_DEV * RING, hipHostMallocDefault));
     for (int i = 0; i < RING; ++i) {
       HIP_OK(hipEventCreate(&c.ring[i].ev0));
       HIP_OK(hipEventCreate(&c.ring[i].ev1));
       HIP_OK(hipEventCreateWithFlags(&c.ring[i].done, hipEventDisableTiming));
-      c.ring[i].host_stats = hs + i * art::N_STATS;
+      c.ring[i].host_stats = hs + i * art::N_STATS_DEV;
     }
     // per-launch scratch comes from the stream-ordered allocator: keep what it frees cached
     // so a steady stream of launches does not go back to the driver
@@ -168,9 +208,9 @@ bool others_in_flight(DeviceCtx* c, hipStream_t s) {
   return false;
 }
 
-int pool_get(DeviceCtx* c, size_t slot, size_t bytes, void** p) {
-  if (c->pool.size() <= slot) c->pool.resize(slot + 1, {nullptr, 0});
-  auto& e = c->pool[slot];
+int pool_get_v(PoolVec& pool, size_t slot, size_t bytes, void** p) {
+  if (pool.size() <= slot) pool.resize(slot + 1, {nullptr, 0});
+  auto& e = pool[slot];
   if (e.second < bytes) {
     if (e.first) HIP_OK(hipFree(e.first));
     e.first = nullptr;
@@ -182,9 +222,11 @@ int pool_get(DeviceCtx* c, size_t slot, size_t bytes, void** p) {
   return ART_OK;
 }
 
-int pinned_get(DeviceCtx* c, size_t slot, size_t bytes, void** p, unsigned flags = hipHostMallocDefault) {
-  if (c->pinned.size() <= slot) c->pinned.resize(slot + 1);
-  auto& e = c->pinned[slot];
+int pool_get(DeviceCtx* c, size_t slot, size_t bytes, void** p) { return pool_get_v(c->pool, slot, bytes, p); }
+
+int pinned_get_v(std::vector<Pinned>& pinned, size_t slot, size_t bytes, void** p, unsigned flags = hipHostMallocDefault) {
+  if (pinned.size() <= slot) pinned.resize(slot + 1);
+  auto& e = pinned[slot];
   if (e.bytes < bytes || e.flags != flags) {
     if (e.p) HIP_OK(hipHostFree(e.p));
     e.p = nullptr;
@@ -196,6 +238,10 @@ int pinned_get(DeviceCtx* c, size_t slot, size_t bytes, void** p, unsigned flags
   }
   *p = e.p;
   return ART_OK;
+}
+
+int pinned_get(DeviceCtx* c, size_t slot, size_t bytes, void** p, unsigned flags = hipHostMallocDefault) {
+  return pinned_get_v(c->pinned, slot, bytes, p, flags);
 }
 
 // Host-side copies of the chunked host pipeline (caller arrays <-> pinned staging): a few
@@ -219,8 +265,10 @@ class CopyPool {
     cv_.notify_all();
     for (auto& t : th_) t.join();
   }
-  // copies every segment; pieces of at most 1 MiB are shared by the workers and the caller
+  // copies every segment; pieces of at most 1 MiB are shared by the workers and the caller (one
+  // caller at a time: the asynchronous calls' workers take turns)
   void run(const std::vector<Seg>& segs) {
+    std::lock_guard<std::mutex> one(run_m_);
     pieces_.clear();
     for (const Seg& g : segs)
       for (size_t o = 0; o < g.bytes; o += PIECE)
@@ -258,6 +306,7 @@ class CopyPool {
     }
   }
   std::vector<std::thread> th_;
+  std::mutex run_m_;
   std::vector<Seg> pieces_;
   std::atomic<size_t> next_{0};
   std::mutex m_;
@@ -283,8 +332,21 @@ CopyPool& copy_pool() {
 
 // Every HIP object a device context holds, released in dependency order (the streams drained
 // first). Used by art_shutdown, which runs at exit ahead of the HIP runtime's teardown.
+void stop_workers(DeviceCtx& c) {
+  for (HostLane& H : c.lanes) {
+    if (!H.worker.joinable()) continue;
+    {
+      std::lock_guard<std::mutex> lk(H.m);
+      H.stop = true;
+    }
+    H.cv.notify_all();
+    H.worker.join();
+  }
+}
+
 void release_ctx(DeviceCtx& c) {
   if (c.device < 0) return;
+  stop_workers(c);  // (each finishes its call first)
   (void)hipSetDevice(c.device);
   (void)hipDeviceSynchronize();
   for (LaunchRec& L : c.ring) {
@@ -300,16 +362,31 @@ void release_ctx(DeviceCtx& c) {
   for (hipEvent_t e : c.pev) (void)hipEventDestroy(e);
   for (hipStream_t s : c.pstreams)
     if (s && s != c.stream) (void)hipStreamDestroy(s);
-  for (hipStream_t s : {c.h2d, c.fin, c.m_comp, c.m_up, c.m_dn, c.m_help})
+  for (hipStream_t s : {c.h2d, c.fin})
     if (s) (void)hipStreamDestroy(s);
-  if (c.hsig) (void)hipHostFree(c.hsig);
-  if (c.abort_host) (void)hipHostFree(c.abort_host);
+  for (HostLane& H : c.lanes) {
+    for (auto& e : H.pool)
+      if (e.first) (void)hipFree(e.first);
+    for (auto& e : H.pinned)
+      if (e.p) (void)hipHostFree(e.p);
+    for (hipEvent_t e : H.pev) (void)hipEventDestroy(e);
+    for (hipStream_t s : {H.m_comp, H.m_up, H.m_dn, H.m_help})
+      if (s) (void)hipStreamDestroy(s);
+    if (H.hsig) (void)hipHostFree(H.hsig);
+    if (H.abort_host) (void)hipHostFree(H.abort_host);
+  }
   if (c.stream) (void)hipStreamDestroy(c.stream);
-  c = DeviceCtx();
 }
 
 void shutdown_locked() {
-  for (DeviceCtx& c : g_ctx) release_ctx(c);
+  std::vector<std::unique_ptr<DeviceCtx>> all;
+  {
+    std::lock_guard<std::mutex> lk(g_ctx_mu);
+    all.swap(g_ctx);
+  }
+  for (auto& c : all)
+    if (c) release_ctx(*c);
+  all.clear();
   delete g_copy_pool;
   g_copy_pool = nullptr;
 }
@@ -403,6 +480,7 @@ struct LaunchOpts {
   size_t scratch_bytes = 0;  // the size of `scratch` (checked against the launch's layout)
   bool nan_fill = false;
   hipStream_t finalize_stream = nullptr;  // finalize_kernel on this stream (after the integrator)
+  LaunchRec** launch_out = nullptr;       // the launch's ring entry (finish_timing_slot)
 };
 
 // Tail donation of a launch: the caller's choice, else the device's setting, else (-1, the
@@ -456,12 +534,12 @@ int scratch_layout(DeviceCtx* c, int64_t n, int cap, int32_t donate, ScratchLayo
 int propagate_device_impl(const art_params* p, int64_t n, const double* x0, const double* k0, const double* erg,
                           const double* dw, const double* ln_t0, const int8_t* species, int32_t max_crossings,
                           art_segment_out* out, art_crossing_buf* xc, void* stream, const TrajArgs& tr = TrajArgs(),
-                          const LaunchOpts& opt = LaunchOpts()) {
+                          const LaunchOpts& opt = LaunchOpts(), DeviceCtx* cx = nullptr) {
   bool empty = false;
   int rc = check_segment_args(p, n, x0, k0, erg, dw, ln_t0, species, out, xc, tr, &empty);
   if (rc || empty) return rc;
-  DeviceCtx* c;
-  if ((rc = current_ctx(&c))) return rc;
+  DeviceCtx* c = cx;
+  if (!c && (rc = current_ctx(&c))) return rc;
   hipStream_t s = pick(c, stream);
   const art::KParams K = kparams(*p);
   const int cap = (xc && xc->count) ? xc->capacity : 0;
@@ -473,8 +551,10 @@ int propagate_device_impl(const art_params* p, int64_t n, const double* x0, cons
     return fail(ART_E_INVALID, "caller scratch of %s bytes is smaller than the launch needs (%s)",
                 std::to_string(opt.scratch_bytes).c_str(), std::to_string(SL.total()).c_str());
   const size_t head = SL.head, u0b = SL.u0b, recb = SL.recb, xrb = SL.xrb, ncont = SL.ncont;
+  std::lock_guard<std::mutex> rlk(g_ring_mu);  // (the ring, up to this launch's entry in it)
   LaunchRec* L;
   if ((rc = take_slot(c, &L))) return rc;
+  if (opt.launch_out) *opt.launch_out = L;
   void* blk = opt.scratch;
   if (!blk && (rc = scratch_alloc(s, SL.total(), &blk))) return rc;
   unsigned long long* words = (unsigned long long*)blk;
@@ -521,7 +601,7 @@ int propagate_device_impl(const art_params* p, int64_t n, const double* x0, cons
   HIP_OK(hipMemsetAsync(words, 0, head, s));
   HIP_OK(art::launch_propagate(K, n, in, so, max_crossings, words, words + 1, s, &L->grid, L->ev0, L->ev1,
                                opt.finalize_stream));
-  HIP_OK(hipMemcpyAsync(L->host_stats, words + 1, sizeof(unsigned long long) * art::N_STATS, hipMemcpyDeviceToHost, s));
+  HIP_OK(hipMemcpyAsync(L->host_stats, words + 1, sizeof(unsigned long long) * art::N_STATS_DEV, hipMemcpyDeviceToHost, s));
   HIP_OK(hipEventRecord(L->done, s));
   if (!opt.scratch) HIP_OK(hipFreeAsync(blk, s));
   L->stream = s;
@@ -532,10 +612,12 @@ int propagate_device_impl(const art_params* p, int64_t n, const double* x0, cons
   return ART_OK;
 }
 
-// Latch the most recent propagate launch: its integrator kernel's duration and statistics.
-int finish_timing(DeviceCtx* c) {
-  if (c->last < 0) return ART_OK;
-  LaunchRec& L = c->ring[c->last];
+// Latch one propagate launch (L; null: the most recent): its integrator kernel's duration and
+// statistics, once it has completed.
+int finish_timing_slot(DeviceCtx* c, LaunchRec* Lp) {
+  std::lock_guard<std::mutex> rlk(g_ring_mu);
+  if (!Lp && c->last < 0) return ART_OK;
+  LaunchRec& L = Lp ? *Lp : c->ring[c->last];
   HIP_OK(hipEventSynchronize(L.done));
   float ms = 0.f;
   HIP_OK(hipEventElapsedTime(&ms, L.ev0, L.ev1));
@@ -544,10 +626,12 @@ int finish_timing(DeviceCtx* c) {
   for (int i = 0; i < art::N_STATS; ++i) g_last_stats[i] = L.host_stats[i];
   return ART_OK;
 }
+int finish_timing(DeviceCtx* c) { return finish_timing_slot(c, nullptr); }
 
 // Latch several propagate launches (the chunks of one host call) as one: their integrator
 // kernels' summed durations and summed statistics.
 int finish_timing_sum(DeviceCtx* c, const std::vector<int>& slots) {
+  std::lock_guard<std::mutex> rlk(g_ring_mu);
   double ms_sum = 0.0;
   unsigned long long st[art::N_STATS] = {0};
   int grid = 0;
@@ -626,6 +710,7 @@ int art_recent_kernel_ms(int32_t n, double* ms) {
   int rc = current_ctx(&c);
   if (rc) return rc;
   if (n < 0 || (n > 0 && !ms)) return fail(ART_E_INVALID, "bad buffer");
+  std::lock_guard<std::mutex> rlk(g_ring_mu);
   int64_t m = n;
   if (m > c->launches) m = c->launches;
   if (m > RING) m = RING;
@@ -635,6 +720,27 @@ int art_recent_kernel_ms(int32_t n, double* ms) {
     float f = 0.f;
     HIP_OK(hipEventElapsedTime(&f, L.ev0, L.ev1));
     ms[j] = f;
+  }
+  return (int)m;
+}
+
+// The same launches' integrator spans [ms] from in-kernel clock stamps (first wave start to last
+// wave end, s_memrealtime at 100 MHz; -1 where a launch left none). Returns the count written.
+int art_recent_kernel_span_ms(int32_t n, double* ms) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  DeviceCtx* c;
+  int rc = current_ctx(&c);
+  if (rc) return rc;
+  if (n < 0 || (n > 0 && !ms)) return fail(ART_E_INVALID, "bad buffer");
+  std::lock_guard<std::mutex> rlk(g_ring_mu);
+  int64_t m = n;
+  if (m > c->launches) m = c->launches;
+  if (m > RING) m = RING;
+  for (int64_t j = 0; j < m; ++j) {
+    LaunchRec& L = c->ring[(int)(((int64_t)c->last - (m - 1 - j) + RING) % RING)];
+    HIP_OK(hipEventSynchronize(L.done));
+    const unsigned long long t0 = ~L.host_stats[art::ST_T0], t1 = L.host_stats[art::ST_T1];
+    ms[j] = (L.host_stats[art::ST_T0] == 0ull || t1 < t0) ? -1.0 : (double)(t1 - t0) / art::STAMP_TICKS_PER_MS;
   }
   return (int)m;
 }
@@ -922,32 +1028,27 @@ constexpr int STREAM_FALLBACK = 1 << 20;
 //     copies it to HBM on the upload stream (DMA engines:
 //     profiles/r04k_probe_*.jsonl -- 64 MB copies finish at 56 GB/s under a kernel holding
 //     every CU); a host thread raises the ready counter (host memory) as each piece lands;
-//   * helper blocks of the same launch initialise 256-ray tiles whose inputs have landed
+//   * persistent helper blocks (helper_kernel HK_TILES, a separate kernel on a stream of its own,
+//     resident beside the integrator) initialise 1024-ray tiles whose inputs have landed
 //     (init_one, the init_kernel arithmetic) and flag their chunks; a wave that claims a
 //     chunk of 64 rays waits for its flag. Once every ray of a piece has finished, helpers
 //     finalize its tiles (finalize_one) into the piece's SoA blob in HBM, and the block that
 //     finalizes its last tile raises the piece's flag (host memory);
 //   * the host polls the flags, copies each finished blob to pinned memory (DMA engines) and
 //     scatters it into the caller's arrays.
-// Helper blocks (SegOut::helpers) do the init and finalize tiles while the rest integrate; the
-// blocks whose waves run out of rays join them (art_kernels.hip, s3_helper).
+// Before the integrator, one helper_kernel pass on the integrator's stream initialises the first
+// rays with every block slot; after it, one more pass finalizes what is left.
 // Round 3's CU-masked pipeline ran the init and finalize kernels on 8 reserved CUs, which cost
 // ~10% of the integrator (profiles/r04g_stream_anatomy.jsonl); it is gone. Per-ray results
 // equal the single launch's bit for bit.
-int propagate_host_maskless(DeviceCtx* c, const art_params* p, int64_t n, const double* x0, const double* k0,
-                            const double* erg, const double* dw, const double* ln_t0, const int8_t* species,
-                            int32_t max_crossings, art_segment_out* out, art_crossing_buf* xc, const FluxArgs& fx) {
-  const int cap = (xc && xc->count) ? xc->capacity : 0;
-  const art::KParams K = kparams(*p);
-  int shift = 16;
-  while (((int64_t)1 << (shift + 1)) * 32 <= n) ++shift;  // 32..64 pieces (2^18 rays for 10^7: the last
-  // piece's finalize, copy and scatter are the call's tail, 95.3-96.5 ms against 98.4-101 with 2^19,
-  // profiles/r04ag_piece_shift.jsonl)
-  if (const int e = env_int("ART_HOST_PIECE_SHIFT", 0)) shift = std::max(10, e);  // (tests: many small pieces)
-  while (((n + ((int64_t)1 << shift) - 1) >> shift) > 64) ++shift;  // 64 piece counters and flags
-  const int np = (int)((n + ((int64_t)1 << shift) - 1) >> shift);
-  constexpr int NFLAG = 64;
-  if (!c->m_comp) {
+// The HostLane words the GPU reads and writes over PCIe: [0] the ready counter | [8, 8 + 64)
+// the piece flags | [72] helper blocks started | [HSIG_DONE, ...) SegOut::done_host (the flag,
+// the statistics, the flux)
+constexpr int HSIG_NFLAG = 64, HSIG_DONE = 80;
+constexpr size_t HSIG_WORDS = HSIG_DONE + art::DONE_FLUX + 2 * art::FLUX_HELPER_BINS;
+
+int lane_setup(DeviceCtx* c, HostLane* H) {
+  if (!H->m_comp) {
     // the integrator's and the persistent helpers' streams each on a hardware queue of its own
     // (a stream with a CU mask gets one; here the mask holds every CU): plain streams share the
     // process's few queues (GPU_MAX_HW_QUEUES), and a stream queued behind a persistent kernel
@@ -957,20 +1058,51 @@ int propagate_host_maskless(DeviceCtx* c, const art_params* p, int64_t n, const 
     HIP_OK(hipDeviceGetAttribute(&ncu_all, hipDeviceAttributeMultiprocessorCount, c->device));
     std::vector<uint32_t> all((ncu_all + 31) / 32, 0u);
     for (int i = 0; i < ncu_all; ++i) all[i / 32] |= 1u << (i % 32);
-    HIP_OK(hipExtStreamCreateWithCUMask(&c->m_comp, (uint32_t)all.size(), all.data()));
-    HIP_OK(hipExtStreamCreateWithCUMask(&c->m_help, (uint32_t)all.size(), all.data()));
-    HIP_OK(hipStreamCreateWithFlags(&c->m_up, hipStreamNonBlocking));
-    HIP_OK(hipStreamCreateWithFlags(&c->m_dn, hipStreamNonBlocking));
+    HIP_OK(hipExtStreamCreateWithCUMask(&H->m_comp, (uint32_t)all.size(), all.data()));
+    HIP_OK(hipExtStreamCreateWithCUMask(&H->m_help, (uint32_t)all.size(), all.data()));
+    HIP_OK(hipStreamCreateWithFlags(&H->m_up, hipStreamNonBlocking));
+    HIP_OK(hipStreamCreateWithFlags(&H->m_dn, hipStreamNonBlocking));
   }
-  if (!c->hsig) {
-    // [0] ready | [8, 8 + 64) piece flags | [72] helper blocks started
-    HIP_OK(hipHostMalloc((void**)&c->hsig, sizeof(unsigned long long) * (16 + NFLAG), hipHostMallocCoherent | hipHostMallocMapped));
-    HIP_OK(hipHostGetDevicePointer((void**)&c->hsig_dev, c->hsig, 0));
+  if (!H->hsig) {
+    HIP_OK(hipHostMalloc((void**)&H->hsig, sizeof(unsigned long long) * HSIG_WORDS, hipHostMallocCoherent | hipHostMallocMapped));
+    HIP_OK(hipHostGetDevicePointer((void**)&H->hsig_dev, H->hsig, 0));
   }
-  if (!c->abort_host) {
-    HIP_OK(hipHostMalloc((void**)&c->abort_host, 64, hipHostMallocCoherent | hipHostMallocMapped));
-    HIP_OK(hipHostGetDevicePointer((void**)&c->abort_dev, c->abort_host, 0));
+  if (!H->abort_host) {
+    HIP_OK(hipHostMalloc((void**)&H->abort_host, 64, hipHostMallocCoherent | hipHostMallocMapped));
+    HIP_OK(hipHostGetDevicePointer((void**)&H->abort_dev, H->abort_host, 0));
   }
+  return ART_OK;
+}
+
+// Latch one launch's statistics (the ring entry's, for art_recent_kernel_*; and the "last
+// launch" figures of art_last_stats / art_last_kernel_ms) from words the host already holds.
+int latch_launch(DeviceCtx* c, LaunchRec* L, const unsigned long long* st) {
+  std::lock_guard<std::mutex> rlk(g_ring_mu);
+  for (int i = 0; i < art::N_STATS_DEV; ++i) L->host_stats[i] = st[i];
+  HIP_OK(hipEventSynchronize(L->ev1));
+  float ms = 0.f;
+  HIP_OK(hipEventElapsedTime(&ms, L->ev0, L->ev1));
+  g_last_ms = ms;
+  g_last_grid = L->grid;
+  for (int i = 0; i < art::N_STATS; ++i) g_last_stats[i] = st[i];
+  return ART_OK;
+}
+
+int propagate_host_maskless(DeviceCtx* c, HostLane* H, bool overlap, const art_params* p, int64_t n, const double* x0,
+                            const double* k0, const double* erg, const double* dw, const double* ln_t0,
+                            const int8_t* species, int32_t max_crossings, art_segment_out* out, art_crossing_buf* xc,
+                            const FluxArgs& fx) {
+  const int cap = (xc && xc->count) ? xc->capacity : 0;
+  const art::KParams K = kparams(*p);
+  int shift = 16;
+  while (((int64_t)1 << (shift + 1)) * 32 <= n) ++shift;  // 32..64 pieces (2^18 rays for 10^7: the last
+  // piece's finalize, copy and scatter are the call's tail, 95.3-96.5 ms against 98.4-101 with 2^19,
+  // profiles/r04ag_piece_shift.jsonl)
+  if (const int e = env_int("ART_HOST_PIECE_SHIFT", 0)) shift = std::max(10, e);  // (tests: many small pieces)
+  while (((n + ((int64_t)1 << shift) - 1) >> shift) > HSIG_NFLAG) ++shift;  // 64 piece counters and flags
+  const int np = (int)((n + ((int64_t)1 << shift) - 1) >> shift);
+  int rc;
+  if ((rc = lane_setup(c, H))) return rc;
   const size_t nd = (size_t)n;
   auto up = [](size_t b) { return (b + 255) & ~size_t(255); };
   const size_t in_bytes = nd * 9 * sizeof(double) + nd;  // x0 (3n) k0 (3n) erg dw lnt0 | species
@@ -980,17 +1112,16 @@ int propagate_host_maskless(DeviceCtx* c, const art_params* p, int64_t n, const 
   auto xd_off = [&](int64_t m) { return cnt_off(m) + up((size_t)m * sizeof(int32_t)); };
   auto out_bytes = [&](int64_t m) { return cap ? xd_off(m) + (size_t)cap * m * 9 * sizeof(double) : cnt_off(m); };
   const size_t stride = up(out_bytes((int64_t)1 << shift));
-  // scratch: head [queue | stats (8) | init_next (16) fin_next (17) chunk misses (18) | finished rays per piece from
-  // word 32 | finalized tiles per piece from word 96] | chunk flags | u0 16n | rec 16n | xrec
+  // scratch: head [queue | stats (10) | init_next (16) fin_next (17) chunk misses (18) exit count (19) waves done (20) |
+  // finished rays per piece from word 32 | finalized tiles per piece from word 96] | chunk flags | u0 16n | rec 16n | xrec
   const size_t nchunk = (nd + art::CHUNK - 1) / art::CHUNK;
   const size_t head = 2048, ccb = up(nchunk * sizeof(unsigned)), u0b = nd * 16 * sizeof(double),
                recb = nd * art::END_REC * sizeof(double);
   const size_t xrb = (size_t)cap * nd * art::X_REC * sizeof(double);
   void *pi, *po, *din, *dout, *dsc;
-  int rc;
-  if ((rc = pinned_get(c, 2, in_bytes, &pi)) || (rc = pinned_get(c, 3, stride * np, &po)) ||
-      (rc = pool_get(c, 20, in_bytes, &din)) || (rc = pool_get(c, 21, stride * np, &dout)) ||
-      (rc = pool_get(c, 22, head + ccb + u0b + recb + xrb, &dsc)))
+  if ((rc = pinned_get_v(H->pinned, 0, in_bytes, &pi)) || (rc = pinned_get_v(H->pinned, 1, stride * np, &po)) ||
+      (rc = pool_get_v(H->pool, 0, in_bytes, &din)) || (rc = pool_get_v(H->pool, 1, stride * np, &dout)) ||
+      (rc = pool_get_v(H->pool, 2, head + ccb + u0b + recb + xrb, &dsc)))
     return rc;
   double* pin = (double*)pi;
   double* di = (double*)din;
@@ -1012,53 +1143,61 @@ int propagate_host_maskless(DeviceCtx* c, const art_params* p, int64_t n, const 
     if (lo >= n) break;
   }
   const int nu = (int)ulo.size() - 1;
-  while ((int64_t)c->pev.size() < nu + np + 2) {
+  while ((int64_t)H->pev.size() < nu + np + 2) {
     hipEvent_t ev;
     HIP_OK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-    c->pev.push_back(ev);
+    H->pev.push_back(ev);
   }
-  hipEvent_t* ev_up = c->pev.data();
-  hipEvent_t* ev_dn = c->pev.data() + nu;
+  hipEvent_t* ev_up = H->pev.data();
+  hipEvent_t* ev_dn = H->pev.data() + nu;
   const bool trace = env_int("ART_HOST_TRACE", 0) != 0;
   auto clk = [] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
   const double t_start = clk();
-  unsigned long long* hready = c->hsig;
-  unsigned long long* hflag = c->hsig + 8;
+  unsigned long long* hready = H->hsig;
+  unsigned long long* hflag = H->hsig + 8;
+  unsigned long long* hdone = H->hsig + HSIG_DONE;
   __atomic_store_n(hready, 0ull, __ATOMIC_RELEASE);
-  for (int k = 0; k <= NFLAG; ++k) __atomic_store_n(hflag + k, 0ull, __ATOMIC_RELEASE);  // (+ the started count)
-  __atomic_store_n(c->abort_host, 0u, __ATOMIC_RELEASE);
-  HIP_OK(hipMemsetAsync(words, 0, head + ccb, c->m_comp));
+  for (int k = 0; k <= HSIG_NFLAG; ++k) __atomic_store_n(hflag + k, 0ull, __ATOMIC_RELEASE);  // (+ the started count)
+  __atomic_store_n(hdone, 0ull, __ATOMIC_RELEASE);
+  __atomic_store_n(H->abort_host, 0u, __ATOMIC_RELEASE);
+  HIP_OK(hipMemsetAsync(words, 0, head + ccb, H->m_comp));
+  // the batch's flux: binned by the helpers as they finalize (bins <= FLUX_HELPER_BINS), else by
+  // flux kernels over the pieces' blobs after the integrator
+  const bool hflux = fx.nbins > 0 && fx.nbins <= art::FLUX_HELPER_BINS;
   double* hist_dev = nullptr;
   if (fx.nbins) {
-    if ((rc = pool_get(c, 23, 2 * (size_t)fx.nbins * sizeof(double), (void**)&hist_dev))) return rc;
-    HIP_OK(hipMemsetAsync(hist_dev, 0, 2 * (size_t)fx.nbins * sizeof(double), c->m_comp));
+    if ((rc = pool_get_v(H->pool, 3, 2 * (size_t)fx.nbins * sizeof(double), (void**)&hist_dev))) return rc;
+    HIP_OK(hipMemsetAsync(hist_dev, 0, 2 * (size_t)fx.nbins * sizeof(double), H->m_comp));
   }
-  // the integrator, first: its waves wait for the first piece
-  LaunchRec* L;
-  if ((rc = take_slot(c, &L))) return rc;
   art::SegOut so{};
   so.rec = rec;
   so.cap = cap;
   so.xrec = xrec;
   so.xcount = cap ? (int32_t*)((char*)dout + cnt_off(piece_lo(1) - piece_lo(0))) : nullptr;  // (tested for null only)
   so.piece_cnt = words + 32;
-  so.abort_word = c->abort_dev;
+  so.abort_word = H->abort_dev;
+  so.queue_word = words;
   // (tests: ART_HOST_WAVE_WAIT_MS shortens a wave's bound on its chunk, s_memrealtime at 100 MHz)
   so.wait_ticks = env_int("ART_HOST_WAVE_WAIT_MS", 0) > 0 ? (unsigned long long)env_int("ART_HOST_WAVE_WAIT_MS", 0) * 100000ull
                                                          : art::STREAM_WAIT_TICKS;
   so.piece_shift = shift;
-  so.host_ready = c->hsig_dev;
-  so.host_flags = c->hsig_dev + 8;
+  so.host_ready = H->hsig_dev;
+  so.host_flags = H->hsig_dev + 8;
   so.init_next = words + 16;
   so.fin_next = words + 17;
   so.piece_fin = words + 96;
   so.chunk_ready = ccnt;
   so.blob = (char*)dout;
   so.blob_stride = (int64_t)stride;
+  so.flux_hist = hflux ? hist_dev : nullptr;
+  so.flux_nbins = hflux ? fx.nbins : 0;
+  so.done_host = H->hsig_dev + HSIG_DONE;
+  so.exit_count = words + 19;
+  so.waves_done = words + 20;
   int ncu = 0;
   HIP_OK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device));
   const int slots = std::max(2, env_int("ART_HOST_BLOCKS", 2 * ncu));  // block slots: 2 per CU
-  // helper blocks beside the integrator (ART_HOST_HELPERS, default 16): launched first, and the
+  // helper blocks beside the integrator (ART_HOST_HELPERS, default 8): launched first, and the
   // integrator only once every one of them is resident, so it cannot take their slots
   const int helpers = std::min(slots - 1, std::max(1, env_int("ART_HOST_HELPERS", 8)));
   so.helpers = helpers;
@@ -1066,50 +1205,69 @@ int propagate_host_maskless(DeviceCtx* c, const art_params* p, int64_t n, const 
   // integrator and finalized after it, kernel by kernel: for a counter-collection run, which
   // serialises kernels; the integrator's code and traffic are the same)
   const bool serial = env_int("ART_HOST_STREAM_SERIAL", 0) != 0;
-  hipEvent_t ev_zero = c->pev[nu + np];  // (the helpers start on zeroed counters)
-  HIP_OK(hipEventRecord(ev_zero, c->m_comp));
-  HIP_OK(hipStreamWaitEvent(c->m_help, ev_zero, 0));
-  if (!serial) HIP_OK(art::launch_helpers(K, n, in, so, helpers, -1, 1, words + 1, c->m_help));
-  if (!serial) {
+  // After the integrator, one pass of every block slot finalizes what is left -- unless this call
+  // overlaps the next one (art_propagate_host_flux_async): then the next call's integrator would
+  // hold those slots, and the helpers finalize alone
+  const bool final_pass = serial || !overlap;
+  const int iblocks = serial ? slots : slots - helpers;
+  const int igrid = (int)std::min((n + 255) / 256, (int64_t)iblocks);  // launch_integrator_streamed's grid
+  so.exit_expected = (serial ? 0 : helpers) + (final_pass ? slots : 0);
+  so.waves_expected = igrid * 4;
+  hipEvent_t ev_zero = H->pev[nu + np];  // (the helpers start on zeroed counters)
+  HIP_OK(hipEventRecord(ev_zero, H->m_comp));
+  HIP_OK(hipStreamWaitEvent(H->m_help, ev_zero, 0));
+  if (!serial) HIP_OK(art::launch_helpers(K, n, in, so, helpers, -1, 1, words + 1, H->m_help));
+  // the integrator, once every helper block is resident: before the uploads when they are at once
+  // (a lone call), else from the upload loop as soon as they are (a call overlapping the previous
+  // one, whose blocks hold the slots until its drain)
+  LaunchRec* L = nullptr;
+  bool launched = false;
+  auto helpers_in = [&] { return serial || __atomic_load_n(hflag + HSIG_NFLAG, __ATOMIC_ACQUIRE) >= (unsigned long long)helpers; };
+  auto launch_main = [&]() -> int {
+    std::lock_guard<std::mutex> rlk(g_ring_mu);
+    int r = take_slot(c, &L);
+    if (r) return r;
+    // every block slot initialises two rays per integrator lane before the integrator starts (258k
+    // rays; the first unit alone left the integrator's first waves waiting on 8 helpers: 33 ms
+    // against 18 per 1.25e6-ray call), then the helpers keep ahead (ART_HOST_INIT_RAYS: tests and
+    // A/B, another amount)
+    const int64_t first =
+        serial ? n : std::min(n, (int64_t)std::max(1, env_int("ART_HOST_INIT_RAYS", (slots - helpers) * 4 * 64 * 2)));
+    if (env_int("ART_HOST_INITPASS", 1))  // (dev: 0 leaves the first piece to the helpers)
+      HIP_OK(art::launch_helpers(K, n, in, so, iblocks, first, 0, words + 1, H->m_comp));
+    HIP_OK(hipEventRecord(L->ev0, H->m_comp));
+    int grid = 0;
+    HIP_OK(art::launch_integrator_streamed(K, n, in, so, max_crossings, words, words + 1, iblocks, H->m_comp, &grid));
+    L->grid = grid;
+    HIP_OK(hipEventRecord(L->ev1, H->m_comp));
+    if (final_pass) {
+      HIP_OK(art::launch_helpers(K, n, in, so, slots, -1, 0, words + 1, H->m_comp));
+      hipEvent_t ev_help = H->pev[nu + np + 1];  // (the persistent helpers' init counts, in the statistics)
+      HIP_OK(hipEventRecord(ev_help, H->m_help));
+      HIP_OK(hipStreamWaitEvent(H->m_comp, ev_help, 0));
+      HIP_OK(hipMemcpyAsync(L->host_stats, words + 1, sizeof(unsigned long long) * art::N_STATS_DEV,
+                            hipMemcpyDeviceToHost, H->m_comp));
+    }
+    // (overlapping calls: the statistics come from the helpers' completion words, and nothing
+    // after the integrator waits on this stream for CU slots the next call holds)
+    HIP_OK(hipEventRecord(L->done, H->m_comp));
+    L->stream = H->m_comp;
+    L->pending = true;
+    c->last = c->next;
+    c->next = (c->next + 1) % RING;
+    c->launches += 1;
+    launched = true;
+    return ART_OK;
+  };
+  if (helpers_in() || !overlap) {
     const double tw = clk();
-    while (__atomic_load_n(hflag + NFLAG, __ATOMIC_ACQUIRE) < (unsigned long long)helpers) {
-      if (clk() - tw > 5000.0) {  // (never seen: the device is shared or wedged) -- let them go, fall back
-        __atomic_store_n(c->abort_host, 1u, __ATOMIC_RELEASE);
-        (void)hipStreamSynchronize(c->m_help);
-        std::fprintf(stderr, "[art] maskless streamed pipeline: helper blocks did not start; running the batch again\n");
-        return STREAM_FALLBACK;
-      }
+    while (!helpers_in()) {
+      if (clk() - tw > 5000.0) break;  // (never seen: the device is shared or wedged; handled below)
       std::this_thread::sleep_for(std::chrono::microseconds(5));
     }
+    if (helpers_in() && (rc = launch_main())) return rc;
   }
-  // every block slot initialises the first piece, then the integrator, then every slot helps
-  // finalize what is left
-  // every block slot initialises two rays per integrator lane before the integrator starts (258k
-  // rays; the first unit alone left the integrator's first waves waiting on 8 helpers: 33 ms
-  // against 18 per 1.25e6-ray call), then the helpers keep ahead (ART_HOST_INIT_RAYS: tests and
-  // A/B, another amount)
-  const int64_t first =
-      serial ? n
-             : std::min(n, (int64_t)std::max(1, env_int("ART_HOST_INIT_RAYS", (slots - helpers) * 4 * 64 * 2)));
-  if (env_int("ART_HOST_INITPASS", 1))  // (dev: 0 leaves the first piece to the helpers)
-    HIP_OK(art::launch_helpers(K, n, in, so, serial ? slots : slots - helpers, first, 0, words + 1, c->m_comp));
-  HIP_OK(hipEventRecord(L->ev0, c->m_comp));
-  HIP_OK(art::launch_integrator_streamed(K, n, in, so, max_crossings, words, words + 1, serial ? slots : slots - helpers,
-                                         c->m_comp, &L->grid));
-  HIP_OK(hipEventRecord(L->ev1, c->m_comp));
-  HIP_OK(art::launch_helpers(K, n, in, so, slots, -1, 0, words + 1, c->m_comp));
-  hipEvent_t ev_help = c->pev[nu + np + 1];  // (the persistent helpers' init counts, in the statistics)
-  HIP_OK(hipEventRecord(ev_help, c->m_help));
-  HIP_OK(hipStreamWaitEvent(c->m_comp, ev_help, 0));
-  HIP_OK(hipMemcpyAsync(L->host_stats, words + 1, sizeof(unsigned long long) * art::N_STATS, hipMemcpyDeviceToHost,
-                        c->m_comp));
-  HIP_OK(hipEventRecord(L->done, c->m_comp));
-  L->stream = c->m_comp;
-  L->pending = true;
-  c->last = c->next;
-  c->next = (c->next + 1) % RING;
-  c->launches += 1;
-  // a host thread raises the ready counter as each piece's copies land
+  // a host thread raises the ready counter as each unit's copies land
   std::atomic<int> recorded{0};
   std::atomic<bool> stop{false};
   std::atomic<int> ready_err{0};
@@ -1163,8 +1321,8 @@ int propagate_host_maskless(DeviceCtx* c, const art_params* p, int64_t n, const 
     while (dk < np && __atomic_load_n(hflag + dk, __ATOMIC_ACQUIRE) != 0ull) {
       const int64_t m = piece_lo(dk + 1) - piece_lo(dk);
       if (hipMemcpyAsync((char*)po + stride * dk, (char*)dout + stride * dk, out_bytes(m), hipMemcpyDeviceToHost,
-                         c->m_dn) != hipSuccess ||
-          hipEventRecord(ev_dn[dk], c->m_dn) != hipSuccess)
+                         H->m_dn) != hipSuccess ||
+          hipEventRecord(ev_dn[dk], H->m_dn) != hipSuccess)
         return -1;
       if (trace) std::fprintf(stderr, "[art-host] t=%.2f piece %d done\n", clk() - t_start, dk);
       ++dk;
@@ -1187,6 +1345,7 @@ int propagate_host_maskless(DeviceCtx* c, const art_params* p, int64_t n, const 
   // waves outwait their 2 s bound and the device side gives the call up)
   const int delay_ms = env_int("ART_HOST_UPLOAD_DELAY_MS", 0);
   for (int u = 0; u < nu && !perr; ++u) {
+    if (!launched && helpers_in() && launch_main() != ART_OK) perr = 1;
     const int64_t lo = ulo[u], m = ulo[u + 1] - lo;
     if (delay_ms > 0 && u == 1) std::this_thread::sleep_for(std::chrono::milliseconds(delay_ms));
     const double* src[9] = {x0, x0 + n, x0 + 2 * n, k0, k0 + n, k0 + 2 * n, erg, dw, ln_t0};
@@ -1197,14 +1356,29 @@ int propagate_host_maskless(DeviceCtx* c, const art_params* p, int64_t n, const 
     copy_pool().run(g);
     for (int r = 0; r < 9 && !perr; ++r)
       perr |= hipMemcpyAsync(di + r * nd + lo, pin + r * nd + lo, (size_t)m * sizeof(double), hipMemcpyHostToDevice,
-                             c->m_up) != hipSuccess;
+                             H->m_up) != hipSuccess;
     perr |= hipMemcpyAsync((int8_t*)(di + 9 * nd) + lo, (int8_t*)(pin + 9 * nd) + lo, (size_t)m, hipMemcpyHostToDevice,
-                           c->m_up) != hipSuccess;
-    perr |= hipEventRecord(ev_up[u], c->m_up) != hipSuccess;
+                           H->m_up) != hipSuccess;
+    perr |= hipEventRecord(ev_up[u], H->m_up) != hipSuccess;
     recorded.store(u + 1, std::memory_order_release);
-    if (trace) std::fprintf(stderr, "[art-host] t=%.2f unit %d gathered in %.2f ms\n", tg0 - t_start, u, clk() - tg0);
+    if (trace) std::fprintf(stderr, "[art-host] t=%.2f unit %d gathered in %.2f ms%s\n", tg0 - t_start, u, clk() - tg0,
+                            launched ? "" : " (integrator not launched yet)");
     if (!perr && progress() < 0) perr = 1;
   }
+  if (!perr && !launched) {  // the helpers wait for CU slots the previous call still holds
+    const double tw = clk();
+    while (!helpers_in() && clk() - tw < 5000.0) {
+      if (progress() < 0) break;
+      std::this_thread::sleep_for(std::chrono::microseconds(20));
+    }
+    if (!helpers_in()) {
+      std::fprintf(stderr, "[art] maskless streamed pipeline: helper blocks did not start; running the batch again\n");
+      perr = 1;
+    } else if (launch_main() != ART_OK) {
+      perr = 1;
+    }
+  }
+  if (trace) std::fprintf(stderr, "[art-host] t=%.2f uploads submitted\n", clk() - t_start);
   const double limit_ms = (double)env_int("ART_HOST_STREAM_TIMEOUT_MS", 30000);
   double t_last = clk(), t_peek = clk();
   bool gave_up = perr != 0;
@@ -1214,8 +1388,8 @@ int propagate_host_maskless(DeviceCtx* c, const art_params* p, int64_t n, const 
   while (!gave_up && sk < np) {
     if (peek && clk() - t_peek > (double)env_int("ART_HOST_PEEK_MS", 100)) {
       t_peek = clk();
-      if (hipMemcpyAsync(peek, words, 160 * sizeof(unsigned long long), hipMemcpyDeviceToHost, c->m_dn) == hipSuccess &&
-          hipStreamSynchronize(c->m_dn) == hipSuccess) {
+      if (hipMemcpyAsync(peek, words, 160 * sizeof(unsigned long long), hipMemcpyDeviceToHost, H->m_dn) == hipSuccess &&
+          hipStreamSynchronize(H->m_dn) == hipSuccess) {
         unsigned long long fin = 0, tiles = 0;
         for (int k = 0; k < np; ++k) {
           fin += peek[32 + k];
@@ -1224,8 +1398,8 @@ int propagate_host_maskless(DeviceCtx* c, const art_params* p, int64_t n, const 
         std::fprintf(stderr, "[art-host] t=%.1f queue %llu init_next %llu fin_next %llu misses %llu finished %llu tiles %llu flags:",
                      clk() - t_start, peek[0], peek[16], peek[17], peek[18], fin, tiles);
         for (int k = 0; k < np; ++k) std::fprintf(stderr, "%llu", hflag[k]);
-        std::fprintf(stderr, " ready %llu started %llu abort %u init-pass %s integrator %s\n", *hready, hflag[NFLAG],
-                     *c->abort_host, hipEventQuery(L->ev0) == hipSuccess ? "done" : "running",
+        std::fprintf(stderr, " ready %llu started %llu abort %u init-pass %s integrator %s\n", *hready, hflag[HSIG_NFLAG],
+                     *H->abort_host, hipEventQuery(L->ev0) == hipSuccess ? "done" : "running",
                      hipEventQuery(L->ev1) == hipSuccess ? "done" : "running");
       }
     }
@@ -1238,24 +1412,36 @@ int propagate_host_maskless(DeviceCtx* c, const art_params* p, int64_t n, const 
       t_last = clk();
       continue;
     }
-    if (__atomic_load_n(c->abort_host, __ATOMIC_ACQUIRE) != 0u || clk() - t_last > limit_ms) {
+    if (__atomic_load_n(H->abort_host, __ATOMIC_ACQUIRE) != 0u || clk() - t_last > limit_ms) {
       gave_up = true;
       break;
     }
     std::this_thread::sleep_for(std::chrono::microseconds(20));
   }
+  // the call's end: the helpers' completion words (the statistics, the flux), raised by the last
+  // serving helper block once every integrator wave has counted itself (bounded like the pieces)
+  if (!gave_up) {
+    while (__atomic_load_n(hdone, __ATOMIC_ACQUIRE) == 0ull) {
+      if (__atomic_load_n(H->abort_host, __ATOMIC_ACQUIRE) != 0u || clk() - t_last > limit_ms) {
+        gave_up = true;
+        break;
+      }
+      std::this_thread::sleep_for(std::chrono::microseconds(10));
+    }
+  }
   stop = true;
   if (peek) (void)hipHostFree(peek);
   if (gave_up) {
-    // let the integrator run out (waves waiting for inputs stop on their own bound), then leave
-    // the batch to another path
-    __atomic_store_n(c->abort_host, 1u, __ATOMIC_RELEASE);
-    __atomic_store_n(hready, (unsigned long long)n, __ATOMIC_RELEASE);
+    // stop the launch, then leave the batch to another path: every wait of the helpers and the
+    // waves ends on the abort word, and a helper that sees it drains the work queue (queue_word),
+    // so the integrator stops at each wave's next chunk claim. (The ready counter is NOT raised:
+    // helpers would initialise tiles whose inputs never landed)
+    __atomic_store_n(H->abort_host, 1u, __ATOMIC_RELEASE);
     readier.join();
-    (void)hipStreamSynchronize(c->m_up);
-    (void)hipStreamSynchronize(c->m_comp);
-    (void)hipStreamSynchronize(c->m_help);
-    (void)hipStreamSynchronize(c->m_dn);
+    (void)hipStreamSynchronize(H->m_up);
+    (void)hipStreamSynchronize(H->m_comp);
+    (void)hipStreamSynchronize(H->m_help);
+    (void)hipStreamSynchronize(H->m_dn);
     (void)hipGetLastError();
     if (trace) {  // the device counters at the give-up
       std::vector<unsigned long long> w(160);
@@ -1267,61 +1453,49 @@ int propagate_host_maskless(DeviceCtx* c, const art_params* p, int64_t n, const 
       }
     }
     std::fprintf(stderr, "[art] maskless streamed pipeline gave up at piece %d of %d (abort=%u); running the batch again\n",
-                 sk, np, *c->abort_host);
+                 sk, np, *H->abort_host);
     return STREAM_FALLBACK;
   }
   readier.join();
   if (trace) std::fprintf(stderr, "[art-host] maskless total %.2f ms (%d pieces of 2^%d)\n", clk() - t_start, np, shift);
-  if (fx.nbins) {  // the flux of every piece's blob, once the integrator is done (a few hundred µs)
+  const bool complete = __atomic_load_n(hdone, __ATOMIC_ACQUIRE) == 1ull;
+  if (fx.nbins && hflux && complete) {
+    for (int b = 0; b < 2 * fx.nbins; ++b) {
+      const unsigned long long v = __atomic_load_n(hdone + art::DONE_FLUX + b, __ATOMIC_ACQUIRE);
+      std::memcpy(fx.hist + b, &v, sizeof(double));
+    }
+  } else if (fx.nbins) {  // flux kernels over the pieces' blobs, once the integrator is done
+    if (hflux) HIP_OK(hipMemsetAsync(hist_dev, 0, 2 * (size_t)fx.nbins * sizeof(double), H->m_comp));
     for (int k = 0; k < np; ++k) {
       const int64_t lo = piece_lo(k), m = piece_lo(k + 1) - lo;
       double* dd = (double*)((char*)dout + stride * k);
       const int32_t* st = (const int32_t*)(dd + 8 * m);
-      HIP_OK(art::launch_flux(K, m, dd, dd + 3 * m, st, in.species + lo, nullptr, fx.nbins, hist_dev, c->m_comp));
+      HIP_OK(art::launch_flux(K, m, dd, dd + 3 * m, st, in.species + lo, nullptr, fx.nbins, hist_dev, H->m_comp));
     }
-    HIP_OK(hipMemcpyAsync(fx.hist, hist_dev, 2 * (size_t)fx.nbins * sizeof(double), hipMemcpyDeviceToHost, c->m_comp));
-    HIP_OK(hipStreamSynchronize(c->m_comp));
+    HIP_OK(hipMemcpyAsync(fx.hist, hist_dev, 2 * (size_t)fx.nbins * sizeof(double), hipMemcpyDeviceToHost, H->m_comp));
+    HIP_OK(hipStreamSynchronize(H->m_comp));
   }
-  return finish_timing(c);
+  if (complete && !final_pass) {  // the statistics from the completion words
+    unsigned long long st[art::N_STATS_DEV];
+    for (int i = 0; i < art::N_STATS_DEV; ++i) st[i] = __atomic_load_n(hdone + art::DONE_STATS + i, __ATOMIC_ACQUIRE);
+    return latch_launch(c, L, st);
+  }
+  if (!final_pass) {  // (the helpers' copy timed out: the statistics as the stream has them)
+    HIP_OK(hipMemcpyAsync(L->host_stats, words + 1, sizeof(unsigned long long) * art::N_STATS_DEV, hipMemcpyDeviceToHost,
+                          H->m_comp));
+    HIP_OK(hipStreamSynchronize(H->m_comp));
+  }
+  return finish_timing_slot(c, L);
 }
 
-int propagate_host_impl(const art_params* p, int64_t n, const double* x0, const double* k0, const double* erg,
-                        const double* dw, const double* ln_t0, const int8_t* species, int32_t max_crossings,
-                        art_segment_out* out, art_crossing_buf* xc, const TrajArgs& htr,
-                        const FluxArgs& fx = FluxArgs()) {
-  bool empty = false;
-  int rc = check_segment_args(p, n, x0, k0, erg, dw, ln_t0, species, out, xc, htr, &empty);
-  if (rc) return rc;
-  if (fx.nbins && (fx.nbins < 1 || fx.nbins > 4096 || !fx.hist)) return fail(ART_E_INVALID, "flux needs nbins in [1, 4096] and hist");
-  if (fx.nbins) std::fill(fx.hist, fx.hist + 2 * (size_t)fx.nbins, 0.0);
-  if (empty) return rc;
-  DeviceCtx* c;
-  if ((rc = current_ctx(&c))) return rc;
-  g_host_cnt[HC_CALLS] += 1;
-  // large batches (ART_HOST_CHUNK_MIN rays and more, default 2^20, so the 1.25e6-ray shard of
-  // 8 GPUs streams: 18.3 ms against 20.0 in one launch, profiles/r04x_shard_sizes.jsonl; no
-  // saveat): the streamed pipeline (ART_HOST_MODE=stream, the default, Vern6) or the chunked
-  // one (=chunked); smaller
-  // batches, RK4, saveat, ART_HOST_MODE=single and a streamed call that gave up take the single
-  // launch below
-  const char* mode_env = std::getenv("ART_HOST_MODE");
-  const std::string mode = (mode_env && *mode_env) ? mode_env : "stream";
-  if (htr.ntimes == 0 && n >= env_int("ART_HOST_CHUNK_MIN", 1 << 20)) {
-    if (mode == "stream" && p->integrator == ART_VERN6) {
-      rc = propagate_host_maskless(c, p, n, x0, k0, erg, dw, ln_t0, species, max_crossings, out, xc, fx);
-      if (rc != STREAM_FALLBACK) {
-        if (rc == ART_OK) g_host_cnt[HC_STREAMED] += 1;
-        return rc;
-      }
-      g_host_cnt[HC_GIVEUPS] += 1;
-    } else if (mode == "chunked") {
-      g_host_cnt[HC_CHUNKED] += 1;
-      return propagate_host_chunked(c, p, n, x0, k0, erg, dw, ln_t0, species, max_crossings, out, xc,
-                                    std::max(2, env_int("ART_HOST_CHUNKS", 4)), std::max(1, env_int("ART_HOST_SLOTS", 2)),
-                                    fx);
-    }
-  }
-  g_host_cnt[HC_SINGLE] += 1;
+// The single-launch host path: the inputs up, one propagate launch (init, integrator, finalize),
+// the outputs back, all on stream s with device staging from `pool` (slots pb .. pb + 4): the
+// context's own for synchronous calls, a host lane's for an asynchronous call's fallback.
+int propagate_host_single(DeviceCtx* c, hipStream_t s, PoolVec& pool, size_t pb, const art_params* p, int64_t n,
+                          const double* x0, const double* k0, const double* erg, const double* dw, const double* ln_t0,
+                          const int8_t* species, int32_t max_crossings, art_segment_out* out, art_crossing_buf* xc,
+                          const TrajArgs& htr, const FluxArgs& fx) {
+  int rc;
   const int cap = (xc && xc->count) ? xc->capacity : 0;
   const size_t nd = (size_t)n;
   // staging layout: inputs 3n+3n+n+n+n doubles + n int8; outputs 3n+3n+n+n doubles + 3n int32 (+ crossings)
@@ -1330,11 +1504,10 @@ int propagate_host_impl(const art_params* p, int64_t n, const double* x0, const 
   const size_t out_bytes = nd * 8 * sizeof(double) + nd * 3 * sizeof(int32_t);
   const size_t cnt_bytes = ((nd * sizeof(int32_t) + 15) / 16) * 16;
   const size_t xc_bytes = cap ? cnt_bytes + (size_t)cap * nd * 9 * sizeof(double) : 0;
-  if ((rc = pool_get(c, 0, in_bytes, &din))) return rc;
-  if ((rc = pool_get(c, 1, out_bytes, &dout))) return rc;
-  if (cap && (rc = pool_get(c, 2, xc_bytes, &dxc))) return rc;
+  if ((rc = pool_get_v(pool, pb + 0, in_bytes, &din))) return rc;
+  if ((rc = pool_get_v(pool, pb + 1, out_bytes, &dout))) return rc;
+  if (cap && (rc = pool_get_v(pool, pb + 2, xc_bytes, &dxc))) return rc;
   double* di = (double*)din;
-  hipStream_t s = c->stream;
   HIP_OK(hipMemcpyAsync(di, x0, nd * 3 * sizeof(double), hipMemcpyHostToDevice, s));
   HIP_OK(hipMemcpyAsync(di + 3 * nd, k0, nd * 3 * sizeof(double), hipMemcpyHostToDevice, s));
   HIP_OK(hipMemcpyAsync(di + 6 * nd, erg, nd * sizeof(double), hipMemcpyHostToDevice, s));
@@ -1356,7 +1529,7 @@ int propagate_host_impl(const art_params* p, int64_t n, const double* x0, const 
   if (htr.ntimes != 0) {
     void* dt_ = nullptr;
     const size_t nt = (size_t)htr.ntimes * nd;
-    if ((rc = pool_get(c, 7, nt * 4 * sizeof(double) + nd * sizeof(int32_t), &dt_))) return rc;
+    if ((rc = pool_get_v(pool, pb + 3, nt * 4 * sizeof(double) + nd * sizeof(int32_t), &dt_))) return rc;
     dtr.ntimes = htr.ntimes;
     dtr.traj = (double*)dt_;
     dtr.t = dtr.traj + 3 * nt;
@@ -1366,12 +1539,14 @@ int propagate_host_impl(const art_params* p, int64_t n, const double* x0, const 
   // held: finalize_kernel writes them (LaunchOpts::nan_fill)
   LaunchOpts opt;
   opt.nan_fill = true;
+  LaunchRec* L = nullptr;
+  opt.launch_out = &L;
   rc = propagate_device_impl(p, n, di, di + 3 * nd, di + 6 * nd, di + 7 * nd, di + 8 * nd, (const int8_t*)(di + 9 * nd),
-                             max_crossings, &dso, dxbp, s, dtr, opt);
+                             max_crossings, &dso, dxbp, s, dtr, opt, c);
   if (rc) return rc;
   if (fx.nbins) {  // the batch's flux from its outputs in HBM
     double* hist_dev = nullptr;
-    if ((rc = pool_get(c, 23, 2 * (size_t)fx.nbins * sizeof(double), (void**)&hist_dev))) return rc;
+    if ((rc = pool_get_v(pool, pb + 4, 2 * (size_t)fx.nbins * sizeof(double), (void**)&hist_dev))) return rc;
     HIP_OK(hipMemsetAsync(hist_dev, 0, 2 * (size_t)fx.nbins * sizeof(double), s));
     HIP_OK(art::launch_flux(kparams(*p), n, dso.x_end, dso.k_end, dso.status, (const int8_t*)(di + 9 * nd), nullptr,
                             fx.nbins, hist_dev, s));
@@ -1399,7 +1574,118 @@ int propagate_host_impl(const art_params* p, int64_t n, const double* x0, const 
     HIP_OK(hipMemcpyAsync(xc->p_nonad, dxb.p_nonad, (size_t)cap * nd * sizeof(double), hipMemcpyDeviceToHost, s));
   }
   HIP_OK(hipStreamSynchronize(s));
-  return finish_timing(c);
+  return finish_timing_slot(c, L);
+}
+
+// Synchronous host calls wait for every asynchronous one first: they share lane 0 and the
+// context's staging (art_propagate_host_flux_async).
+void drain_async(DeviceCtx* c) {
+  for (HostLane& H : c->lanes) {
+    std::unique_lock<std::mutex> lk(H.m);
+    H.cv.wait(lk, [&] { return !H.busy; });
+  }
+}
+
+// Which path a host call of n rays takes: the streamed pipeline for large Vern6 batches without
+// saveat (ART_HOST_CHUNK_MIN rays and more, default 2^20, so the 1.25e6-ray shard of 8 GPUs
+// streams: 18.3 ms against 20.0 in one launch, profiles/r04x_shard_sizes.jsonl), the chunked one
+// with ART_HOST_MODE=chunked; the single launch otherwise (and after a streamed call gave up)
+enum HostPath { HP_STREAM, HP_CHUNKED, HP_SINGLE };
+HostPath host_path(const art_params* p, int64_t n, const TrajArgs& htr) {
+  const char* mode_env = std::getenv("ART_HOST_MODE");
+  const std::string mode = (mode_env && *mode_env) ? mode_env : "stream";
+  if (htr.ntimes == 0 && n >= env_int("ART_HOST_CHUNK_MIN", 1 << 20)) {
+    if (mode == "stream" && p->integrator == ART_VERN6) return HP_STREAM;
+    if (mode == "chunked") return HP_CHUNKED;
+  }
+  return HP_SINGLE;
+}
+
+int host_args(const art_params* p, int64_t n, const double* x0, const double* k0, const double* erg, const double* dw,
+              const double* ln_t0, const int8_t* species, art_segment_out* out, art_crossing_buf* xc, const TrajArgs& htr,
+              const FluxArgs& fx, bool* empty) {
+  int rc = check_segment_args(p, n, x0, k0, erg, dw, ln_t0, species, out, xc, htr, empty);
+  if (rc) return rc;
+  if (fx.nbins && (fx.nbins < 1 || fx.nbins > 4096 || !fx.hist)) return fail(ART_E_INVALID, "flux needs nbins in [1, 4096] and hist");
+  if (fx.nbins) std::fill(fx.hist, fx.hist + 2 * (size_t)fx.nbins, 0.0);
+  return ART_OK;
+}
+
+int propagate_host_impl(const art_params* p, int64_t n, const double* x0, const double* k0, const double* erg,
+                        const double* dw, const double* ln_t0, const int8_t* species, int32_t max_crossings,
+                        art_segment_out* out, art_crossing_buf* xc, const TrajArgs& htr,
+                        const FluxArgs& fx = FluxArgs()) {
+  bool empty = false;
+  int rc = host_args(p, n, x0, k0, erg, dw, ln_t0, species, out, xc, htr, fx, &empty);
+  if (rc || empty) return rc;
+  DeviceCtx* c;
+  if ((rc = current_ctx(&c))) return rc;
+  drain_async(c);
+  g_host_cnt[HC_CALLS] += 1;
+  const HostPath hp = host_path(p, n, htr);
+  if (hp == HP_STREAM) {
+    rc = propagate_host_maskless(c, &c->lanes[0], false, p, n, x0, k0, erg, dw, ln_t0, species, max_crossings, out, xc, fx);
+    if (rc != STREAM_FALLBACK) {
+      if (rc == ART_OK) g_host_cnt[HC_STREAMED] += 1;
+      return rc;
+    }
+    g_host_cnt[HC_GIVEUPS] += 1;
+  } else if (hp == HP_CHUNKED) {
+    g_host_cnt[HC_CHUNKED] += 1;
+    return propagate_host_chunked(c, p, n, x0, k0, erg, dw, ln_t0, species, max_crossings, out, xc,
+                                  std::max(2, env_int("ART_HOST_CHUNKS", 4)), std::max(1, env_int("ART_HOST_SLOTS", 2)), fx);
+  }
+  g_host_cnt[HC_SINGLE] += 1;
+  return propagate_host_single(c, c->stream, c->pool, 0, p, n, x0, k0, erg, dw, ln_t0, species, max_crossings, out, xc,
+                               htr, fx);
+}
+
+// The asynchronous calls' workers: one thread per host lane, one call at a time.
+void lane_worker(DeviceCtx* c, HostLane* H) {
+  (void)hipSetDevice(c->device);
+  for (;;) {
+    std::function<int()> job;
+    {
+      std::unique_lock<std::mutex> lk(H->m);
+      H->cv.wait(lk, [&] { return H->stop || (bool)H->job; });
+      if (!H->job) return;  // (stop, nothing left)
+      job = std::move(H->job);
+      H->job = nullptr;
+    }
+    job();
+    {
+      std::lock_guard<std::mutex> lk(H->m);
+      H->busy = false;
+    }
+    H->cv.notify_all();
+  }
+}
+
+// Ticket t runs on lane t % HOST_LANES once that lane's previous call has ended; its result waits
+// in c->results for art_host_wait.
+int64_t submit_async(DeviceCtx* c, std::function<int(HostLane*)> body) {
+  const int64_t t = c->next_ticket++;
+  HostLane* H = &c->lanes[t % HOST_LANES];
+  {
+    std::lock_guard<std::mutex> lk(c->res_m);
+    c->pending.insert(t);
+  }
+  {
+    std::unique_lock<std::mutex> lk(H->m);
+    H->cv.wait(lk, [&] { return !H->busy; });
+    H->busy = true;
+    H->job = [c, H, t, body] {
+      g_err.clear();
+      const int rc = body(H);
+      std::lock_guard<std::mutex> lk2(c->res_m);
+      c->results[t] = {rc, g_err};
+      c->res_cv.notify_all();
+      return rc;
+    };
+    if (!H->worker.joinable()) H->worker = std::thread(lane_worker, c, H);
+  }
+  H->cv.notify_all();
+  return t;
 }
 }  // namespace
 
@@ -1423,13 +1709,74 @@ int art_propagate_host_flux(const art_params* p, int64_t n, const double* x0, co
   return propagate_host_impl(p, n, x0, k0, erg, dw, ln_t0, species, max_crossings, out, xc, TrajArgs(), fx);
 }
 
+int art_propagate_host_flux_async(const art_params* p, int64_t n, const double* x0, const double* k0, const double* erg,
+                                  const double* dw, const double* ln_t0, const int8_t* species, int32_t max_crossings,
+                                  art_segment_out* out, art_crossing_buf* xc, int32_t nbins, double* hist, int64_t* ticket) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (!ticket) return fail(ART_E_INVALID, "ticket is NULL");
+  if (nbins < 1) return fail(ART_E_INVALID, "nbins must be >= 1");
+  FluxArgs fx;
+  fx.nbins = nbins;
+  fx.hist = hist;
+  bool empty = false;
+  int rc = host_args(p, n, x0, k0, erg, dw, ln_t0, species, out, xc, TrajArgs(), fx, &empty);
+  if (rc) return rc;
+  DeviceCtx* c;
+  if ((rc = current_ctx(&c))) return rc;
+  if (empty || host_path(p, n, TrajArgs()) != HP_STREAM) {
+    // (a batch the streamed pipeline does not take runs now, in this thread; its ticket is complete)
+    const int rc1 = empty ? ART_OK : propagate_host_impl(p, n, x0, k0, erg, dw, ln_t0, species, max_crossings, out, xc,
+                                                          TrajArgs(), fx);
+    const std::string e1 = g_err;
+    *ticket = submit_async(c, [rc1, e1](HostLane*) {
+      g_err = e1;
+      return rc1;
+    });
+    return ART_OK;
+  }
+  g_host_cnt[HC_CALLS] += 1;
+  const art_params pc = *p;  // (the caller's structs by value: they may go out of scope before the call ends)
+  art_segment_out oc = *out;
+  const bool has_xc = xc != nullptr;
+  art_crossing_buf xcc = has_xc ? *xc : art_crossing_buf{};
+  *ticket = submit_async(c, [=](HostLane* H) mutable {
+    int r = propagate_host_maskless(c, H, true, &pc, n, x0, k0, erg, dw, ln_t0, species, max_crossings, &oc,
+                                    has_xc ? &xcc : nullptr, fx);
+    if (r == STREAM_FALLBACK) {  // the batch again as one launch, on this lane's stream and staging
+      g_host_cnt[HC_GIVEUPS] += 1;
+      g_host_cnt[HC_SINGLE] += 1;
+      if (fx.nbins) std::fill(fx.hist, fx.hist + 2 * (size_t)fx.nbins, 0.0);
+      r = propagate_host_single(c, H->m_comp, H->pool, 4, &pc, n, x0, k0, erg, dw, ln_t0, species, max_crossings, &oc,
+                                has_xc ? &xcc : nullptr, TrajArgs(), fx);
+    } else if (r == ART_OK) {
+      g_host_cnt[HC_STREAMED] += 1;
+    }
+    return r;
+  });
+  return ART_OK;
+}
+
+int art_host_wait(int64_t ticket) {
+  DeviceCtx* c;
+  int rc = current_ctx(&c);
+  if (rc) return rc;
+  std::unique_lock<std::mutex> lk(c->res_m);
+  if (!c->pending.count(ticket)) return fail(ART_E_INVALID, "unknown ticket, or one already waited for");
+  c->res_cv.wait(lk, [&] { return c->results.count(ticket) > 0; });
+  const std::pair<int, std::string> r = c->results[ticket];
+  c->results.erase(ticket);
+  c->pending.erase(ticket);
+  if (r.first != ART_OK) g_err = r.second;
+  return r.first;
+}
+
 int art_host_path_counters(uint64_t* counters, int32_t n, int32_t reset) {
   std::lock_guard<std::mutex> lk(g_mu);
   if (n < 0 || (n > 0 && !counters)) return fail(ART_E_INVALID, "bad buffer");
   for (int i = 0; i < n && i < HC_N; ++i) counters[i] = g_host_cnt[i];
   for (int i = HC_N; i < n; ++i) counters[i] = 0;
   if (reset)
-    for (uint64_t& v : g_host_cnt) v = 0;
+    for (auto& v : g_host_cnt) v = 0;
   return HC_N;
 }
 

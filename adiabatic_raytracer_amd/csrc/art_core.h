@@ -24,7 +24,7 @@
 // how many uses each product has at the inlined site, and it differed between the two in the
 // scan and the back-transform). The ray equations' right-hand side keeps "fast" contraction
 // (ART_FP_FAST at the top of its functions): it is 2% of the headline kernel's time faster
-// that way, and its roundings were checked equal between the kernels (tools/exp_tail_trace*.py).
+// that way, and its roundings were checked equal between the kernels (the ART_TRACE per-attempt build; the trace tools are in git history).
 #if defined(__clang__)
 #define ART_FP_FAST _Pragma("clang fp contract(fast)")
 #else

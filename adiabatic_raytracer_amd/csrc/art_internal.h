@@ -58,19 +58,23 @@ struct SegOut {
   // long (STREAM_WAIT_TICKS of s_memrealtime) raises *abort_word and stops taking rays.
   unsigned long long* piece_cnt;
   unsigned int* abort_word;
+  // the launch's work-queue word: a helper that sees the call given up adds 2^40 to it, so every
+  // integrator wave's next chunk claim finds the queue drained and the launch runs out at once
+  unsigned long long* queue_word;
   unsigned long long wait_ticks;  // a wave's bound on a chunk flag (STREAM_WAIT_TICKS; tests set less)
   int32_t piece_shift;
   // The maskless streamed pipeline (DON = 3, art_capi.cpp propagate_host_maskless): one launch
   // over the whole batch holds every CU; its first `helpers` blocks are helpers, not
   // integrators. *host_ready (host memory, raised by the host as each piece's copies land)
-  // counts rays whose inputs are in HBM. Helpers claim 256-ray tiles to initialise
+  // counts rays whose inputs are in HBM. Helpers claim 1024-ray tiles (HELPER_TILE) to initialise
   // (*init_next, init_one) and set chunk_ready[c] for each 64-ray chunk they finish; an
   // integrator wave that claims a chunk waits for its flag. Finished rays count into
   // piece_cnt[p] as in DON = 2; once a piece is complete, helpers claim its tiles to finalize
   // (*fin_next, finalize_one) into the piece's SoA blob (blob + p blob_stride, piece_blob), and
   // the block that finalizes a piece's last tile sets host_flags[p] (host memory the host
-  // polls, then copies the blob out). Integrator blocks become helpers when their waves run out
-  // of rays; every block initialises tiles of the first piece before it integrates.
+  // polls, then copies the blob out). The helpers are a separate persistent kernel on a stream of
+  // their own; one helper pass over every block slot initialises the first rays before the
+  // integrator starts, and another finalizes the rest after it.
   const unsigned long long* host_ready;
   unsigned long long* host_flags;
   unsigned long long *init_next, *fin_next;
@@ -79,6 +83,18 @@ struct SegOut {
   char* blob;
   int64_t blob_stride;
   int32_t helpers;
+  // The end of a streamed call without the integrator's stream (art_capi.cpp, HostLane): the
+  // helpers bin the radiated flux of the rays they finalize (flux_hist, 2 flux_nbins doubles of
+  // device memory, flux_nbins <= FLUX_HELPER_BINS; 0 = none), every integrator wave counts itself
+  // into *waves_done after its statistics, and the last of the exit_expected serving helper blocks
+  // to leave (*exit_count) waits for waves_expected of them, then copies the statistics
+  // (stats[0, N_STATS_DEV)) and the flux into host memory (done_host[DONE_STATS...], [DONE_FLUX...])
+  // and raises done_host[0]. The host then has the call's results without waiting on a stream.
+  double* flux_hist;
+  int32_t flux_nbins;
+  unsigned long long* done_host;
+  unsigned long long *exit_count, *waves_done;
+  int32_t exit_expected, waves_expected;
   // Small batches (art_capi.cpp, propagate_device_impl): 1 = every fresh ray goes straight to
   // tail_kernel, one wave per ray (pack_fresh_kernel writes their CONT_REC records to cont),
   // instead of one lane per ray of the persistent integrator
@@ -93,13 +109,19 @@ struct SegOut {
   int32_t grad_cap, graduate;
 };
 constexpr unsigned long long STREAM_WAIT_TICKS = 200000000ull;  // 2 s at 100 MHz
+constexpr int FLUX_HELPER_BINS = 256;  // flux bins the helpers bin themselves (2 x 256 doubles of LDS)
+constexpr int DONE_STATS = 1, DONE_FLUX = 16;  // done_host layout: [0] flag | [1, 11) statistics | [16, 16 + 2 nbins) flux
 constexpr int CHUNK = 64;  // rays a persistent wave claims from the queue at once
 constexpr int HELPER_TILE = 1024;  // rays a helper block initialises or finalizes per claim
 constexpr int END_REC = 16;
 constexpr int X_REC = 8;
 constexpr int CONT_REC = 24;  // [u (7) | f (7) | τ, dt, qpow, cprev, bstart, erg | int4 {ray, n_acc, n_rej, ncross} | int4 {iter, sprev, flags, save_k}]
 constexpr int N_STATS = 8;  // propagate statistics: attempts, accepted, root re-steps, scan evals,
-                            // interpolant-root evals, rays, init RHS, (reserved)
+                            // interpolant-root evals, rays, init RHS, certified steps (art_last_stats)
+// ... followed by the integrator's span from in-kernel clock stamps (s_memrealtime, the device's
+// 100 MHz constant clock): [8] the max over waves of ~(start), [9] the max of the end
+constexpr int ST_T0 = 8, ST_T1 = 9, N_STATS_DEV = 10;
+constexpr double STAMP_TICKS_PER_MS = 1e5;
 int persistent_blocks(const void* func, int64_t work, int block, int fallback_per_cu);
 // propagate = init (u0 of every ray) -> the persistent integrator -> finalize (Cartesian
 // end state, conversion probability at the crossings); ev0/ev1 (may be null) bracket the

@@ -174,6 +174,17 @@ __device__ inline double scan_point_lds(const KParams& P, const double* S, int s
   return 0.5 * N / D;  // = condition_t, bit for bit
 }
 
+// The integrator's span from in-kernel clock stamps (stats[ST_T0], stats[ST_T1]: the earliest
+// wave start as the max of ~t, the latest wave end): s_memrealtime is the device's one 100 MHz
+// constant clock, so the figure is the launch's own duration without a profiler's completion
+// signals (art_recent_kernel_span_ms). Two atomics per wave.
+__device__ inline void span_stamp(unsigned long long* stats, bool end) {
+  if ((threadIdx.x & 63) == 0) {
+    const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+    atomicMax(stats + (end ? ST_T1 : ST_T0), end ? t : ~t);
+  }
+}
+
 // Completes this wave's LDS traffic before other lanes of the same wave read it.
 __device__ inline void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -484,13 +495,43 @@ __device__ inline unsigned init_one(const KParams& P, int64_t n, int64_t i, cons
   return nrhs;
 }
 
+// np.histogram's bin of x for `nbins` equal bins over [-π, π] (numpy 2.x histogram: the
+// index from (x - lo) / (hi - lo) * nbins, then corrected against the edges of
+// linspace(lo, hi, nbins + 1) = i * ((hi - lo) / nbins) + lo, the right edge in the last bin),
+// with the same roundings: no contraction into FMAs. -1 outside [lo, hi] (and for NaN).
+// The range defaults to flux_kernel's fixed [-π, π]; flux_phi_kernel also takes a data-dependent
+// one (np.histogram(a, bins) without `range` bins over [a.min(), a.max()], plot/flux.py:43-47).
+__device__ inline int np_hist_bin(double x, int nbins, double lo = -PI, double hi = PI) {
+#pragma clang fp contract(off)  // numpy rounds every product and sum (HIP's __dmul_rn would still fuse)
+  if (!(x >= lo && x <= hi)) return -1;
+  const double span = hi - lo;
+  int i = (int)(((x - lo) / span) * (double)nbins);
+  if (i == nbins) i -= 1;
+  const double step = span / (double)nbins;
+  const double e0 = (double)i * step + lo;
+  if (x < e0) i -= 1;
+  const double e1 = (i + 1 == nbins) ? hi : (double)(i + 1) * step + lo;
+  if (x >= e1 && i != nbins - 1) i += 1;
+  return i;
+}
+
+// The radiated-flux bin of one segment's end state (plot/flux.py:38-48 over a batch's escaping
+// segments): is_final -- no crossing and escaped beyond 1.1 rNS (MainRunner.jl:203-209) -- and
+// the azimuth of its momentum binned as np.histogram(range = (-π, π)); -1 = not counted.
+// flux_kernel and the streamed pipeline's helpers (finalize_one) both bin through here.
+__device__ inline int flux_bin_of(const KParams& P, const double* x, const double* k, int status, int nbins) {
+  const double xr = sqrt(x[0] * x[0] + x[1] * x[1] + x[2] * x[2]);
+  if (status == ART_STATUS_CROSSING || !(xr > 1.1 * P.rNS)) return -1;
+  return np_hist_bin(atan2(k[1], k[0]), nbins);
+}
+
 // End state of ray i in Cartesian form (back-transform, RayTracer.jl:393-416) from the raw end
 // record the integrator left in out.rec, spread into the SoA outputs at o (row stride m), and
 // the conversion probability of every recorded crossing (get_Prob_nonAD with Nc = 1,
 // MainRunner.jl:265). finalize_kernel runs it one thread per ray; the maskless streamed
 // integrator (DON = 3) for each chunk whose rays have all finished.
 __device__ inline void finalize_one(const KParams& P, int64_t n, int64_t i, int64_t o, int64_t m, const SegIn& in,
-                                    const SegOut& out) {
+                                    const SegOut& out, double* fl = nullptr, int fl_nbins = 0) {
   const double erg = in.erg[i];
   int ncross = 0;
   {
@@ -513,6 +554,10 @@ __device__ inline void finalize_one(const KParams& P, int64_t n, int64_t i, int6
     ncross = ri.w;
     if (out.xcount) out.xcount[o] = ncross;
     if (out.ntimes >= 2) out.traj_n[o] = reinterpret_cast<const int4*>(rq + 4)[1].x;
+    if (fl) {  // (the streamed pipeline's helpers: the ray's radiated-flux bin, an exact count)
+      const int bin = flux_bin_of(P, xe, ke, ri.x, fl_nbins);
+      if (bin >= 0) atomicAdd(&fl[(in.species[i] == ART_AXION ? 0 : 1) * fl_nbins + bin], 1.0);
+    }
   }
   if (out.ntimes >= 2) {  // saveat: start (u0 back-transformed), interior to Cartesian, end
     double u0[7], xs[3], ks[3];
@@ -569,7 +614,7 @@ __device__ inline void finalize_one(const KParams& P, int64_t n, int64_t i, int6
   }
 }
 
-// (DON = 3) the SoA output blob of piece p (art_capi.cpp, propagate_host_streamed: the same
+// (DON = 3) the SoA output blob of piece p (art_capi.cpp, propagate_host_maskless: the same
 // layout and 256-byte alignments), its rows m long
 __device__ inline SegOut piece_blob(const SegOut& out, int64_t n, int p, int64_t& m) {
   const int64_t lo = (int64_t)p << out.piece_shift;
@@ -606,6 +651,9 @@ __device__ inline unsigned long long ld_sys(const unsigned long long* p) {
 }
 __device__ inline unsigned long long ld_agent(const unsigned long long* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ inline bool ld_abort(const SegOut& out) {
+  return __hip_atomic_load(out.abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u;
 }
 
 // (DON = 3) the claimed chunk's fresh state: its flag as the leader lane reads it now, or after
@@ -668,6 +716,7 @@ __global__ __launch_bounds__(BLOCK, WPS) void propagate_kernel(const KParams P_i
   const int npts = P.interp_points;
   for (int j = threadIdx.x; j < npts; j += BLOCK) thgrid[j] = double(j) / double(npts - 1);
   if constexpr (DON == 3) pend_lds[threadIdx.x >> 6][threadIdx.x & 63] = 0u;
+  span_stamp(stats, false);
   __syncthreads();
 
   int mode = M_IDLE;
@@ -865,13 +914,22 @@ __global__ __launch_bounds__(BLOCK, WPS) void propagate_kernel(const KParams P_i
     double kA[7], y[7], kk[7];
 #pragma unroll
     for (int i = 0; i < 7; ++i) kA[i] = 0.0;  // read (times a zero coefficient) before its first store
+#ifdef ART_SLOT_PREFETCH
+    // (dev A/B) the next slot's row of scalars loaded before this slot's RHS, so its scalar-load
+    // latency hides behind the RHS instead of opening the next slot
+    SlotRow Rnext = T.row[0];
+#endif
 #pragma unroll SUNROLL
     for (int s = 0; s < NSLOT; ++s) {
 #ifdef ART_PRIO_GLUE  // (dev A/B) the stage combination's LDS reads at the high priority
       if (outlier) __builtin_amdgcn_s_setprio(3);
       else __builtin_amdgcn_s_setprio(1);
 #endif
+#ifdef ART_SLOT_PREFETCH
+      const SlotRow R = Rnext;
+#else
       const SlotRow R = T.row[s];
+#endif
       const double cf = R.cf, cA = R.cA;
       double acc[7];
 #pragma unroll
@@ -895,6 +953,9 @@ __global__ __launch_bounds__(BLOCK, WPS) void propagate_kernel(const KParams P_i
 #pragma unroll
       for (int i = 0; i < 7; ++i) y[i] = u[i] + hs * acc[i];
       const double ty = tau + R.ct * hs;
+#ifdef ART_SLOT_PREFETCH
+      Rnext = T.row[s + 1 < NSLOT ? s + 1 : s];
+#endif
       ART_SMARK(8)
 #ifdef ART_PRIO_GLUE
       if (outlier) __builtin_amdgcn_s_setprio(2);
@@ -1581,9 +1642,8 @@ __global__ __launch_bounds__(BLOCK, WPS) void propagate_kernel(const KParams P_i
     }
   }
 
-  if constexpr (DON == 3) stream_flush(out, pend_lds[threadIdx.x >> 6], lane);
-
-  // wave-reduce the statistics and add them once per wave
+  // wave-reduce the statistics and add them once per wave (DON = 3: before the wave counts itself
+  // done and flushes its last piece counts, so the helper that ends the call finds them complete)
 #if defined(ART_SLOT_TIMING)
   if (lane == 0) {  // [refill etc, combination, RHS, slot rest, norm..park, grid, fast+walk+coop, fallback]
     const unsigned long long v[8] = {t_sec[0], t_sec[8] + t_sec[1], t_sec[9], t_sec[10], t_sec[2], t_sec[3],
@@ -1614,6 +1674,14 @@ __global__ __launch_bounds__(BLOCK, WPS) void propagate_kernel(const KParams P_i
     if (lane == 0 && x) atomicAdd(&stats[slot[k]], x);
   }
 #endif
+  span_stamp(stats, true);
+  if constexpr (DON == 3) {
+    if (out.waves_done) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      if (lane == 0) __hip_atomic_fetch_add(out.waves_done, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    stream_flush(out, pend_lds[threadIdx.x >> 6], lane);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1714,6 +1782,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
                                                                                    : (int64_t)out.grad_cap)
                               : 0;
   bool grads = ng > 0;
+  span_stamp(stats, false);
   while (true) {
     const double* src = nullptr;
     while (src == nullptr) {
@@ -2210,6 +2279,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
     for (int k = 0; k < 6; ++k)
       if (v[k]) atomicAdd(&stats[slot[k]], (unsigned long long)v[k]);
   }
+  span_stamp(stats, true);
 }
 
 // Small batches (SegOut::small_tail): every fresh ray as a CONT_REC record for tail_kernel, the
@@ -2259,7 +2329,7 @@ __global__ __launch_bounds__(256) void pack_fresh_kernel(const int64_t n, const 
 //   HK_INIT  rays [i0, i1): fresh state into in.u0 (grid-stride over 256-ray tiles);
 //   HK_FIN   rays [i0, i1): the end state into `out` at o = i - i0, row stride i1 - i0;
 //   HK_TILES the maskless streamed pipeline's helper duty (SegOut::host_ready ...): claim
-//            256-ray tiles to initialise once the host's copies of their inputs have landed,
+//            1024-ray tiles (S3_TILE) to initialise once the host's copies of their inputs have landed,
 //            and tiles of each finished piece to finalize into its blob; flag each initialised
 //            chunk (chunk_ready, which the integrator's waves poll) and each finalized piece
 //            (host_flags, which the host polls). init_limit >= 0: initialise only, until every
@@ -2275,7 +2345,13 @@ __global__ __launch_bounds__(256) void helper_kernel(const KParams P, const int6
                                                      const int64_t init_limit, const int announce,
                                                      unsigned long long* __restrict__ stats) {
   __shared__ long long cmd[2];  // HK_TILES: [what, tile]: 0 nothing now, 1 initialise, 2 finalize, 3 done
+  __shared__ double hfl[2 * FLUX_HELPER_BINS];  // (HK_TILES with SegOut::flux_hist) this block's flux counts
+  __shared__ int last_out, complete;
   const int tid = threadIdx.x;
+  const bool flb = mode == HK_TILES && out.flux_hist != nullptr;
+  if (flb)
+    for (int b = tid; b < 2 * out.flux_nbins; b += 256) hfl[b] = 0.0;
+  __syncthreads();
   const int64_t full = (int64_t)1 << out.piece_shift;
   auto piece_rays = [&](int p) {
     const int64_t lo = (int64_t)p << out.piece_shift;
@@ -2286,6 +2362,7 @@ __global__ __launch_bounds__(256) void helper_kernel(const KParams P, const int6
   unsigned long long hr = 0;  // (HK_TILES, thread 0) host_ready as last read: it only grows
   long long pend = -1;  // (HK_TILES, thread 0) a claimed finalize tile whose piece is still running
   unsigned long long t_idle = __builtin_amdgcn_s_memrealtime();
+  unsigned npoll = 0;  // (HK_TILES, thread 0) claim rounds: every 16th reads the abort word
   unsigned nrhs = 0;
   if (mode == HK_TILES && announce && tid == 0)
     __hip_atomic_fetch_add(out.host_flags + 64, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -2298,8 +2375,11 @@ __global__ __launch_bounds__(256) void helper_kernel(const KParams P, const int6
       tile += gridDim.x;
     } else {
       if (tid == 0) {
+        // a given-up call (the host's or a wave's abort word) ends here: every 16th claim round
+        // reads the word (a host-memory load, ~2 us), every wait below reads it each time
+        if ((++npoll & 15u) == 0u && ld_abort(out)) what = 3;
         const unsigned long long inext = ld_agent(out.init_next);
-        if (init_limit >= 0 && (int64_t)inext >= init_limit) what = 3;
+        if (what == 0 && init_limit >= 0 && (int64_t)inext >= init_limit) what = 3;
         if (what == 0 && (int64_t)inext < n && inext >= hr) hr = ld_sys(out.host_ready);
         if (what == 0 && (int64_t)inext < n && inext < hr) {
           if (init_limit >= 0) {
@@ -2364,6 +2444,9 @@ __global__ __launch_bounds__(256) void helper_kernel(const KParams P, const int6
           __hip_atomic_store(out.abort_word, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
           what = 3;
         }
+        // aborted: drain the integrator's work queue, so each of its waves stops at its next
+        // chunk claim instead of integrating every chunk the helpers had flagged
+        if (what == 3 && out.queue_word && ld_abort(out)) atomicAdd(out.queue_word, 1ull << 40);
         if (what == 1 || what == 2) {
           t_idle = __builtin_amdgcn_s_memrealtime();
           // the inputs the DMA engines wrote / the end records other CUs wrote
@@ -2393,7 +2476,7 @@ __global__ __launch_bounds__(256) void helper_kernel(const KParams P, const int6
     }
     for (int64_t i = t + tid; i < t1; i += 256) {  // (one call site of each)
       if (what == 1) nrhs += init_one(P, n, i, in);
-      else finalize_one(P, n, i, i - ob, m, in, ol);
+      else finalize_one(P, n, i, i - ob, m, in, ol, flb ? hfl : nullptr, out.flux_nbins);
     }
     if (mode == HK_TILES) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -2420,6 +2503,47 @@ __global__ __launch_bounds__(256) void helper_kernel(const KParams P, const int6
   unsigned long long x = nrhs;  // init RHS evaluations -> stats[6]
   for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off);
   if ((tid & 63) == 0 && x) atomicAdd(&stats[6], x);
+  if (mode == HK_TILES && init_limit < 0 && out.exit_count) {
+    // the end of the call (SegOut::done_host): this block's flux counts into the call's histogram
+    // (sums of 1.0: exact in any order), then the last serving block out copies the statistics
+    // and the flux into host memory and raises the flag the host waits for
+    __syncthreads();
+    if (flb)
+      for (int b = tid; b < 2 * out.flux_nbins; b += 256)
+        if (hfl[b] != 0.0) atomicAdd(out.flux_hist + b, hfl[b]);
+    __syncthreads();
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const unsigned long long old = __hip_atomic_fetch_add(out.exit_count, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      last_out = (old + 1ull == (unsigned long long)out.exit_expected) ? 1 : 0;
+    }
+    __syncthreads();
+    if (last_out) {
+      if (tid == 0) {  // the integrator's waves have added their statistics (they count themselves after)
+        const unsigned long long w0 = __builtin_amdgcn_s_memrealtime();
+        bool ok = true;
+        while (ld_agent(out.waves_done) < (unsigned long long)out.waves_expected) {
+          if (ld_abort(out) || __builtin_amdgcn_s_memrealtime() - w0 > STREAM_WAIT_TICKS) { ok = false; break; }
+          __builtin_amdgcn_s_sleep(8);
+        }
+        complete = ok ? 1 : 2;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      }
+      __syncthreads();
+      for (int k = tid; k < N_STATS_DEV; k += 256)
+        __hip_atomic_store(out.done_host + DONE_STATS + k, ld_agent(stats + k), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (out.flux_hist)
+        for (int b = tid; b < 2 * out.flux_nbins; b += 256)
+          __hip_atomic_store(out.done_host + DONE_FLUX + b, ld_agent(reinterpret_cast<const unsigned long long*>(out.flux_hist) + b),
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __syncthreads();
+      if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // (system scope)
+        __hip_atomic_store(out.done_host, (unsigned long long)complete, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -2852,25 +2976,6 @@ __global__ __launch_bounds__(256) void prob_kernel(const KParams P, const int64_
   }
 }
 
-// np.histogram's bin of x for `nbins` equal bins over [-π, π] (numpy 2.x histogram: the
-// index from (x - lo) / (hi - lo) * nbins, then corrected against the edges of
-// linspace(lo, hi, nbins + 1) = i * ((hi - lo) / nbins) + lo, the right edge in the last bin),
-// with the same roundings: no contraction into FMAs. -1 outside [lo, hi] (and for NaN).
-// The range defaults to flux_kernel's fixed [-π, π]; flux_phi_kernel also takes a data-dependent
-// one (np.histogram(a, bins) without `range` bins over [a.min(), a.max()], plot/flux.py:43-47).
-__device__ inline int np_hist_bin(double x, int nbins, double lo = -PI, double hi = PI) {
-#pragma clang fp contract(off)  // numpy rounds every product and sum (HIP's __dmul_rn would still fuse)
-  if (!(x >= lo && x <= hi)) return -1;
-  const double span = hi - lo;
-  int i = (int)(((x - lo) / span) * (double)nbins);
-  if (i == nbins) i -= 1;
-  const double step = span / (double)nbins;
-  const double e0 = (double)i * step + lo;
-  if (x < e0) i -= 1;
-  const double e1 = (i + 1 == nbins) ? hi : (double)(i + 1) * step + lo;
-  if (x >= e1 && i != nbins - 1) i += 1;
-  return i;
-}
 
 // ---------------------------------------------------------------------------
 // Binned flux (plot/flux.py:38-48): φf = atan2(k_y, k_x) of final particles, per species.
@@ -2882,10 +2987,8 @@ __global__ __launch_bounds__(256) void flux_kernel(const KParams P, const int64_
   for (int i = threadIdx.x; i < 2 * nbins; i += blockDim.x) sh[i] = 0.0;
   __syncthreads();
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const double xr = sqrt(x_end[i] * x_end[i] + x_end[n + i] * x_end[n + i] + x_end[2 * n + i] * x_end[2 * n + i]);
-    // is_final: no crossing and escaped beyond 1.1 rNS (MainRunner.jl:203-209)
-    if (status[i] == ART_STATUS_CROSSING || !(xr > 1.1 * P.rNS)) continue;
-    const int bin = np_hist_bin(atan2(k_end[n + i], k_end[i]), nbins);  // np.histogram(range = (-π, π))
+    const double x[3] = {x_end[i], x_end[n + i], x_end[2 * n + i]}, k[3] = {k_end[i], k_end[n + i], k_end[2 * n + i]};
+    const int bin = flux_bin_of(P, x, k, status[i], nbins);
     if (bin < 0) continue;
     const int row = (species && species[i] == ART_AXION) ? 0 : 1;
     atomicAdd(&sh[row * nbins + bin], w ? w[i] : 1.0);
@@ -3134,31 +3237,6 @@ hipError_t launch_propagate(const KParams& P, int64_t n, const SegIn& in, const 
   }
   KFn fn = out.donate > 0 ? pick_propagate<1>(out.ntimes >= 2, rk4, flat, sch)
                            : pick_propagate<0>(out.ntimes >= 2, rk4, flat, sch);
-  // (dev A/B, ART_DEV_STREAMED_KERNEL=3: the streamed pipeline's integrator build on a
-  // device-resident batch -- every chunk flagged in -- to price its extra code against this
-  // launch's own, profiles/r04s3_streamed_kernel_ab.jsonl)
-  if (const char* e = std::getenv("ART_DEV_STREAMED_KERNEL")) {
-    if (std::atoi(e) == 3 && flat && !rk4 && out.ntimes < 2 && out.donate <= 0) {
-      static void* dbuf = nullptr;
-      static size_t dbytes = 0;
-      const size_t need = 4096 + ((size_t)n / CHUNK + 1) * sizeof(unsigned);
-      if (dbytes < need) {
-        if (dbuf) (void)hipFree(dbuf);
-        if (hipMalloc(&dbuf, need) != hipSuccess) return hipErrorOutOfMemory;
-        dbytes = need;
-      }
-      unsigned long long* w = (unsigned long long*)dbuf;
-      (void)hipMemsetAsync(w, 0, 4096, s);
-      (void)hipMemsetAsync((char*)dbuf + 4096, 1, need - 4096, s);
-      out.piece_cnt = w + 32;
-      out.piece_shift = 19;
-      out.chunk_ready = (unsigned*)((char*)dbuf + 4096);
-      out.init_next = w + 16;
-      out.abort_word = (unsigned*)(w + 8 * 60);
-      out.wait_ticks = STREAM_WAIT_TICKS;
-      fn = propagate_kernel<ART_VERN6, GEOM_FLAT, false, 3>;
-    }
-  }
   // A batch that fits one ray per lane of 1 wave per SIMD runs the 1-wave/SIMD build, which
   // does not spill: lone GR tail ray -3%, flat -4.5% per attempt, bit-identical
   // (profiles/r02j_small_batch_w1_ab.txt, tests/test_edges.py). ART_W1=0 switches it off (A/B).
@@ -3167,7 +3245,11 @@ hipError_t launch_propagate(const KParams& P, int64_t n, const SegIn& in, const 
     int dev = 0, ncu = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+#ifndef ART_W1_ALWAYS
     if (n <= (int64_t)ncu * 4 * 64) {
+#else
+    if (true) {  // (dev A/B build: the 1-wave/SIMD integrator for every batch, the occupancy sensitivity)
+#endif
       fn = flat ? propagate_kernel<ART_VERN6, GEOM_FLAT, false, 0, 1> : propagate_kernel<ART_VERN6, GEOM_GR, false, 0, 1>;
       w1 = true;
     }

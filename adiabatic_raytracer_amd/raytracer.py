@@ -182,7 +182,10 @@ def propagate_batch(params: Params, x0, k0, erg, dw, ln_t0, species, max_crossin
     With ntimes >= 2 (art_propagate_traj_host) also the saved points of RayTracer.jl:176,383:
     traj (3, ntimes, n) Cartesian positions, traj_t (ntimes, n) ln t, traj_n (n) points.
     With flux_nbins (art_propagate_host_flux) also `flux` (2, flux_nbins): the batch's binned
-    radiated flux (plot/flux.py:38-48), axions in row 0, photons in row 1."""
+    radiated flux (plot/flux.py:38-48), axions in row 0, photons in row 1. The two are separate
+    entry points of the C ABI: asking for both raises ValueError."""
+    if ntimes and flux_nbins:
+        raise ValueError("ntimes (saveat) and flux_nbins are separate entry points: ask for one of them")
     lib = _lib.load()
     n = int(np.asarray(erg).size)
     f64 = lambda a: np.ascontiguousarray(a, np.float64)  # noqa: E731
@@ -220,6 +223,48 @@ def propagate_batch(params: Params, x0, k0, erg, dw, ln_t0, species, max_crossin
     return out
 
 
+class HostCall:
+    """An asynchronous art_propagate_host_flux call (propagate_batch_async): holds the call's
+    arrays until wait() returns its outputs (the dict propagate_batch returns)."""
+
+    def __init__(self, ticket, out, keep):
+        self.ticket, self.out, self._keep = ticket, out, keep
+
+    def wait(self) -> dict:
+        check(_lib.load().art_host_wait(self.ticket))
+        self.out["flux"] = self.out["flux"].reshape(2, -1)
+        self._keep = None
+        return self.out
+
+
+def propagate_batch_async(params: Params, x0, k0, erg, dw, ln_t0, species, flux_nbins, max_crossings=-1,
+                          capacity=1) -> HostCall:
+    """art_propagate_host_flux_async: the call runs on a library worker thread (two per device
+    in flight, the next batch's uploads and first rays overlapping this one's drain); wait() on
+    the returned HostCall gives propagate_batch's dict, bit for bit the synchronous call's."""
+    lib = _lib.load()
+    n = int(np.asarray(erg).size)
+    f64 = lambda a: np.ascontiguousarray(a, np.float64)  # noqa: E731
+    x0, k0, erg, dw, ln_t0 = f64(x0), f64(k0), f64(erg), f64(dw), f64(ln_t0)
+    species = np.ascontiguousarray(species, np.int8)
+    if x0.size != 3 * n or k0.size != 3 * n or dw.size != n or ln_t0.size != n or species.size != n:
+        raise ValueError("inconsistent batch sizes")
+    out = {"x_end": np.zeros(3 * n), "k_end": np.zeros(3 * n), "u7_end": np.zeros(n), "tau_end": np.zeros(n),
+           "status": np.zeros(n, np.int32), "n_accept": np.zeros(n, np.int32), "n_reject": np.zeros(n, np.int32),
+           "n_cross": np.zeros(n, np.int32), "xc_pos": np.zeros(3 * capacity * n), "xc_k": np.zeros(3 * capacity * n),
+           "xc_t": np.zeros(capacity * n), "xc_dw": np.zeros(capacity * n), "xc_p": np.zeros(capacity * n),
+           "capacity": capacity, "flux": np.zeros(2 * int(flux_nbins))}
+    so = SegmentOut(*[_ptr(out[k]) for k in ("x_end", "k_end", "u7_end", "tau_end", "status", "n_accept",
+                                               "n_reject")])
+    xb = CrossingBuf(capacity, *[_ptr(out[k]) for k in ("n_cross", "xc_pos", "xc_k", "xc_t", "xc_dw", "xc_p")])
+    cp = params.to_c()
+    ticket = C.c_int64(-1)
+    check(lib.art_propagate_host_flux_async(C.byref(cp), n, _ptr(x0), _ptr(k0), _ptr(erg), _ptr(dw), _ptr(ln_t0),
+                                            _ptr(species), int(max_crossings), C.byref(so), C.byref(xb),
+                                            int(flux_nbins), _ptr(out["flux"]), C.byref(ticket)))
+    return HostCall(ticket.value, out, (x0, k0, erg, dw, ln_t0, species, so, xb, cp))
+
+
 def last_stats() -> dict:
     lib = _lib.load()
     s = (C.c_uint64 * 8)()
@@ -232,6 +277,18 @@ def last_stats() -> dict:
 
 
 HOST_PATH_KEYS = ("calls", "streamed", "stream_giveups", "chunked", "single")
+
+
+def recent_kernel_span_ms(n: int = 1) -> list:
+    """The last n propagate launches' integrator spans [ms] from in-kernel clock stamps (first
+    wave start to last wave end, art_recent_kernel_span_ms), oldest first: the launch's own
+    duration, free of a profiler's completion signals; -1 where a launch left no stamps."""
+    lib = _lib.load()
+    buf = (C.c_double * max(1, n))()
+    got = lib.art_recent_kernel_span_ms(int(n), buf)
+    if got < 0:
+        check(got)
+    return list(buf)[:got]
 
 
 def host_path_counters(reset=False) -> dict:

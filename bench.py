@@ -108,12 +108,14 @@ def host_arrays(inp, n):
     return h, out
 
 
-def timed(run, steps, warmup, world, sync):
+def timed(run, steps, warmup, world, sync, drain=lambda: None):
     """W untimed warmup steps, then EXACTLY `steps` steps bracketed by a barrier and a device
-    synchronize on both sides; returns this rank's elapsed seconds."""
+    synchronize on both sides; returns this rank's elapsed seconds. `drain` completes the steps
+    still in flight (host calls submitted asynchronously) before each synchronize."""
     import torch.distributed as dist
     for i in range(warmup):
         run(i)
+    drain()
     sync()
     if world > 1:
         dist.barrier()
@@ -121,6 +123,7 @@ def timed(run, steps, warmup, world, sync):
     t0 = time.perf_counter()
     for i in range(steps):
         run(warmup + i)
+    drain()
     sync()
     if world > 1:
         dist.barrier()
@@ -145,12 +148,17 @@ def main():
     ap.add_argument("--cpu-rays-1t", type=int, default=int(os.environ.get("ART_CPU_RAYS_1T", "24000")))
     ap.add_argument("--donate", type=int, default=-1,
                     help="tail donation lanes for the device-resident passes in flight; -1: auto")
+    ap.add_argument("--inflight", type=int, default=0,
+                    help="host calls in flight per rank (art_propagate_host_flux_async: the next batch's uploads and "
+                         "first rays overlap this one's drain); 0: 1 for per-GPU batches of >= 8e6 rays, else 2")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-device", action="store_true", help="skip the device-resident side figures")
     ap.add_argument("--no-pcie", action="store_true", help="(compat) same as --no-device")
     args = ap.parse_args()
     n_shard = args.rays // max(1, int(os.environ.get("WORLD_SIZE", "1")))  # this rank's share (to within one ray)
     gr = not CONFIGS[args.config].get("flat", False)
+    if args.inflight <= 0:
+        args.inflight = 1 if n_shard >= 8_000_000 else 2
     if args.streams <= 0:
         # device-resident side figure only (value is one host call per batch). The drain tail
         # (~3 ms: the last long rays) is ~3% of a 1e7-ray pass but ~20% of the 1.25e6 rays per GPU
@@ -206,25 +214,55 @@ def main():
     # integrator / finalize kernels, every output back into the caller's arrays, the batch's
     # binned flux from the outputs while they are in HBM) and the all-reduce of that flux over
     # the ranks (RCCL over xGMI; the path's only exchange, north_star).
-    h, hout = host_arrays(inp, n)
+    h, out0 = host_arrays(inp, n)
     P = lambda a: a.ctypes.data_as(C.c_void_p)  # noqa: E731
-    so = SegmentOut(*[P(hout[k]) for k in ("x_end", "k_end", "u7_end", "tau_end", "status", "n_accept", "n_reject")])
-    xb = CrossingBuf(1, *[P(hout[k]) for k in ("n_cross", "xc_pos", "xc_k", "xc_t", "xc_dw", "xc_p")])
-    hflux = np.zeros(2 * args.nbins)
+    # one set of output arrays per call in flight (the inputs are only read)
+    sets = []
+    for j in range(args.inflight):
+        o = host_arrays(inp, n)[1] if j else out0
+        sets.append({"out": o, "flux": np.zeros(2 * args.nbins),
+                     "so": SegmentOut(*[P(o[k]) for k in ("x_end", "k_end", "u7_end", "tau_end", "status", "n_accept",
+                                                         "n_reject")]),
+                     "xb": CrossingBuf(1, *[P(o[k]) for k in ("n_cross", "xc_pos", "xc_k", "xc_t", "xc_dw", "xc_p")])})
     flux_red = {}
+    pending = []  # (ticket, set) of the calls in flight, oldest first
+    ins = [P(h[k]) for k in ("x0", "k0", "erg", "dw", "ln_t0", "species")]
+
+    def reduce_flux(st):
+        t = torch.from_numpy(st["flux"].copy())
+        flux_red["host"] = allreduce_flux(t.to(eng.device) if hist_dev else t, world)
+        flux_red["set"] = st
+
+    def wait_oldest():
+        tk, st = pending.pop(0)
+        check(lib.art_host_wait(tk))
+        reduce_flux(st)
 
     def host_step(i):
-        check(lib.art_propagate_host_flux(C.byref(eng.cp), n, *[P(h[k]) for k in ("x0", "k0", "erg", "dw", "ln_t0",
-                                                                                 "species")],
-                                          -1, C.byref(so), C.byref(xb), args.nbins, P(hflux)))
-        t = torch.from_numpy(hflux.copy())
-        flux_red["host"] = allreduce_flux(t.to(eng.device) if hist_dev else t, world)
+        st = sets[i % args.inflight]
+        if args.inflight == 1:
+            check(lib.art_propagate_host_flux(C.byref(eng.cp), n, *ins, -1, C.byref(st["so"]), C.byref(st["xb"]),
+                                              args.nbins, P(st["flux"])))
+            reduce_flux(st)
+            return
+        if len(pending) == args.inflight:
+            wait_oldest()
+        tk = C.c_int64(-1)
+        check(lib.art_propagate_host_flux_async(C.byref(eng.cp), n, *ins, -1, C.byref(st["so"]), C.byref(st["xb"]),
+                                                args.nbins, P(st["flux"]), C.byref(tk)))
+        pending.append((tk.value, st))
+
+    def drain():
+        while pending:
+            wait_oldest()
 
     A.raytracer.host_path_counters(reset=True)
     for i in range(args.warmup):  # (the first call also allocates the pinned staging and streams)
         host_step(i)
+    drain()
     cnt_w = A.raytracer.host_path_counters(reset=True)
-    host_s = timed(host_step, args.steps, 0, world, sync)
+    host_s = timed(host_step, args.steps, 0, world, sync, drain)
+    hout = flux_red["set"]["out"]  # (the last call's outputs)
     cnt = A.raytracer.host_path_counters()
     # every timed pass ran the path its size selects, and none gave up and ran twice
     assert cnt["stream_giveups"] == 0, f"streamed host pipeline gave up inside the timed passes: {cnt}"
@@ -232,6 +270,7 @@ def main():
     kms_buf = (C.c_double * args.steps)()
     got = lib.art_recent_kernel_ms(args.steps, kms_buf)
     host_kms = list(kms_buf)[:max(0, got)]
+    host_span = A.raytracer.recent_kernel_span_ms(args.steps)  # the same launches, in-kernel clock stamps
     host_stats = A.raytracer.last_stats()
     assert int(hout["n_accept"].sum()) == host_stats["accepted"]
     host_steps_total, host_t_max, total_rays = reduce_totals(host_stats["accepted"] * args.steps, host_s, n, world,
@@ -261,6 +300,7 @@ def main():
             el = timed(one_step, steps, warmup, world, sync)
             kb = (C.c_double * steps)()
             g = lib.art_recent_kernel_ms(steps, kb)
+            span = A.raytracer.recent_kernel_span_ms(steps)
             eng.kernel_ms()  # latches the last launch's counters
             st = A.raytracer.last_stats()
             k_last = (warmup + steps - 1) % len(streams)
@@ -268,6 +308,7 @@ def main():
             tot, tmax, _ = reduce_totals(st["accepted"] * steps, el, n, world, device=eng.device)
             eng.set_tail_donation(-1)
             return {"value": tot / tmax, "ms_per_step": tmax / steps * 1e3, "kernel_ms": float(np.mean(list(kb)[:g])),
+                    "kernel_span_ms": float(np.mean(span)) if span else None,
                     "streams": nstreams, "tail_donation": donate_lanes, "elapsed_s": el, "stats": st,
                     "hist": hists[k_last].cpu().numpy()}
         dev = {"one": device_run(1, -1, args.steps, args.warmup)}  # (-1: the library default by geometry)
@@ -297,6 +338,9 @@ def main():
         kms = float(np.mean(host_kms))
         fpl = flops_per_launch(host_stats, fl, args.integrator)
         host_ms = host_t_max / args.steps * 1e3
+        # one call at a time: the integrator launch's own duration; calls in flight overlap each
+        # other's launches, so the wall per call is the basis (as for device_resident_in_flight)
+        basis_ms = kms if args.inflight == 1 else host_ms
         ncross = int(np.minimum(hout["n_cross"], 1).sum())
         att = (hout["n_accept"].astype(np.float64) + hout["n_reject"])
         q = np.quantile(att, [0.5, 0.99, 0.999])
@@ -331,14 +375,22 @@ def main():
                        "m_a_eV": params.mass_a, "theta_m": params.theta_m, "omega_pul": params.omega_pul,
                        "B0_G": params.B0, "rNS_km": params.rNS, "abstol": params.abstol, "reltol": params.reltol,
                        "interp_points": params.interp_points, "parallelism": f"rays sharded x{world}",
+                       "host_calls_in_flight": args.inflight,
                        "host_path": ("streamed pipeline" if streamed else
                                      "single launch" if cnt["single"] == args.steps else str(cnt)),
                        "host_path_counters": cnt, "host_path_counters_warmup": cnt_w},
-            "roofline": {"bound": "fp64-valu", "achieved": fpl / (kms * 1e-3) / 1e12, "peak": PEAK_FP64_TFLOPS,
-                         "unit": "TFLOP/s", "frac": fpl / (kms * 1e-3) / 1e12 / PEAK_FP64_TFLOPS,
+            "roofline": {"bound": "fp64-valu", "achieved": fpl / (basis_ms * 1e-3) / 1e12, "peak": PEAK_FP64_TFLOPS,
+                         "unit": "TFLOP/s", "frac": fpl / (basis_ms * 1e-3) / 1e12 / PEAK_FP64_TFLOPS,
                          "traffic": tr, "traffic_source": tr_src, "kernel": kname, "kernel_ms": kms,
-                         "time_basis": "the integrator launch's own duration (HIP events on its stream), mean over "
-                                       "the timed passes",
+                         "time_basis": ("the integrator launch's own duration (HIP events on its stream), mean over "
+                                        "the timed passes" if args.inflight == 1 else
+                                        f"wall per host call ({args.inflight} calls in flight overlap their launches)"),
+                         "kernel_span_ms": float(np.mean(host_span)) if host_span else None,
+                         "kernel_span_ms_each": host_span,
+                         "frac_span": (fpl / (np.mean(host_span) * 1e-3) / 1e12 / PEAK_FP64_TFLOPS) if host_span else None,
+                         "span_basis": "the same launches from in-kernel clock stamps (first wave start to last wave "
+                                       "end, s_memrealtime at 100 MHz; art_recent_kernel_span_ms): no profiler",
+                         "kernel_ms_each": host_kms,
                          "achieved_wall": fpl / (host_ms * 1e-3) / 1e12,
                          "frac_wall": fpl / (host_ms * 1e-3) / 1e12 / PEAK_FP64_TFLOPS,
                          "wall_basis": "the whole host pass (ms_per_step: H2D + kernels + D2H)",
@@ -370,6 +422,7 @@ def main():
                                   "frac": fpl_d / (basis * 1e-3) / 1e12 / PEAK_FP64_TFLOPS,
                                   "kernel": "propagate_kernel<Vern6>" if args.integrator == "vern6" else
                                             "propagate_kernel<RK4>", "kernel_ms": d["kernel_ms"],
+                                  "kernel_span_ms": d["kernel_span_ms"],
                                   "time_basis": ("launch duration (HIP events)" if d["streams"] == 1 else
                                                  f"wall per launch ({d['streams']} overlapping passes)"),
                                   "traffic": trd if d["streams"] == 1 else None,

@@ -20,6 +20,7 @@
  *   art_flux_histogram_phi_device  plot/flux.py:38-48 (binned flux of the npy rows' φf;
  *   art_flux_histogram_phi_range_device  _range: over flux.py's data-dependent bins)
  *   art_propagate_host_flux        RT.propagate + the batch's binned flux (bench.py's step)
+ *   art_propagate_host_flux_async  the same, two batches in flight; art_host_wait
  *   art_comm_* / art_flux_allreduce  the reduction of the flux and counters over the GPUs of
  *                                  a node (the reference merges files instead,
  *                                  Combine_Files.py, Gen_Samples.jl:195-239)
@@ -157,6 +158,11 @@ int art_last_stats(uint64_t* stats, int32_t* grid);
  * device, oldest first, each from the HIP events around that launch on its own stream (waits
  * for them). Returns the number written (>= 0) or a negative ART_E* code. */
 int art_recent_kernel_ms(int32_t n, double* ms);
+/* The same launches' integrator spans [ms] from in-kernel clock stamps: the first wave's start
+ * to the last wave's end on the device's 100 MHz constant clock (s_memrealtime), so free of a
+ * profiler's per-dispatch completion signals; -1 where a launch left none. Returns the number
+ * written (>= 0) or a negative ART_E* code. (No reference counterpart: measurement) */
+int art_recent_kernel_span_ms(int32_t n, double* ms);
 /* Tail donation for propagate launches that are pipelined with others (several batches in
  * flight on different streams): once a launch's work queue is drained, a wave with at most
  * `lanes` live rays (all between steps) hands them to a continuation launch on the same
@@ -211,6 +217,23 @@ int art_propagate_host_flux(const art_params* p, int64_t n, const double* x0, co
                             const double* erg, const double* dw, const double* ln_t0,
                             const int8_t* species, int32_t max_crossings, art_segment_out* out,
                             art_crossing_buf* xc, int32_t nbins, double* hist);
+/* art_propagate_host_flux, asynchronous: checks the arguments, returns at once with *ticket, and
+ * runs the call on a library worker thread; art_host_wait(ticket) returns the call's result code.
+ * Two calls per device can be in flight (a third waits for the lane of the one two before it),
+ * each with its own streams and staging, so the next batch's uploads and first rays overlap this
+ * batch's drain (MainRunner.jl:179-190 calls RT.propagate batch after batch; a host that has the
+ * next batch ready submits it before waiting for this one). Every buffer of a call must stay
+ * valid and untouched until its art_host_wait returns; wait on the device the call was submitted
+ * on. A batch the streamed pipeline does not take (below ART_HOST_CHUNK_MIN rays, default 2^20)
+ * runs inside the submitting call and its ticket is complete. Synchronous host calls first wait
+ * for every asynchronous one. Results equal art_propagate_host_flux's bit for bit. */
+int art_propagate_host_flux_async(const art_params* p, int64_t n, const double* x0, const double* k0,
+                                  const double* erg, const double* dw, const double* ln_t0,
+                                  const int8_t* species, int32_t max_crossings, art_segment_out* out,
+                                  art_crossing_buf* xc, int32_t nbins, double* hist, int64_t* ticket);
+/* Waits for an asynchronous host call and returns its result (ART_OK or the ART_E* code it
+ * failed with; art_last_error() then says why). Each ticket is waited for once. */
+int art_host_wait(int64_t ticket);
 /* What the art_propagate_host* calls of this process ran as, since load or the last reset:
  * [0] calls, [1] streamed-pipeline completions, [2] streamed-pipeline give-ups (a wait
  * outlasted its bound; the batch then ran again as one launch, same results), [3] chunked-

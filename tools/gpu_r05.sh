@@ -1,0 +1,66 @@
+#!/bin/bash
+# Round-5 GPU session steps. Usage: TAG=r05a bash tools/gpu_r05.sh STEP [STEP ...]
+# Every GPU step runs under its own time limit; the first failure ends the session.
+TAG=${TAG:-r05}
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
+mkdir -p gpurun_out
+O=gpurun_out/${TAG}
+say() { echo "[$(date +%T)] $*"; }
+run_step() {
+  case "$1" in
+    pytest)  # the whole GPU suite
+      timeout -k 10 900 python3 -u -m pytest tests -m gpu -v --timeout 600 --timeout-method thread > ${O}_pytest_gpu.log 2>&1 ;;
+    pytest_rehearsal)
+      timeout -k 10 400 python3 -u -m pytest tests/test_gpu_configs2_full.py -m gpu -v -k rehearsal --timeout 300 --timeout-method thread > ${O}_pytest_rehearsal.log 2>&1 ;;
+    pytest_edges)
+      timeout -k 10 400 python3 -u -m pytest tests/test_edges.py -m gpu -v --timeout 300 --timeout-method thread > ${O}_pytest_edges.log 2>&1 ;;
+    smoke)
+      timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > ${O}_smoke.log 2>&1 ;;
+    bench)  # the default bench line (host path, 1e7 flat)
+      timeout -k 10 600 python3 -u bench.py > ${O}_bench_flat1e7.json 2> ${O}_bench.err ;;
+    bench_nocpu)
+      timeout -k 10 600 python3 -u bench.py --no-cpu-baseline --steps 10 --warmup 2 > ${O}_bench_flat1e7_nocpu.json 2> ${O}_bench_nocpu.err ;;
+    rocprof)  # kernel trace of the bench command (no counters)
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats -d ${O}_prof -o prof --output-format csv -- python3 bench.py --steps 5 --no-cpu-baseline > ${O}_bench_prof.json 2> ${O}_prof.err ;;
+    rocprof_copies)  # the same with the memory-copy trace: are the pipeline's copies DMA or blit kernels?
+      timeout -k 10 600 rocprofv3 --kernel-trace --memory-copy-trace --stats -d ${O}_profmc -o prof --output-format csv -- python3 bench.py --steps 5 --no-cpu-baseline --no-device > ${O}_bench_profmc.json 2> ${O}_profmc.err ;;
+    shard)  # the 8-GPU shard size on one GPU, with the host pipeline's trace
+      ART_HOST_TRACE=1 timeout -k 10 300 python3 -u bench.py --rays 1250000 --steps 10 --warmup 2 --no-cpu-baseline > ${O}_bench_1250000.json 2> ${O}_shard_trace.err ;;
+    shard1)  # the same, one host call at a time
+      timeout -k 10 300 python3 -u bench.py --rays 1250000 --steps 10 --warmup 2 --no-cpu-baseline --inflight 1 > ${O}_bench_1250000_if1.json 2> ${O}_shard1.err ;;
+    bench_if2)  # the 1e7 headline workload with two host calls in flight
+      timeout -k 10 600 python3 -u bench.py --no-cpu-baseline --steps 10 --warmup 2 --inflight 2 --no-device > ${O}_bench_flat1e7_if2.json 2> ${O}_bench_if2.err ;;
+    ab_pf)  # the slot-row prefetch variant against this build, interleaved
+      ROUNDS=3 bash tools/ab_kernel.sh ${O}_ab_prefetch.jsonl base tools/build/libart_pf.so ;;
+    gr)
+      timeout -k 10 600 python3 -u bench.py --config gr --rays 1000000 --steps 5 --no-cpu-baseline > ${O}_bench_gr1e6.json 2> ${O}_gr.err ;;
+    tail)  # ray 717277 alone on the tail kernel
+      TAIL_DONATE=4 timeout -k 10 300 python3 -u tools/exp_gr_tail.py 1000000 717277 > ${O}_gr_tail.jsonl 2> ${O}_gr_tail.err ;;
+    grsmall)  # GR batches between 1024 and ncu x 256 rays, donation 16 vs 0
+      timeout -k 10 300 python3 -u tools/exp_gr_donate_small.py 4096,16384,65536 > ${O}_gr_donate_small.jsonl 2> ${O}_grsmall.err ;;
+    w1)  # occupancy sensitivity: the 1-wave/SIMD integrator on the 1e7 device-resident batch
+      ART_LIB=tools/build/libart_w1.so timeout -k 10 300 python3 -u tools/exp_sections.py > ${O}_w1_device.jsonl 2> ${O}_w1.err &&
+      timeout -k 10 300 python3 -u tools/exp_sections.py > ${O}_w2_device.jsonl 2>> ${O}_w1.err ;;
+    tcc)  # L2 hit/miss of both integrator builds (the fetch question), and FETCH_SIZE twice
+      for i in 1 2; do
+        ART_HOST_STREAM_SERIAL=1 timeout -s KILL 300 rocprofv3 --kernel-trace --pmc TCC_HIT_sum TCC_MISS_sum -d ${O}_tcc/hit$i -o p \
+          --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline > ${O}_tcc_hit$i.log 2>&1 || return 1
+        ART_HOST_STREAM_SERIAL=1 timeout -s KILL 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d ${O}_tcc/fetch$i -o p \
+          --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline > ${O}_tcc_fetch$i.log 2>&1 || return 1
+      done ;;
+    pmc_gr)  # configs[3]: bulk, continuation and tail kernels of one batch, and ray 717277 alone
+      bash tools/pmc_gr.sh ${O}_pmc_gr > ${O}_pmc_gr.log 2>&1 ;;
+    pmc)  # the full PMC set of this build (bench.py's roofline.traffic)
+      bash tools/pmc_passes.sh ${O}_pmc 10000000 > ${O}_pmc.log 2>&1 ;;
+    *) echo "unknown step $1"; return 2 ;;
+  esac
+}
+for s in "$@"; do
+  say "$s"
+  run_step "$s"
+  rc=$?
+  say "$s rc=$rc"
+  if [ "${s#pytest}" != "$s" ]; then [ $rc -le 1 ] || exit $rc; else [ $rc -eq 0 ] || exit $rc; fi
+done
+say done
