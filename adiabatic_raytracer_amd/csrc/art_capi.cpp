@@ -97,6 +97,7 @@ struct DeviceCtx {
   int next = 0, last = -1;       // next ring slot; the most recent propagate launch
   int64_t launches = 0;          // propagate launches issued so far
   int32_t donate = -1;           // tail donation (art_set_tail_donation): lanes per wave, 0 = off, -1 = by geometry
+  int32_t graduate = -1;         // graduation (art_set_graduation): attempts, 0 = off, -1 = the default (2048)
   std::vector<std::pair<void*, size_t>> pool;  // host-entry staging buffers (grow-only, used under g_mu by the
                                                // synchronous *_host calls only)
   // the chunked host pipeline of art_propagate_host (propagate_host_chunked): its compute
@@ -190,22 +191,6 @@ int take_slot(DeviceCtx* c, LaunchRec** out) {
   }
   *out = &L;
   return ART_OK;
-}
-
-// Whether a propagate launch of this context on a stream other than s is still running. With
-// other passes in flight, graduation only costs: a graduated ray holds a whole wave of the tail
-// kernel instead of one lane, and the other passes already fill the CUs its wave would free
-// (profiles/r04al_graduation_in_flight.txt: 16 GR passes in flight 4.9e8 with, 7.7e8 without).
-bool others_in_flight(DeviceCtx* c, hipStream_t s) {
-  for (LaunchRec& L : c->ring) {
-    if (!L.pending || L.stream == s) continue;
-    if (hipEventQuery(L.done) == hipErrorNotReady) {
-      // not an error: keep it out of the thread's last error, which the launches check
-      if (hipPeekAtLastError() == hipErrorNotReady) (void)hipGetLastError();
-      return true;
-    }
-  }
-  return false;
 }
 
 int pool_get_v(PoolVec& pool, size_t slot, size_t bytes, void** p) {
@@ -592,8 +577,11 @@ int propagate_device_impl(const art_params* p, int64_t n, const double* x0, cons
       so.grad_count = words + 20;
       so.grad_queue = words + 21;
       so.grad_cap = (int32_t)std::min(ncont, (size_t)INT32_MAX);
-      // (off while another pass of this context runs on another stream: others_in_flight)
-      so.graduate = others_in_flight(c, s) ? 0 : std::max(0, env_int("ART_GRADUATE", 2048));
+      // (the caller's setting, art_set_graduation: a host that keeps several passes in flight turns
+      // it off -- each graduated ray then holds a whole tail wave while the other passes fill the
+      // CUs it would free, profiles/r04al_graduation_in_flight.txt; round 4 decided this per launch
+      // from the other streams' events, which made it depend on host timing)
+      so.graduate = c->graduate >= 0 ? c->graduate : std::max(0, env_int("ART_GRADUATE", 2048));
     }
     so.donate = donate;
     so.small_tail = small_tail ? 1 : 0;
@@ -677,6 +665,16 @@ int art_set_tail_donation(int32_t lanes) {
   int rc = current_ctx(&c);
   if (rc) return rc;
   c->donate = lanes;
+  return ART_OK;
+}
+
+int art_set_graduation(int32_t attempts) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (attempts < -1) return fail(ART_E_INVALID, "graduation attempts must be >= -1");
+  DeviceCtx* c;
+  int rc = current_ctx(&c);
+  if (rc) return rc;
+  c->graduate = attempts;
   return ART_OK;
 }
 

@@ -85,6 +85,12 @@ class Engine:
         library's default by geometry (16 for Schwarzschild batches, else 0)."""
         check(self.lib.art_set_tail_donation(int(lanes)))
 
+    def set_graduation(self, attempts: int) -> None:
+        """Graduation of a launch's outlier rays to the one-wave-per-ray tail kernel
+        (art_set_graduation, include/art.h): 0 = off (several batches in flight), -1 = the
+        default (2048 attempts). Bit-identical results."""
+        check(self.lib.art_set_graduation(int(attempts)))
+
     def kernel_ms(self) -> float:
         """Duration of the last propagate kernel (HIP events on its stream); synchronizes."""
         check(self.lib.art_synchronize())

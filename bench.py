@@ -284,6 +284,7 @@ def main():
 
         def device_run(nstreams, donate_lanes, steps, warmup):
             eng.set_tail_donation(donate_lanes)
+            eng.set_graduation(0 if nstreams > 1 else -1)  # (batches in flight: off, include/art.h)
             streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(nstreams - 1)]
             outs = [eng.alloc_out(n, capacity=1) for _ in streams]
             hists = [torch.zeros(2 * args.nbins, dtype=torch.float64, device=eng.device) for _ in streams]
@@ -307,6 +308,7 @@ def main():
             assert int(outs[k_last]["n_accept"].sum().item()) == st["accepted"]
             tot, tmax, _ = reduce_totals(st["accepted"] * steps, el, n, world, device=eng.device)
             eng.set_tail_donation(-1)
+            eng.set_graduation(-1)
             return {"value": tot / tmax, "ms_per_step": tmax / steps * 1e3, "kernel_ms": float(np.mean(list(kb)[:g])),
                     "kernel_span_ms": float(np.mean(span)) if span else None,
                     "streams": nstreams, "tail_donation": donate_lanes, "elapsed_s": el, "stats": st,

@@ -174,6 +174,14 @@ int art_recent_kernel_span_ms(int32_t n, double* ms);
  * the current device's subsequent launches (the streamed host pipeline never donates). No
  * reference counterpart (an execution policy). */
 int art_set_tail_donation(int32_t lanes);
+/* Graduation for Vern6 launches with tail donation (the Schwarzschild default): a ray still
+ * stepping after `attempts` step attempts leaves its lane at its next step boundary for the
+ * one-wave-per-ray tail kernel, so a batch's longest rays run at lone-wave speed without waiting
+ * for their waves to drain (configs[3] as one batch: 260-297 -> 230 ms). 0 switches it off -- for
+ * a host that keeps several batches in flight, where each graduated ray would hold a whole tail
+ * wave while the other batches fill the CUs it frees; -1 (the default) = 2048 attempts (or
+ * ART_GRADUATE). Per device; results are bit-identical either way. */
+int art_set_graduation(int32_t attempts);
 /* The Vern6 tableau the kernel uses: c[9], A[81] row-major, b[9], bhat[9]. */
 int art_vern6_tableau(double* c, double* A, double* b, double* bhat);
 
