@@ -1110,7 +1110,8 @@ int propagate_host_maskless(DeviceCtx* c, HostLane* H, bool overlap, const art_p
   auto xd_off = [&](int64_t m) { return cnt_off(m) + up((size_t)m * sizeof(int32_t)); };
   auto out_bytes = [&](int64_t m) { return cap ? xd_off(m) + (size_t)cap * m * 9 * sizeof(double) : cnt_off(m); };
   const size_t stride = up(out_bytes((int64_t)1 << shift));
-  // scratch: head [queue | stats (10) | init_next (16) fin_next (17) chunk misses (18) exit count (19) waves done (20) |
+  // scratch: head [queue | stats (10) | init_next (16) fin_next (17) chunk misses (18) exit count (19) waves done (20)
+  // waves started (21) |
   // finished rays per piece from word 32 | finalized tiles per piece from word 96] | chunk flags | u0 16n | rec 16n | xrec
   const size_t nchunk = (nd + art::CHUNK - 1) / art::CHUNK;
   const size_t head = 2048, ccb = up(nchunk * sizeof(unsigned)), u0b = nd * 16 * sizeof(double),
@@ -1192,6 +1193,7 @@ int propagate_host_maskless(DeviceCtx* c, HostLane* H, bool overlap, const art_p
   so.done_host = H->hsig_dev + HSIG_DONE;
   so.exit_count = words + 19;
   so.waves_done = words + 20;
+  so.waves_started = words + 21;
   int ncu = 0;
   HIP_OK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device));
   const int slots = std::max(2, env_int("ART_HOST_BLOCKS", 2 * ncu));  // block slots: 2 per CU
@@ -1208,9 +1210,7 @@ int propagate_host_maskless(DeviceCtx* c, HostLane* H, bool overlap, const art_p
   // hold those slots, and the helpers finalize alone
   const bool final_pass = serial || !overlap;
   const int iblocks = serial ? slots : slots - helpers;
-  const int igrid = (int)std::min((n + 255) / 256, (int64_t)iblocks);  // launch_integrator_streamed's grid
   so.exit_expected = (serial ? 0 : helpers) + (final_pass ? slots : 0);
-  so.waves_expected = igrid * 4;
   hipEvent_t ev_zero = H->pev[nu + np];  // (the helpers start on zeroed counters)
   HIP_OK(hipEventRecord(ev_zero, H->m_comp));
   HIP_OK(hipStreamWaitEvent(H->m_help, ev_zero, 0));
@@ -1856,8 +1856,18 @@ int sample_device_impl(const art_params* p, double max_r, uint64_t seed, int64_t
   void* q = nullptr;  // this launch's work-queue word
   if ((rc = scratch_alloc(s, 256, &q))) return rc;
   HIP_OK(hipMemsetAsync(q, 0, sizeof(unsigned long long), s));
+  HIP_OK(hipMemsetAsync(q, 0, 256, s));
   HIP_OK(art::launch_sample(kparams(*p), max_r, seed, ray_offset, n, x, k_init, erg_inf, vifty, weights,
                             attempts, (unsigned long long*)q, s));
+#ifdef ART_SAMPLER_SECTIONS  // (dev build: the sampler's section cycles to stderr)
+  {
+    unsigned long long w[16];
+    HIP_OK(hipMemcpyAsync(w, q, sizeof w, hipMemcpyDeviceToHost, s));
+    HIP_OK(hipStreamSynchronize(s));
+    std::fprintf(stderr, "[sampler-sections] n=%lld setup %llu control %llu cert %llu grid %llu brackets %llu out %llu "
+                 "grid_steps %llu steps %llu\n", (long long)n, w[8], w[9], w[10], w[11], w[12], w[13], w[14], w[15]);
+  }
+#endif
   HIP_OK(hipFreeAsync(q, s));
   return ART_OK;
 }

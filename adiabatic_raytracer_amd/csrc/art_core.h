@@ -522,10 +522,22 @@ __host__ __device__ inline T psi_of(const KParams& P, const T& phi, const T& t) 
   return phi - P.omega * t;
 }
 
+// A branch condition the caller knows to be wave-uniform (UNI: the one-wave-per-ray tail kernel,
+// whose lanes hold the ray alike): a scalar branch on lane 0's value instead of an exec-mask
+// branch; elsewhere the condition itself. The values either way are the same.
+template <bool UNI>
+__host__ __device__ inline bool uni_if(bool c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  if constexpr (UNI) return __builtin_amdgcn_readfirstlane((int)c) != 0;
+#endif
+  return c;
+}
+
 // rhs_photon_gj from its transcendental inputs: t = e^τ, (sin, cos) of θ = u[1] and of ψ = psi_of(u[2], t).
 // The one-ray-per-wave tail kernel evaluates the two sincos on two lanes at once and every
-// stage's e^τ ahead of the stage; the values and the arithmetic here are the same.
-template <class T>
+// stage's e^τ ahead of the stage (and takes its branches as wave-uniform, UNI); the values and
+// the arithmetic here are the same.
+template <class T, bool UNI = false>
 __host__ __device__ inline void rhs_photon_gj_tr(const KParams& P, const T* u, const T& t, const T& st, const T& ct,
                                                  const T& sp, const T& cp, double erg, T* du, T* aux = nullptr);
 
@@ -540,7 +552,7 @@ __host__ __device__ inline void rhs_photon_gj(const KParams& P, const T* u, cons
   rhs_photon_gj_tr(P, u, t, st, ct, sp, cp, erg, du, aux);
 }
 
-template <class T>
+template <class T, bool UNI>
 __host__ __device__ inline void rhs_photon_gj_tr(const KParams& P, const T* u, const T& t, const T& st, const T& ct,
                                                  const T& sp, const T& cp, double erg, T* du, T* aux) {
   ART_FP_FAST
@@ -563,7 +575,7 @@ __host__ __device__ inline void rhs_photon_gj_tr(const KParams& P, const T* u, c
   // the prefactor (:82), which differs only inside the star
   T grr = 1.0, dgtt = 0.0, dgrr = 0.0, grr_u = 1.0, sq = 1.0, isq = 1.0;
   if (!flat) {
-    if (rc <= 10.0) {  // g_schwartz's interior patch (a radius clamped to rNS <= 10 km)
+    if (uni_if<UNI>(rc <= 10.0)) {  // g_schwartz's interior patch (a radius clamped to rNS <= 10 km)
       T gtt;
       metric_tr_d(rc, P.rs_eff, gtt, grr, dgtt, dgrr);
       sq = msqrt(grr);
@@ -577,7 +589,7 @@ __host__ __device__ inline void rhs_photon_gj_tr(const KParams& P, const T* u, c
       isq = sq * ig;  // 1/√g^rr = √g^rr / g^rr
     }
     grr_u = grr;
-    if (r < P.rNS) {
+    if (uni_if<UNI>(r < P.rNS)) {
       T gtt_u;
       metric_tr(r, P.rs_eff, gtt_u, grr_u);
     }

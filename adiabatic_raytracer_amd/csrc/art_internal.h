@@ -86,15 +86,17 @@ struct SegOut {
   // The end of a streamed call without the integrator's stream (art_capi.cpp, HostLane): the
   // helpers bin the radiated flux of the rays they finalize (flux_hist, 2 flux_nbins doubles of
   // device memory, flux_nbins <= FLUX_HELPER_BINS; 0 = none), every integrator wave counts itself
-  // into *waves_done after its statistics, and the last of the exit_expected serving helper blocks
-  // to leave (*exit_count) waits for waves_expected of them, then copies the statistics
-  // (stats[0, N_STATS_DEV)) and the flux into host memory (done_host[DONE_STATS...], [DONE_FLUX...])
-  // and raises done_host[0]. The host then has the call's results without waiting on a stream.
+  // into *waves_started as it starts and into *waves_done after its statistics, and the last of the
+  // exit_expected serving helper blocks to leave (*exit_count) -- every ray is done by then -- waits
+  // until every started wave is done (blocks the next call's kernels kept from starting find the
+  // queue drained and add nothing), then copies the statistics (stats[0, N_STATS_DEV)) and the flux
+  // into host memory (done_host[DONE_STATS...], [DONE_FLUX...]) and raises done_host[0]. The host
+  // then has the call's results without waiting on a stream.
   double* flux_hist;
   int32_t flux_nbins;
   unsigned long long* done_host;
-  unsigned long long *exit_count, *waves_done;
-  int32_t exit_expected, waves_expected;
+  unsigned long long *exit_count, *waves_started, *waves_done;
+  int32_t exit_expected;
   // Small batches (art_capi.cpp, propagate_device_impl): 1 = every fresh ray goes straight to
   // tail_kernel, one wave per ray (pack_fresh_kernel writes their CONT_REC records to cont),
   // instead of one lane per ray of the persistent integrator

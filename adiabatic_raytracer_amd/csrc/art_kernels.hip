@@ -715,7 +715,11 @@ __global__ __launch_bounds__(BLOCK, WPS) void propagate_kernel(const KParams P_i
   const double tend = P.ln_t_end;
   const int npts = P.interp_points;
   for (int j = threadIdx.x; j < npts; j += BLOCK) thgrid[j] = double(j) / double(npts - 1);
-  if constexpr (DON == 3) pend_lds[threadIdx.x >> 6][threadIdx.x & 63] = 0u;
+  if constexpr (DON == 3) {
+    pend_lds[threadIdx.x >> 6][threadIdx.x & 63] = 0u;
+    if (out.waves_started && (threadIdx.x & 63) == 0)
+      __hip_atomic_fetch_add(out.waves_started, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
   span_stamp(stats, false);
   __syncthreads();
 
@@ -1754,7 +1758,11 @@ __device__ inline void tail_rhs(const KParams& P, int lane, const double* y, dou
     double sn, cs;
     msincos(arg, sn, cs);
     const double st = rdlane(sn, 0), ct = rdlane(cs, 0), sp = rdlane(sn, 1), cp = rdlane(cs, 1);
+#ifdef ART_TAIL_RHS_UNI  // (dev A/B: the RHS's own branches wave-uniform too)
+    rhs_photon_gj_tr<double, true>(P, y, t, st, ct, sp, cp, erg, kk, aux);
+#else
     rhs_photon_gj_tr(P, y, t, st, ct, sp, cp, erg, kk, aux);
+#endif
   } else {
     rhs_photon(P, y, ty, erg, kk, aux);
   }
@@ -1767,6 +1775,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
   const KParams P = specialize<GEOM>(P_in);
   using V = Vern6;
   const int lane = threadIdx.x;
+  // Every lane holds the ray's state alike, so its control decisions are wave-uniform: U() makes
+  // that visible to the compiler (a scalar branch on lane 0's value instead of an exec-mask
+  // branch with its saved masks -- SGPRs the kernel otherwise spills to VGPR lanes); the values
+  // and the arithmetic do not change
+#ifndef ART_TAIL_NO_UNI
+  auto U = [](bool c) { return __builtin_amdgcn_readfirstlane((int)c) != 0; };
+#else
+  auto U = [](bool c) { return c; };  // (dev A/B)
+#endif
   const int64_t nq = (int64_t)*out.cont_count;
   (void)max_rays;
   __builtin_amdgcn_s_setprio(3);  // the rays that set the launch's end
@@ -1829,16 +1846,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
     double hroot = 0.0, r_tha = 0.0, r_ca = 0.0, r_thb = 0.0, r_cb = 0.0, r_t = 0.0, r_slope = 1.0, post_c = 0.0;
     int post_s = 0, r_side = 0, r_it = 0;
     int finish = -1;
-    while (finish < 0) {
+    while (U(finish < 0)) {
       // ---- this attempt's step size (the bulk kernel's rules) ----
       bool last = false, forced = false;
       double hs;
-      if (mode == M_ROOT) {
+      if (U(mode == M_ROOT)) {
         hs = r_t * hroot;
       } else {
         hs = dt;
-        if (tau + hs >= tend) { hs = tend - tau; last = true; }
-        else if (hs < P.dtmin) { hs = P.dtmin; forced = true; }
+        if (U(tau + hs >= tend)) { hs = tend - tau; last = true; }
+        else if (U(hs < P.dtmin)) { hs = P.dtmin; forced = true; }
       }
       // ---- e^τ of the eight stages at once (lane s: stage s) ----
       const double tl = fexp(tau + my_ct * hs);
@@ -1853,7 +1870,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
         const double ty = tau + ct * hs;
         const double t = rdlane(tl, s);
         tail_rhs<GEOM>(P, lane, y, ty, t, erg, kk, aux);
-        if (!photon) {
+        if (U(!photon)) {
           double ka[7];
           rhs_axion(P, y, ty, erg, ka);
 #pragma unroll
@@ -1960,17 +1977,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
       // ---- controller (STEP) ----
       bool scan = false;
       double dtnext = dt;
-      if (mode == M_STEP) {
+      if (U(mode == M_STEP)) {
         s_att += 1;
         ++iter;
         bool finite = !isnan(EEst2) && !isinf(EEst2);
 #pragma unroll
         for (int i = 0; i < 7; ++i) finite = finite && !isnan(y[i]) && !isinf(y[i]);
-        if (!finite) {
+        if (U(!finite)) {
           finish = ART_STATUS_NONFINITE;
         } else {
           double q = 1.0, q11 = 1.0, y60 = 0.0;
-          if (EEst2 == 0.0) {
+          if (U(EEst2 == 0.0)) {
             q = 0.1;
           } else {
             y60 = fexp(flog(EEst2) * (1.0 / 120.0));
@@ -1979,7 +1996,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
             q = q11 * frcp(qpow);
             q = fmax(0.1, fmin(5.0, q * (1.0 / 0.9)));
           }
-          const bool accept = (EEst2 <= 1.0) || forced;
+          const bool accept = U((EEst2 <= 1.0) || forced);
           if (!accept) {
             dt = hs * frcp(fmin(5.0, q11 * (1.0 / 0.9)));
             ++n_rej;
@@ -1994,12 +2011,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
           }
         }
       }
-      if (finish >= 0) break;
+      if (U(finish >= 0)) break;
       // ---- resonance scan of an accepted step: certificate, else the 49 grid points at once ----
       const int ccode = !scan ? 0 : (cbs ? scan_certified_code(P, u, f, y, kk, hs, bend, tlast, bstart) : 3);
-      const bool cert = ccode != 0;
+      const bool cert = U(ccode != 0);
       s_cert += cert ? 1u : 0u;
-      const bool grid = scan && !cert;
+      const bool grid = U(scan && !cert);
       double gN = 0.0, gD = 1.0;  // lane l: N, D at grid point l + 1
       unsigned cw[SCAN_WORDS] = {0u, 0u, 0u, 0u};
       double lastv = 0.0;  // value at the last grid point
@@ -2018,7 +2035,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
         for (int w = 0; w < SCAN_WORDS; ++w) cw[w] = 0x55555555u * (unsigned)ccode;
       }
       auto gval = [&](int j) {  // the condition at grid point j of this step (from the grid pass when it ran)
-        if (grid && j >= 1) return 0.5 * rdlane(gN, j - 1) / rdlane(gD, j - 1);
+        if (U(grid && j >= 1)) return 0.5 * rdlane(gN, j - 1) / rdlane(gD, j - 1);
         s_interp += 1;
         return scan_point_regs(P, u, f, y, kk, hs, tau, double(j) / double(npts - 1));
       };
@@ -2028,9 +2045,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
       int last_s = sprev;
       double last_c = cprev;
       bool lc_ok = cprev_ok;
-      if (ph == 2) {
+      if (U(ph == 2)) {
         const unsigned s0 = cw[0] & 3u;
-        if (s0 == 1u || s0 == 2u) {
+        if (U(s0 == 1u || s0 == 2u)) {
           bool same = (last_s == 0) || (last_s == (s0 == 1u ? 1 : -1));
 #pragma unroll
           for (int w = 0; w < SCAN_WORDS; ++w) {
@@ -2039,14 +2056,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
             const unsigned m = nw >= 16 ? 0xffffffffu : ((1u << (2 * nw)) - 1u);
             same = same && ((cw[w] & m) == ((s0 * 0x55555555u) & m));
           }
-          if (same) {
+          if (U(same)) {
             last_s = (s0 == 1u) ? 1 : -1;
             last_j = nper;
             if (!cert) last_c = lastv;
             lc_ok = !cert;
             ph = 0;
           }
-        } else if (s0 == 3u) {
+        } else if (U(s0 == 3u)) {
           bool all = true;
 #pragma unroll
           for (int w = 0; w < SCAN_WORDS; ++w) {
@@ -2055,7 +2072,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
             const unsigned m = nw >= 16 ? 0xffffffffu : ((1u << (2 * nw)) - 1u);
             all = all && ((cw[w] & m) == m);
           }
-          if (all) {
+          if (U(all)) {
             last_s = 0;
             lc_ok = false;
             ph = 0;
@@ -2094,7 +2111,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
         i_tr = i_tha - i_ca * (i_thb - i_tha) / (i_cb - i_ca);
         i_side = 0;
         i_it = 0;
-        if (just_evented && i_tha < 0.01) {
+        if (U(just_evented && i_tha < 0.01)) {
           ph = 3;
         } else {
           open_root(i_tr);
@@ -2109,9 +2126,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
         last_s = ws.last_s;
         last_j = ws.last_j;
         lc_ok = ws.lc_ok;
-        if (found) {
+        if (U(found)) {
           ph = 5;
-        } else if (!lc_ok && last_j == nper) {
+        } else if (U(!lc_ok && last_j == nper)) {
           if (!cert) {
             last_c = lastv;
             lc_ok = true;
@@ -2139,22 +2156,22 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
         root_done = done;
         ph = 0;
       };
-      if (mode == M_ROOT) {  // the re-stepped end's value (th = 1 of this step)
+      if (U(mode == M_ROOT)) {  // the re-stepped end's value (th = 1 of this step)
         s_root += 1;
         polish(scan_point_regs(P, u, f, y, kk, hs, tau, 1.0));
       }
-      if (ph == 2) walk();
+      if (U(ph == 2)) walk();
 #pragma unroll 1
-      while (ph != 0) {
-        if (ph == 2) {
+      while (U(ph != 0)) {
+        if (U(ph == 2)) {
           walk();
-          if (ph == 0) break;
+          if (U(ph == 0)) break;
         }
-        if (ph == 5) {  // the values at the change point and, when unknown, at the bracket start
+        if (U(ph == 5)) {  // the values at the change point and, when unknown, at the bracket start
           i_cg = gval(ip);
-          if (!lc_ok) last_c = gval(last_j);
+          if (U(!lc_ok)) last_c = gval(last_j);
           open_bracket();
-        } else if (ph == 7) {
+        } else if (U(ph == 7)) {
           last_c = gval(last_j);
           lc_ok = true;
           ph = 0;
@@ -2176,9 +2193,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
               if (++i_it >= 40) stop = true;
             }
           }
-          if (stop) {
+          if (U(stop)) {
             const double t_int = i_tr;
-            if (!below && !(just_evented && t_int < 0.01)) {
+            if (U(!below && !(just_evented && t_int < 0.01))) {
               open_root(t_int);
               ph = 0;
             } else {
@@ -2193,7 +2210,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
         }
       }
       // ---- the state the ray continues from (the bulk kernel's reload and event logic) ----
-      if (root_done || (scan && !hit)) {
+      if (U(root_done || (scan && !hit))) {
 #pragma unroll
         for (int i = 0; i < 7; ++i) {
           u[i] = y[i];
@@ -2201,8 +2218,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
         }
         bstart = bend;
       }
-      if (hit) mode = M_ROOT;
-      if (root_done) {
+      if (U(hit)) mode = M_ROOT;
+      if (U(root_done)) {
         const double tau_r = tau + hs;
         int a = 0;
         {  // affect! (RayTracer.jl:301-350) as the bulk kernel's affect(), stored by lane 0
@@ -2250,7 +2267,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
         else if (photon && u[0] < P.rNS101) finish = ART_STATUS_HIT_NS;
         else if (iter >= P.maxiters) finish = ART_STATUS_MAXITERS;
       }
-      if (scan && !hit) {
+      if (U(scan && !hit)) {
         tau = last ? tend : tau + hs;
         cprev = last_c;
         cprev_ok = lc_ok;
@@ -2520,10 +2537,11 @@ __global__ __launch_bounds__(256) void helper_kernel(const KParams P, const int6
     }
     __syncthreads();
     if (last_out) {
-      if (tid == 0) {  // the integrator's waves have added their statistics (they count themselves after)
+      if (tid == 0) {  // the integrator's started waves have added their statistics (they count themselves after)
         const unsigned long long w0 = __builtin_amdgcn_s_memrealtime();
         bool ok = true;
-        while (ld_agent(out.waves_done) < (unsigned long long)out.waves_expected) {
+        const unsigned long long started = ld_agent(out.waves_started);
+        while (ld_agent(out.waves_done) < started) {
           if (ld_abort(out) || __builtin_amdgcn_s_memrealtime() - w0 > STREAM_WAIT_TICKS) { ok = false; break; }
           __builtin_amdgcn_s_sleep(8);
         }
@@ -2615,6 +2633,21 @@ __global__ __launch_bounds__(256, WPS) void sample_kernel(const KParams P, const
   const unsigned long long lt = (1ull << lane) - 1ull;
   if (threadIdx.x < np) sgrid[threadIdx.x] = 0.5 * double(threadIdx.x) / double(np - 1);
   __syncthreads();
+#ifdef ART_SAMPLER_SECTIONS
+  // dev build: s_memtime cycles per section, summed over the wave's iterations, into queue[8..15]
+  // [refill + line set-up, step loop control + window, certificate, grid pass, brackets + flush,
+  //  sample out]; queue[14] wave-steps with a grid pass, queue[15] wave-steps run
+  unsigned long long q_sec[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long q_last = __builtin_amdgcn_s_memtime();
+#define ART_QMARK(k)                                                \
+  {                                                                 \
+    const unsigned long long q_now_ = __builtin_amdgcn_s_memtime(); \
+    q_sec[k] += q_now_ - q_last;                                    \
+    q_last = q_now_;                                                \
+  }
+#else
+#define ART_QMARK(k)
+#endif
   while (true) {
     if (!exhausted) {
       unsigned long long need = __ballot(ray < 0);
@@ -2755,7 +2788,11 @@ __global__ __launch_bounds__(256, WPS) void sample_kernel(const KParams P, const
       wave_lds_sync();
     };
 
+    ART_QMARK(0)
     for (int st = 0; st < nsteps; ++st) {
+#ifdef ART_SAMPLER_SECTIONS
+      q_sec[7] += 1;
+#endif
       const double s0 = st * 0.5;
       const double s1 = fmin(s0 + 0.5, send);
       const bool quiet = !active || (cert_ok && c_prev < 0.0 && (s1 < w_in || s0 > w_out));
@@ -2791,6 +2828,7 @@ __global__ __launch_bounds__(256, WPS) void sample_kernel(const KParams P, const
       //    (r > 10 km), g^rr g^tt = -1, so Cauchy-Schwarz on k∥ with w on the axion shell gives
       //    1 - g^rr k∥²/E² >= g^rr m_a²/E² and the condition >= ½ m_a² (ωp² g^rr/E² - 1)/E² > 0
       //    when wp2n |b|min g^rr(r_min) > E² r_max³ (r_max: at an end of the step).
+      ART_QMARK(1)
       bool cert = active && quiet;
       if (active && !quiet && cert_ok && c_prev != 0.0 && !isnan(c_prev)) {
         const double X0[3] = {Lx[0], Lx[256], Lx[2 * 256]}, VA[3] = {Lx[3 * 256], Lx[4 * 256], Lx[5 * 256]};
@@ -2821,7 +2859,11 @@ __global__ __launch_bounds__(256, WPS) void sample_kernel(const KParams P, const
       const bool unc = active && !cert;
       const unsigned long long mU = __ballot(unc);
       const int nU = __popcll(mU);
+      ART_QMARK(2)
       if (nU == 0) continue;  // all certified: no point, no bracket, c_prev unchanged
+#ifdef ART_SAMPLER_SECTIONS
+      q_sec[6] += 1;
+#endif
       const int uix = __popcll(mU & lt);  // this lane's rank among the uncertified ones
       if (unc) ssrc[wb + uix] = (unsigned char)lane;
       // bit j: signbit / nonzero-ness of point j (bit 0: the step start)
@@ -2882,6 +2924,7 @@ __global__ __launch_bounds__(256, WPS) void sample_kernel(const KParams P, const
         br = (sb ^ (sb << 1)) & nz & (nz << 1) & (((1u << np) - 1u) & ~1u);
         c_prev = slast[threadIdx.x];
       }
+      ART_QMARK(3)
       // the previous step's last grid point, where a bracket at point 1 opens
       const double ps0 = (st - 1) * 0.5;
       const double pds = fmin(ps0 + 0.5, send) - ps0;
@@ -2901,8 +2944,10 @@ __global__ __launch_bounds__(256, WPS) void sample_kernel(const KParams P, const
         qn += __popcll(bm);
         bm = __ballot(br != 0u);
       }
+      ART_QMARK(4)
     }
     if (qn > 0) flush();
+    ART_QMARK(4)
 
     if (active) {
       const bool give_up = attempt + 1 >= 1000000u;  // bounded: no conversion surface reachable
@@ -2935,7 +2980,12 @@ __global__ __launch_bounds__(256, WPS) void sample_kernel(const KParams P, const
         ++attempt;
       }
     }
+    ART_QMARK(5)
   }
+#ifdef ART_SAMPLER_SECTIONS
+  if ((threadIdx.x & 63) == 0)
+    for (int k = 0; k < 8; ++k) atomicAdd(queue + 8 + k, q_sec[k]);
+#endif
 }
 
 // ---------------------------------------------------------------------------

@@ -13,6 +13,8 @@ run_step() {
       timeout -k 10 900 python3 -u -m pytest tests -m gpu -v --timeout 600 --timeout-method thread > ${O}_pytest_gpu.log 2>&1 ;;
     pytest_rehearsal)
       timeout -k 10 400 python3 -u -m pytest tests/test_gpu_configs2_full.py -m gpu -v -k rehearsal --timeout 300 --timeout-method thread > ${O}_pytest_rehearsal.log 2>&1 ;;
+    pytest_host)  # the host paths: streamed, give-up, async
+      timeout -k 10 600 python3 -u -m pytest tests/test_edges.py tests/test_gpu_async_host.py -m gpu -v --timeout 300 --timeout-method thread > ${O}_pytest_host.log 2>&1 ;;
     pytest_edges)
       timeout -k 10 400 python3 -u -m pytest tests/test_edges.py -m gpu -v --timeout 300 --timeout-method thread > ${O}_pytest_edges.log 2>&1 ;;
     smoke)
@@ -31,8 +33,16 @@ run_step() {
       timeout -k 10 300 python3 -u bench.py --rays 1250000 --steps 10 --warmup 2 --no-cpu-baseline --inflight 1 > ${O}_bench_1250000_if1.json 2> ${O}_shard1.err ;;
     bench_if2)  # the 1e7 headline workload with two host calls in flight
       timeout -k 10 600 python3 -u bench.py --no-cpu-baseline --steps 10 --warmup 2 --inflight 2 --no-device > ${O}_bench_flat1e7_if2.json 2> ${O}_bench_if2.err ;;
+    ab_tail)  # tail kernel: wave-uniform branches (this build) against none and against RHS-uniform too
+      ROUNDS=3 bash tools/ab_tail.sh ${O}_ab_tail.jsonl base tools/build/libart_tnouni.so tools/build/libart_trhs.so ;;
+    pytest_tail)
+      timeout -k 10 600 python3 -u -m pytest tests/test_gpu_tail_donation.py tests/test_longest_ray.py -m gpu -v --timeout 300 --timeout-method thread > ${O}_pytest_tail.log 2>&1 ;;
     ab_pf)  # the slot-row prefetch variant against this build, interleaved
       ROUNDS=3 bash tools/ab_kernel.sh ${O}_ab_prefetch.jsonl base tools/build/libart_pf.so ;;
+    ssec)  # the sampler's section split (dev build), flat 1e7 and the scan's largest-maxR point
+      ART_LIB=tools/build/libart_ssec.so timeout -k 10 300 python3 -u tools/exp_sampler_time.py > ${O}_sampler_sections.jsonl 2> ${O}_sampler_sections.err ;;
+    sampler)
+      timeout -k 10 300 python3 -u tools/exp_sampler_time.py > ${O}_sampler_time.jsonl 2> ${O}_sampler.err ;;
     gr)
       timeout -k 10 600 python3 -u bench.py --config gr --rays 1000000 --steps 5 --no-cpu-baseline > ${O}_bench_gr1e6.json 2> ${O}_gr.err ;;
     tail)  # ray 717277 alone on the tail kernel
