@@ -1117,11 +1117,19 @@ int propagate_host_maskless(DeviceCtx* c, HostLane* H, bool overlap, const art_p
   const size_t head = 2048, ccb = up(nchunk * sizeof(unsigned)), u0b = nd * 16 * sizeof(double),
                recb = nd * art::END_REC * sizeof(double);
   const size_t xrb = (size_t)cap * nd * art::X_REC * sizeof(double);
+  // ART_HOST_DIRECT=1: the pieces' output blobs in pinned host memory (fine-grained), written by the
+  // helpers over PCIe and scattered as soon as a piece is flagged -- no download copies (which a
+  // profiler's tracing turns into blit kernels competing for CU slots)
+  const bool direct = env_int("ART_HOST_DIRECT", 0) != 0;
   void *pi, *po, *din, *dout, *dsc;
-  if ((rc = pinned_get_v(H->pinned, 0, in_bytes, &pi)) || (rc = pinned_get_v(H->pinned, 1, stride * np, &po)) ||
-      (rc = pool_get_v(H->pool, 0, in_bytes, &din)) || (rc = pool_get_v(H->pool, 1, stride * np, &dout)) ||
+  if ((rc = pinned_get_v(H->pinned, 0, in_bytes, &pi)) ||
+      (rc = pinned_get_v(H->pinned, 1, stride * np, &po,
+                         direct ? (hipHostMallocMapped | hipHostMallocCoherent) : hipHostMallocDefault)) ||
+      (rc = pool_get_v(H->pool, 0, in_bytes, &din)) ||
+      (!direct && (rc = pool_get_v(H->pool, 1, stride * np, &dout))) ||
       (rc = pool_get_v(H->pool, 2, head + ccb + u0b + recb + xrb, &dsc)))
     return rc;
+  if (direct) HIP_OK(hipHostGetDevicePointer(&dout, po, 0));
   double* pin = (double*)pi;
   double* di = (double*)din;
   unsigned long long* words = (unsigned long long*)dsc;
@@ -1187,6 +1195,7 @@ int propagate_host_maskless(DeviceCtx* c, HostLane* H, bool overlap, const art_p
   so.piece_fin = words + 96;
   so.chunk_ready = ccnt;
   so.blob = (char*)dout;
+  so.blob_host = direct ? 1 : 0;
   so.blob_stride = (int64_t)stride;
   so.flux_hist = hflux ? hist_dev : nullptr;
   so.flux_nbins = hflux ? fx.nbins : 0;
@@ -1316,7 +1325,12 @@ int propagate_host_maskless(DeviceCtx* c, HostLane* H, bool overlap, const art_p
   // downloads of the finished pieces, in order; scatters of the landed ones
   auto progress = [&]() -> int {
     int moved = 0;
-    while (dk < np && __atomic_load_n(hflag + dk, __ATOMIC_ACQUIRE) != 0ull) {
+    while (direct && dk < np && __atomic_load_n(hflag + dk, __ATOMIC_ACQUIRE) != 0ull) {
+      if (trace) std::fprintf(stderr, "[art-host] t=%.2f piece %d done\n", clk() - t_start, dk);
+      ++dk;
+      ++moved;
+    }
+    while (!direct && dk < np && __atomic_load_n(hflag + dk, __ATOMIC_ACQUIRE) != 0ull) {
       const int64_t m = piece_lo(dk + 1) - piece_lo(dk);
       if (hipMemcpyAsync((char*)po + stride * dk, (char*)dout + stride * dk, out_bytes(m), hipMemcpyDeviceToHost,
                          H->m_dn) != hipSuccess ||
@@ -1327,7 +1341,7 @@ int propagate_host_maskless(DeviceCtx* c, HostLane* H, bool overlap, const art_p
       ++moved;
     }
     while (sk < dk) {
-      const hipError_t q = hipEventQuery(ev_dn[sk]);
+      const hipError_t q = direct ? hipSuccess : hipEventQuery(ev_dn[sk]);
       if (q == hipErrorNotReady) break;
       if (q != hipSuccess) return -1;
       const double t0 = clk();

@@ -82,6 +82,7 @@ struct SegOut {
   unsigned* chunk_ready;
   char* blob;
   int64_t blob_stride;
+  int32_t blob_host;  // 1: the blobs are pinned host memory the helpers write over PCIe (no download copies)
   int32_t helpers;
   // The end of a streamed call without the integrator's stream (art_capi.cpp, HostLane): the
   // helpers bin the radiated flux of the rays they finalize (flux_hist, 2 flux_nbins doubles of

@@ -918,9 +918,10 @@ __global__ __launch_bounds__(BLOCK, WPS) void propagate_kernel(const KParams P_i
     double kA[7], y[7], kk[7];
 #pragma unroll
     for (int i = 0; i < 7; ++i) kA[i] = 0.0;  // read (times a zero coefficient) before its first store
-#ifdef ART_SLOT_PREFETCH
-    // (dev A/B) the next slot's row of scalars loaded before this slot's RHS, so its scalar-load
-    // latency hides behind the RHS instead of opening the next slot
+#ifndef ART_NO_SLOT_PREFETCH
+    // the next slot's row of scalars is loaded before this slot's RHS, so its scalar-load latency
+    // hides behind the RHS instead of opening the next slot: 1e7 flat device launch 84.0 -> 83.4 ms
+    // (3 interleaved pairs, profiles/r05c_ab_prefetch.jsonl)
     SlotRow Rnext = T.row[0];
 #endif
 #pragma unroll SUNROLL
@@ -929,7 +930,7 @@ __global__ __launch_bounds__(BLOCK, WPS) void propagate_kernel(const KParams P_i
       if (outlier) __builtin_amdgcn_s_setprio(3);
       else __builtin_amdgcn_s_setprio(1);
 #endif
-#ifdef ART_SLOT_PREFETCH
+#ifndef ART_NO_SLOT_PREFETCH
       const SlotRow R = Rnext;
 #else
       const SlotRow R = T.row[s];
@@ -957,7 +958,7 @@ __global__ __launch_bounds__(BLOCK, WPS) void propagate_kernel(const KParams P_i
 #pragma unroll
       for (int i = 0; i < 7; ++i) y[i] = u[i] + hs * acc[i];
       const double ty = tau + R.ct * hs;
-#ifdef ART_SLOT_PREFETCH
+#ifndef ART_NO_SLOT_PREFETCH
       Rnext = T.row[s + 1 < NSLOT ? s + 1 : s];
 #endif
       ART_SMARK(8)
@@ -2499,7 +2500,8 @@ __global__ __launch_bounds__(256) void helper_kernel(const KParams P, const int6
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       if (tid == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        if (what == 2 && out.blob_host) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // (the blob in host memory)
+        else __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (what == 1) {
           for (int64_t c = t / CHUNK; c * CHUNK < t1; ++c)

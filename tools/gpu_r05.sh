@@ -15,6 +15,27 @@ run_step() {
       timeout -k 10 400 python3 -u -m pytest tests/test_gpu_configs2_full.py -m gpu -v -k rehearsal --timeout 300 --timeout-method thread > ${O}_pytest_rehearsal.log 2>&1 ;;
     pytest_host)  # the host paths: streamed, give-up, async
       timeout -k 10 600 python3 -u -m pytest tests/test_edges.py tests/test_gpu_async_host.py -m gpu -v --timeout 300 --timeout-method thread > ${O}_pytest_host.log 2>&1 ;;
+    pytest_direct)  # the host paths with the pieces' blobs in pinned host memory (ART_HOST_DIRECT=1)
+      ART_HOST_DIRECT=1 timeout -k 10 600 python3 -u -m pytest tests/test_edges.py tests/test_gpu_async_host.py -m gpu -v --timeout 300 --timeout-method thread > ${O}_pytest_direct.log 2>&1 ;;
+    shard_t1)  # the 8-GPU shard size, one call at a time, traced; then the same with direct blobs
+      ART_HOST_TRACE=1 timeout -k 10 300 python3 -u bench.py --rays 1250000 --steps 10 --warmup 2 --no-cpu-baseline --no-device --inflight 1 > ${O}_bench_1250000_if1_trace.json 2> ${O}_shard_if1_trace.err &&
+      ART_HOST_DIRECT=1 ART_HOST_TRACE=1 timeout -k 10 300 python3 -u bench.py --rays 1250000 --steps 10 --warmup 2 --no-cpu-baseline --no-device --inflight 1 > ${O}_bench_1250000_if1_direct_trace.json 2> ${O}_shard_if1_direct_trace.err ;;
+    ab_direct)  # interleaved: host pipeline with download copies vs direct blobs, 1e7 and 1.25e6, one call in flight
+      for r in 1 2; do
+        for dm in 0 1; do
+          ART_HOST_DIRECT=$dm timeout -k 10 300 python3 -u bench.py --no-cpu-baseline --no-device --steps 10 --warmup 2 --inflight 1 > ${O}_abd_1e7_d${dm}_r$r.json 2>> ${O}_ab_direct.err || return 1
+          ART_HOST_DIRECT=$dm timeout -k 10 300 python3 -u bench.py --rays 1250000 --no-cpu-baseline --no-device --steps 10 --warmup 2 --inflight 1 > ${O}_abd_1250000_d${dm}_r$r.json 2>> ${O}_ab_direct.err || return 1
+        done
+      done ;;
+    ab_gr_pf)  # GR 1e6 batch: slot-row prefetch (this build) vs without, interleaved
+      for r in 1 2; do
+        timeout -k 10 300 python3 -u bench.py --config gr --rays 1000000 --steps 5 --warmup 1 --no-cpu-baseline --no-device > ${O}_abpf_gr_base_r$r.json 2>> ${O}_ab_gr_pf.err || return 1
+        ART_LIB=tools/build/libart_nopf.so timeout -k 10 300 python3 -u bench.py --config gr --rays 1000000 --steps 5 --warmup 1 --no-cpu-baseline --no-device > ${O}_abpf_gr_nopf_r$r.json 2>> ${O}_ab_gr_pf.err || return 1
+      done ;;
+    fetch_grad)  # device-resident 1e7 launch: FETCH_SIZE with graduation at its default and off
+      timeout -s KILL 200 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d ${O}_fetch/grad_default -o p --output-format csv -- python3 tools/exp_sections.py > ${O}_fetch_grad_default.log 2>&1 &&
+      ART_GRADUATE=0 timeout -s KILL 200 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d ${O}_fetch/grad_off -o p --output-format csv -- python3 tools/exp_sections.py > ${O}_fetch_grad_off.log 2>&1 &&
+      timeout -s KILL 200 rocprofv3 --kernel-trace --pmc TCC_HIT_sum TCC_MISS_sum -d ${O}_fetch/hit_default -o p --output-format csv -- python3 tools/exp_sections.py > ${O}_fetch_hit_default.log 2>&1 ;;
     pytest_edges)
       timeout -k 10 400 python3 -u -m pytest tests/test_edges.py -m gpu -v --timeout 300 --timeout-method thread > ${O}_pytest_edges.log 2>&1 ;;
     smoke)
