@@ -1167,6 +1167,39 @@ int propagate_host_maskless(DeviceCtx* c, HostLane* H, bool overlap, const art_p
   for (int k = 0; k <= HSIG_NFLAG; ++k) __atomic_store_n(hflag + k, 0ull, __ATOMIC_RELEASE);  // (+ the started count)
   __atomic_store_n(hdone, 0ull, __ATOMIC_RELEASE);
   __atomic_store_n(H->abort_host, 0u, __ATOMIC_RELEASE);
+  // The host gathers the upload units from the caller's arrays into pinned staging on a thread of
+  // its own, from the call's first moment: the set-up and launches below (~1.5 ms at 1.25e6 rays)
+  // and the first units' gathers overlap instead of adding up (profiles/r05d_shard_if1_trace.err).
+  // (tests: ART_HOST_UPLOAD_DELAY_MS holds back the second upload unit, so the integrator's
+  // waves outwait their 2 s bound and the device side gives the call up)
+  const int delay_ms = env_int("ART_HOST_UPLOAD_DELAY_MS", 0);
+  std::atomic<int> gathered{0};
+  std::atomic<bool> gstop{false};
+  std::thread gatherer([&] {
+    using Seg = CopyPool::Seg;
+    for (int u = 0; u < nu && !gstop.load(); ++u) {
+      if (delay_ms > 0 && u == 1)
+        for (int w = 0; w < delay_ms && !gstop.load(); ++w) std::this_thread::sleep_for(std::chrono::milliseconds(1));
+      const int64_t lo = ulo[u], m = ulo[u + 1] - lo;
+      const double* src[9] = {x0, x0 + n, x0 + 2 * n, k0, k0 + n, k0 + 2 * n, erg, dw, ln_t0};
+      std::vector<Seg> g;
+      for (int r = 0; r < 9; ++r) g.push_back({pin + r * nd + lo, src[r] + lo, (size_t)m * sizeof(double)});
+      g.push_back({(int8_t*)(pin + 9 * nd) + lo, species + lo, (size_t)m});
+      const double tg0 = clk();
+      copy_pool().run(g);
+      gathered.store(u + 1, std::memory_order_release);
+      if (trace) std::fprintf(stderr, "[art-host] t=%.2f unit %d gathered in %.2f ms\n", tg0 - t_start, u, clk() - tg0);
+    }
+  });
+  // (every return below, the early ones of HIP_OK included, stops and joins the gatherer first)
+  struct JoinOnExit {
+    std::atomic<bool>& stop;
+    std::thread& t;
+    ~JoinOnExit() {
+      stop = true;
+      if (t.joinable()) t.join();
+    }
+  } gjoin{gstop, gatherer};
   HIP_OK(hipMemsetAsync(words, 0, head + ccb, H->m_comp));
   // the batch's flux: binned by the helpers as they finalize (bins <= FLUX_HELPER_BINS), else by
   // flux kernels over the pieces' blobs after the integrator
@@ -1224,6 +1257,7 @@ int propagate_host_maskless(DeviceCtx* c, HostLane* H, bool overlap, const art_p
   HIP_OK(hipEventRecord(ev_zero, H->m_comp));
   HIP_OK(hipStreamWaitEvent(H->m_help, ev_zero, 0));
   if (!serial) HIP_OK(art::launch_helpers(K, n, in, so, helpers, -1, 1, words + 1, H->m_help));
+  if (trace) std::fprintf(stderr, "[art-host] t=%.2f counters zeroed, helpers launched\n", clk() - t_start);
   // the integrator, once every helper block is resident: before the uploads when they are at once
   // (a lone call), else from the upload loop as soon as they are (a call overlapping the previous
   // one, whose blocks hold the slots until its drain)
@@ -1273,6 +1307,8 @@ int propagate_host_maskless(DeviceCtx* c, HostLane* H, bool overlap, const art_p
       std::this_thread::sleep_for(std::chrono::microseconds(5));
     }
     if (helpers_in() && (rc = launch_main())) return rc;
+    if (trace) std::fprintf(stderr, "[art-host] t=%.2f helpers resident (%.2f ms), integrator launched\n", clk() - t_start,
+                            clk() - tw);
   }
   // a host thread raises the ready counter as each unit's copies land
   std::atomic<int> recorded{0};
@@ -1353,27 +1389,23 @@ int propagate_host_maskless(DeviceCtx* c, HostLane* H, bool overlap, const art_p
     return moved;
   };
   int perr = 0;
-  // (tests: ART_HOST_UPLOAD_DELAY_MS holds back the second upload unit, so the integrator's
-  // waves outwait their 2 s bound and the device side gives the call up)
-  const int delay_ms = env_int("ART_HOST_UPLOAD_DELAY_MS", 0);
   for (int u = 0; u < nu && !perr; ++u) {
     if (!launched && helpers_in() && launch_main() != ART_OK) perr = 1;
+    while (!perr && gathered.load(std::memory_order_acquire) <= u) {  // (the gatherer is ahead of the H2D copies)
+      if (progress() < 0) perr = 1;
+      if (!launched && helpers_in() && launch_main() != ART_OK) perr = 1;
+      std::this_thread::sleep_for(std::chrono::microseconds(5));
+    }
+    if (perr) break;
     const int64_t lo = ulo[u], m = ulo[u + 1] - lo;
-    if (delay_ms > 0 && u == 1) std::this_thread::sleep_for(std::chrono::milliseconds(delay_ms));
-    const double* src[9] = {x0, x0 + n, x0 + 2 * n, k0, k0 + n, k0 + 2 * n, erg, dw, ln_t0};
-    std::vector<Seg> g;
-    for (int r = 0; r < 9; ++r) g.push_back({pin + r * nd + lo, src[r] + lo, (size_t)m * sizeof(double)});
-    g.push_back({(int8_t*)(pin + 9 * nd) + lo, species + lo, (size_t)m});
-    const double tg0 = clk();
-    copy_pool().run(g);
-    for (int r = 0; r < 9 && !perr; ++r)
-      perr |= hipMemcpyAsync(di + r * nd + lo, pin + r * nd + lo, (size_t)m * sizeof(double), hipMemcpyHostToDevice,
-                             H->m_up) != hipSuccess;
+    // the nine double rows of the unit in one strided copy (one DMA command instead of nine)
+    perr |= hipMemcpy2DAsync(di + lo, nd * sizeof(double), pin + lo, nd * sizeof(double), (size_t)m * sizeof(double), 9,
+                             hipMemcpyHostToDevice, H->m_up) != hipSuccess;
     perr |= hipMemcpyAsync((int8_t*)(di + 9 * nd) + lo, (int8_t*)(pin + 9 * nd) + lo, (size_t)m, hipMemcpyHostToDevice,
                            H->m_up) != hipSuccess;
     perr |= hipEventRecord(ev_up[u], H->m_up) != hipSuccess;
     recorded.store(u + 1, std::memory_order_release);
-    if (trace) std::fprintf(stderr, "[art-host] t=%.2f unit %d gathered in %.2f ms%s\n", tg0 - t_start, u, clk() - tg0,
+    if (trace) std::fprintf(stderr, "[art-host] t=%.2f unit %d submitted%s\n", clk() - t_start, u,
                             launched ? "" : " (integrator not launched yet)");
     if (!perr && progress() < 0) perr = 1;
   }

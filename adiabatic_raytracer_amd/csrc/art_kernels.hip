@@ -918,23 +918,23 @@ __global__ __launch_bounds__(BLOCK, WPS) void propagate_kernel(const KParams P_i
     double kA[7], y[7], kk[7];
 #pragma unroll
     for (int i = 0; i < 7; ++i) kA[i] = 0.0;  // read (times a zero coefficient) before its first store
+    // flat builds: the next slot's row of scalars is loaded before this slot's RHS, so its
+    // scalar-load latency hides behind the RHS instead of opening the next slot: 1e7 flat device
+    // launch 84.0 -> 83.4 ms (3 interleaved pairs, profiles/r05c_ab_prefetch.jsonl); the GR build
+    // (slot loop unrolled by two) lost 0.5% with it (profiles/r05d_ab_gr_prefetch.txt)
 #ifndef ART_NO_SLOT_PREFETCH
-    // the next slot's row of scalars is loaded before this slot's RHS, so its scalar-load latency
-    // hides behind the RHS instead of opening the next slot: 1e7 flat device launch 84.0 -> 83.4 ms
-    // (3 interleaved pairs, profiles/r05c_ab_prefetch.jsonl)
-    SlotRow Rnext = T.row[0];
+    constexpr bool PF = GEOM == GEOM_FLAT;
+#else
+    constexpr bool PF = false;
 #endif
+    SlotRow Rnext = T.row[0];
 #pragma unroll SUNROLL
     for (int s = 0; s < NSLOT; ++s) {
 #ifdef ART_PRIO_GLUE  // (dev A/B) the stage combination's LDS reads at the high priority
       if (outlier) __builtin_amdgcn_s_setprio(3);
       else __builtin_amdgcn_s_setprio(1);
 #endif
-#ifndef ART_NO_SLOT_PREFETCH
-      const SlotRow R = Rnext;
-#else
-      const SlotRow R = T.row[s];
-#endif
+      const SlotRow R = PF ? Rnext : T.row[s];
       const double cf = R.cf, cA = R.cA;
       double acc[7];
 #pragma unroll
@@ -958,9 +958,7 @@ __global__ __launch_bounds__(BLOCK, WPS) void propagate_kernel(const KParams P_i
 #pragma unroll
       for (int i = 0; i < 7; ++i) y[i] = u[i] + hs * acc[i];
       const double ty = tau + R.ct * hs;
-#ifndef ART_NO_SLOT_PREFETCH
-      Rnext = T.row[s + 1 < NSLOT ? s + 1 : s];
-#endif
+      if constexpr (PF) Rnext = T.row[s + 1 < NSLOT ? s + 1 : s];
       ART_SMARK(8)
 #ifdef ART_PRIO_GLUE
       if (outlier) __builtin_amdgcn_s_setprio(2);
@@ -3396,13 +3394,16 @@ hipError_t launch_sample(const KParams& P, double maxR, uint64_t seed, int64_t r
                          double* k, double* erg, double* vifty, int32_t* w, int32_t* att, unsigned long long* queue,
                          hipStream_t s) {
   // lines of up to 2.2 x 60 km (264 steps): the 3-wave build; longer ones: 2 waves
-  // (ART_SAMPLER_WPS=2|3 forces one, for A/B runs)
+  // (ART_SAMPLER_WPS=2|3|4 forces one, for A/B runs; 4 spills ~200 VGPRs)
   int wps = maxR <= 60.0 ? 3 : 2;
   if (const char* e = std::getenv("ART_SAMPLER_WPS"))
-    if (e[0] == '2' || e[0] == '3') wps = e[0] - '0';
-  const void* fn = wps == 3 ? (const void*)sample_kernel<3> : (const void*)sample_kernel<2>;
+    if (e[0] == '2' || e[0] == '3' || e[0] == '4') wps = e[0] - '0';
+  const void* fn = wps == 4 ? (const void*)sample_kernel<4> : wps == 3 ? (const void*)sample_kernel<3> : (const void*)sample_kernel<2>;
   const int grid = persistent_blocks(fn, n, 256, 1);
-  if (wps == 3)
+  if (wps == 4)
+    hipLaunchKernelGGL(sample_kernel<4>, dim3(grid), dim3(256), 0, s, P, maxR, seed, ray_offset, n, x, k, erg, vifty, w,
+                       att, queue);
+  else if (wps == 3)
     hipLaunchKernelGGL(sample_kernel<3>, dim3(grid), dim3(256), 0, s, P, maxR, seed, ray_offset, n, x, k, erg, vifty, w,
                        att, queue);
   else

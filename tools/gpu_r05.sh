@@ -36,6 +36,19 @@ run_step() {
       timeout -s KILL 200 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d ${O}_fetch/grad_default -o p --output-format csv -- python3 tools/exp_sections.py > ${O}_fetch_grad_default.log 2>&1 &&
       ART_GRADUATE=0 timeout -s KILL 200 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d ${O}_fetch/grad_off -o p --output-format csv -- python3 tools/exp_sections.py > ${O}_fetch_grad_off.log 2>&1 &&
       timeout -s KILL 200 rocprofv3 --kernel-trace --pmc TCC_HIT_sum TCC_MISS_sum -d ${O}_fetch/hit_default -o p --output-format csv -- python3 tools/exp_sections.py > ${O}_fetch_hit_default.log 2>&1 ;;
+    shard_fu)  # 1.25e6 rays, one call at a time: first upload unit 2^16 (default) vs 2^18, interleaved; then one traced run
+      for r in 1 2; do
+        for fu in 65536 262144; do
+          ART_HOST_FIRST_UNIT=$fu timeout -k 10 300 python3 -u bench.py --rays 1250000 --no-cpu-baseline --no-device --steps 10 --warmup 2 --inflight 1 > ${O}_fu_${fu}_r$r.json 2>> ${O}_shard_fu.err || return 1
+        done
+      done &&
+      ART_HOST_TRACE=1 timeout -k 10 300 python3 -u bench.py --rays 1250000 --steps 10 --warmup 2 --no-cpu-baseline --no-device --inflight 1 > ${O}_bench_1250000_if1_trace.json 2> ${O}_shard_if1_trace.err ;;
+    ab_swps)  # sampler: 2, 3 and 4 waves/SIMD builds, interleaved
+      for r in 1 2; do
+        for w in 2 3 4; do
+          ART_SAMPLER_WPS=$w timeout -k 10 300 python3 -u tools/exp_sampler_time.py > ${O}_swps_${w}_r$r.jsonl 2>> ${O}_ab_swps.err || return 1
+        done
+      done ;;
     pytest_edges)
       timeout -k 10 400 python3 -u -m pytest tests/test_edges.py -m gpu -v --timeout 300 --timeout-method thread > ${O}_pytest_edges.log 2>&1 ;;
     smoke)
