@@ -49,6 +49,17 @@ run_step() {
           ART_SAMPLER_WPS=$w timeout -k 10 300 python3 -u tools/exp_sampler_time.py > ${O}_swps_${w}_r$r.jsonl 2>> ${O}_ab_swps.err || return 1
         done
       done ;;
+    ab_host)  # this build vs tools/build/libart_prev.so (the previous commit), interleaved: 1.25e6 with 1 and 2 calls in flight, 1e7
+      for r in 1 2; do
+        for lib in base prev; do
+          if [ $lib = prev ]; then export ART_LIB=tools/build/libart_prev.so; else unset ART_LIB; fi
+          timeout -k 10 300 python3 -u bench.py --rays 1250000 --no-cpu-baseline --no-device --steps 10 --warmup 2 --inflight 1 > ${O}_abh_1250000_if1_${lib}_r$r.json 2>> ${O}_ab_host.err &&
+          timeout -k 10 300 python3 -u bench.py --rays 1250000 --no-cpu-baseline --no-device --steps 10 --warmup 2 --inflight 2 > ${O}_abh_1250000_if2_${lib}_r$r.json 2>> ${O}_ab_host.err &&
+          timeout -k 10 300 python3 -u bench.py --no-cpu-baseline --no-device --steps 10 --warmup 2 > ${O}_abh_1e7_${lib}_r$r.json 2>> ${O}_ab_host.err || { unset ART_LIB; return 1; }
+        done
+      done; unset ART_LIB ;;
+    shard_trace)  # 1.25e6 rays, one call at a time, traced
+      ART_HOST_TRACE=1 timeout -k 10 300 python3 -u bench.py --rays 1250000 --steps 10 --warmup 2 --no-cpu-baseline --no-device --inflight 1 > ${O}_bench_1250000_if1_trace.json 2> ${O}_shard_if1_trace.err ;;
     pytest_edges)
       timeout -k 10 400 python3 -u -m pytest tests/test_edges.py -m gpu -v --timeout 300 --timeout-method thread > ${O}_pytest_edges.log 2>&1 ;;
     smoke)
