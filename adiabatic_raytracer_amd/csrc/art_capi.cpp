@@ -74,7 +74,7 @@ using PoolVec = std::vector<std::pair<void*, size_t>>;
 // drain); lane 0 also serves the synchronous calls, which first wait for every async call.
 constexpr int HOST_LANES = 2;
 struct HostLane {
-  hipStream_t m_comp = nullptr, m_up = nullptr, m_dn = nullptr, m_help = nullptr, m_fin = nullptr;
+  hipStream_t m_comp = nullptr, m_up = nullptr, m_dn = nullptr, m_help = nullptr;
   unsigned long long* hsig = nullptr;  // [0] ready | [8, 8 + 64) piece flags | [72] helper blocks started
   unsigned long long* hsig_dev = nullptr;
   unsigned int* abort_host = nullptr;  // the word the waves and helpers raise (or read) when a call gives up
@@ -355,7 +355,7 @@ void release_ctx(DeviceCtx& c) {
     for (auto& e : H.pinned)
       if (e.p) (void)hipHostFree(e.p);
     for (hipEvent_t e : H.pev) (void)hipEventDestroy(e);
-    for (hipStream_t s : {H.m_comp, H.m_up, H.m_dn, H.m_help, H.m_fin})
+    for (hipStream_t s : {H.m_comp, H.m_up, H.m_dn, H.m_help})
       if (s) (void)hipStreamDestroy(s);
     if (H.hsig) (void)hipHostFree(H.hsig);
     if (H.abort_host) (void)hipHostFree(H.abort_host);
@@ -1058,7 +1058,6 @@ int lane_setup(DeviceCtx* c, HostLane* H) {
     for (int i = 0; i < ncu_all; ++i) all[i / 32] |= 1u << (i % 32);
     HIP_OK(hipExtStreamCreateWithCUMask(&H->m_comp, (uint32_t)all.size(), all.data()));
     HIP_OK(hipExtStreamCreateWithCUMask(&H->m_help, (uint32_t)all.size(), all.data()));
-    HIP_OK(hipExtStreamCreateWithCUMask(&H->m_fin, (uint32_t)all.size(), all.data()));
     HIP_OK(hipStreamCreateWithFlags(&H->m_up, hipStreamNonBlocking));
     HIP_OK(hipStreamCreateWithFlags(&H->m_dn, hipStreamNonBlocking));
   }
@@ -1248,13 +1247,9 @@ int propagate_host_maskless(DeviceCtx* c, HostLane* H, bool overlap, const art_p
   // integrator and finalized after it, kernel by kernel: for a counter-collection run, which
   // serialises kernels; the integrator's code and traffic are the same)
   const bool serial = env_int("ART_HOST_STREAM_SERIAL", 0) != 0;
-  // A finalize pass of every block slot joins the helpers for the batch's last pieces: launched on a
-  // stream (hardware queue) of its own once the first piece is flagged, its blocks take the
-  // integrator's slots as its waves retire in the drain, instead of after the whole launch (the
-  // pieces completing in the drain were finalized by the 8 helpers alone, ~0.2 ms each, 1.25e6
-  // rays: profiles/r05e_shard_if1_trace.err). Not when this call overlaps the next one
-  // (art_propagate_host_flux_async): that call's integrator takes the slots, and the helpers
-  // finalize alone. (Serial runs: one pass after the integrator, on its stream.)
+  // After the integrator, one pass of every block slot finalizes what is left -- unless this call
+  // overlaps the next one (art_propagate_host_flux_async): then the next call's integrator would
+  // hold those slots, and the helpers finalize alone
   const bool final_pass = serial || !overlap;
   const int iblocks = serial ? slots : slots - helpers;
   so.exit_expected = (serial ? 0 : helpers) + (final_pass ? slots : 0);
@@ -1286,7 +1281,7 @@ int propagate_host_maskless(DeviceCtx* c, HostLane* H, bool overlap, const art_p
     HIP_OK(art::launch_integrator_streamed(K, n, in, so, max_crossings, words, words + 1, iblocks, H->m_comp, &grid));
     L->grid = grid;
     HIP_OK(hipEventRecord(L->ev1, H->m_comp));
-    if (serial) {
+    if (final_pass) {
       HIP_OK(art::launch_helpers(K, n, in, so, slots, -1, 0, words + 1, H->m_comp));
       hipEvent_t ev_help = H->pev[nu + np + 1];  // (the persistent helpers' init counts, in the statistics)
       HIP_OK(hipEventRecord(ev_help, H->m_help));
@@ -1294,8 +1289,8 @@ int propagate_host_maskless(DeviceCtx* c, HostLane* H, bool overlap, const art_p
       HIP_OK(hipMemcpyAsync(L->host_stats, words + 1, sizeof(unsigned long long) * art::N_STATS_DEV,
                             hipMemcpyDeviceToHost, H->m_comp));
     }
-    // (the statistics come from the helpers' completion words, and nothing after the integrator
-    // waits on this stream: for CU slots a next, overlapping call holds)
+    // (overlapping calls: the statistics come from the helpers' completion words, and nothing
+    // after the integrator waits on this stream for CU slots the next call holds)
     HIP_OK(hipEventRecord(L->done, H->m_comp));
     L->stream = H->m_comp;
     L->pending = true;
@@ -1397,15 +1392,8 @@ int propagate_host_maskless(DeviceCtx* c, HostLane* H, bool overlap, const art_p
     }
     return moved;
   };
-  bool fin_pending = final_pass && !serial, int_logged = false;
-  auto maybe_final_pass = [&]() -> int {  // once the first piece is flagged or the integrator is done
-    if (!fin_pending || !launched || (dk == 0 && hipEventQuery(L->ev1) != hipSuccess)) return 0;
-    fin_pending = false;
-    if (art::launch_helpers(K, n, in, so, slots, -1, 0, words + 1, H->m_fin) != hipSuccess) return -1;
-    if (trace) std::fprintf(stderr, "[art-host] t=%.2f finalize pass launched\n", clk() - t_start);
-    return 0;
-  };
   int perr = 0;
+  bool int_logged = false;  // (trace)
   for (int u = 0; u < nu && !perr; ++u) {
     if (!launched && helpers_in() && launch_main() != ART_OK) perr = 1;
     while (!perr && gathered.load(std::memory_order_acquire) <= u) {  // (the gatherer is ahead of the H2D copies)
@@ -1424,7 +1412,7 @@ int propagate_host_maskless(DeviceCtx* c, HostLane* H, bool overlap, const art_p
     recorded.store(u + 1, std::memory_order_release);
     if (trace) std::fprintf(stderr, "[art-host] t=%.2f unit %d submitted%s\n", clk() - t_start, u,
                             launched ? "" : " (integrator not launched yet)");
-    if (!perr && (progress() < 0 || maybe_final_pass() < 0)) perr = 1;
+    if (!perr && progress() < 0) perr = 1;
   }
   if (!perr && !launched) {  // the helpers wait for CU slots the previous call still holds
     const double tw = clk();
@@ -1469,7 +1457,7 @@ int propagate_host_maskless(DeviceCtx* c, HostLane* H, bool overlap, const art_p
       std::fprintf(stderr, "[art-host] t=%.2f integrator done\n", clk() - t_start);
     }
     const int mv = progress();
-    if (mv < 0 || ready_err.load() || maybe_final_pass() < 0) {
+    if (mv < 0 || ready_err.load()) {
       gave_up = true;
       break;
     }
@@ -1485,10 +1473,6 @@ int propagate_host_maskless(DeviceCtx* c, HostLane* H, bool overlap, const art_p
   }
   // the call's end: the helpers' completion words (the statistics, the flux), raised by the last
   // serving helper block once every integrator wave has counted itself (bounded like the pieces)
-  if (!gave_up && fin_pending) {  // (not launched yet: now, since the completion counts its blocks)
-    fin_pending = false;
-    if (art::launch_helpers(K, n, in, so, slots, -1, 0, words + 1, H->m_fin) != hipSuccess) gave_up = true;
-  }
   if (!gave_up) {
     while (__atomic_load_n(hdone, __ATOMIC_ACQUIRE) == 0ull) {
       if (__atomic_load_n(H->abort_host, __ATOMIC_ACQUIRE) != 0u || clk() - t_last > limit_ms) {
@@ -1510,7 +1494,6 @@ int propagate_host_maskless(DeviceCtx* c, HostLane* H, bool overlap, const art_p
     (void)hipStreamSynchronize(H->m_up);
     (void)hipStreamSynchronize(H->m_comp);
     (void)hipStreamSynchronize(H->m_help);
-    (void)hipStreamSynchronize(H->m_fin);
     (void)hipStreamSynchronize(H->m_dn);
     (void)hipGetLastError();
     if (trace) {  // the device counters at the give-up
@@ -1545,14 +1528,12 @@ int propagate_host_maskless(DeviceCtx* c, HostLane* H, bool overlap, const art_p
     HIP_OK(hipMemcpyAsync(fx.hist, hist_dev, 2 * (size_t)fx.nbins * sizeof(double), hipMemcpyDeviceToHost, H->m_comp));
     HIP_OK(hipStreamSynchronize(H->m_comp));
   }
-  if (complete && !serial) {  // the statistics from the completion words
+  if (complete && !final_pass) {  // the statistics from the completion words
     unsigned long long st[art::N_STATS_DEV];
     for (int i = 0; i < art::N_STATS_DEV; ++i) st[i] = __atomic_load_n(hdone + art::DONE_STATS + i, __ATOMIC_ACQUIRE);
     return latch_launch(c, L, st);
   }
-  if (!serial) {  // (the helpers' copy timed out: the statistics as the streams have them)
-    HIP_OK(hipStreamSynchronize(H->m_fin));
-    HIP_OK(hipStreamSynchronize(H->m_help));
+  if (!final_pass) {  // (the helpers' copy timed out: the statistics as the stream has them)
     HIP_OK(hipMemcpyAsync(L->host_stats, words + 1, sizeof(unsigned long long) * art::N_STATS_DEV, hipMemcpyDeviceToHost,
                           H->m_comp));
     HIP_OK(hipStreamSynchronize(H->m_comp));
