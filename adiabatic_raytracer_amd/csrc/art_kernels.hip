@@ -2594,11 +2594,47 @@ __device__ inline double line_rmin2(const double* x0, const double* va, double s
   return xm[0] * xm[0] + xm[1] * xm[1] + xm[2] * xm[2];
 }
 
+// The sampler's certificates on the segment [s0, s1] of a line (x0 + va s, energy E): 1 when every
+// point of it provably has a negative condition, 2 when every point provably has a positive one,
+// 0 otherwise. The bounds are derived at sample_kernel's step loop; both hold for a segment of any
+// length (a block of steps as well as one step) and whatever the sign of the point before it.
+#ifdef ART_SEGCERT_NOINLINE
+#define ART_SEGCERT_ATTR __attribute__((noinline))
+#else
+#define ART_SEGCERT_ATTR inline
+#endif
+__device__ ART_SEGCERT_ATTR int seg_cert(const KParams& P, const double* X0, const double* VA, double E, double s0,
+                                         double s1, double cert_lhs, double cert_rhs) {
+  const double rm2 = line_rmin2(X0, VA, s0, s1);
+  const double rmin = sqrt(rm2);
+  double xa[3], xb[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) { xa[i] = X0[i] + VA[i] * s0; xb[i] = X0[i] + VA[i] * s1; }
+  const double ra2 = xa[0] * xa[0] + xa[1] * xa[1] + xa[2] * xa[2];
+  const double rb2 = xb[0] * xb[0] + xb[1] * xb[1] + xb[2] * xb[2];
+  // (reciprocals from frcp, <= 1 ulp: the margins, 1e-9 relative and 1e-12 absolute on db and 1e-6
+  // on m_a², dwarf that; a certified segment is still provably one-signed)
+  const double ba = (P.cm * (3.0 * xa[2] * xa[2] - ra2) + 3.0 * P.sm * xa[0] * xa[2]) * frcp(ra2);
+  const double bb = (P.cm * (3.0 * xb[2] * xb[2] - rb2) + 3.0 * P.sm * xb[0] * xb[2]) * frcp(rb2);
+  const double irmin = frcp(rmin);
+  const double al = (s1 - s0) * irmin;
+  const double db = 0.75 * al * al * (1.0 + 1e-9) + 1e-12;
+  const double bmax = fmin(2.0, fmax(fabs(ba), fabs(bb)) + db);
+  if (cert_lhs * 0.5 * bmax < cert_rhs * (rm2 * rmin)) return 1;
+  if (rmin > 10.0) {
+    const double bmin = (ba * bb > 0.0) ? fmin(fabs(ba), fabs(bb)) - db : -1.0;
+    const double rmax2 = fmax(ra2, rb2);
+    const double grr = 1.0 - P.rs_gr * irmin * (1.0 + 1e-15);  // (rounded down: a smaller g^rr)
+    if (bmin > 0.0 && P.wp2n * bmin * grr > E * E * (1.0 + 1e-6) * (rmax2 * sqrt(rmax2))) return 2;
+  }
+  return 0;
+}
+
 // Two builds, by waves per SIMD (the LDS allows 3): at 3 the kernel spills a few
 // loop-invariant values, reloaded once per scan step -- a good trade where a line has ~111
 // steps with uncertified ones among them, not where it has ~650 mostly skipped ones
 // (launch_sample picks by the line length).
-template <int WPS>
+template <int WPS, bool BLOCKS>
 __global__ __launch_bounds__(256, WPS) void sample_kernel(const KParams P, const double maxR, const uint64_t seed,
                                                      const int64_t ray_offset, const int64_t n, double* __restrict__ xo,
                                                      double* __restrict__ ko, double* __restrict__ ergo,
@@ -2613,6 +2649,7 @@ __global__ __launch_bounds__(256, WPS) void sample_kernel(const KParams P, const
   __shared__ double sqa[4 * SQCAP], sqb[4 * SQCAP];  // bracket queue: ends -> root
   __shared__ unsigned char sqsrc[4 * SQCAP], sqok[4 * SQCAP];
   __shared__ double sgrid[32];  // (0.5 j)/19: a full step's grid offsets, the same rounding as the division
+  __shared__ unsigned char spair[4 * 64 * 3];  // a wave's (lane, step of the block) pairs to scan: lane << 2 | step
   const int lane = threadIdx.x & 63;
   const int wb = threadIdx.x & ~63;
   const int wq = (threadIdx.x >> 6) * SQCAP;
@@ -2789,6 +2826,205 @@ __global__ __launch_bounds__(256, WPS) void sample_kernel(const KParams P, const
     };
 
     ART_QMARK(0)
+    if constexpr (BLOCKS) {
+    // Blocks of KB = 3 steps (1.5 km). Per block: ONE certificate of the whole block per lane (most
+    // blocks away from the conversion surface pass it); the steps of the lanes whose block failed
+    // are certified one by one as wave-cooperative items (lane, step); the grid points of every
+    // uncertified (lane, step) pair of the block are evaluated together, 64 items a pass, so a pass
+    // is rarely left part-empty. A certificate holds whatever the point before it (the sign logic
+    // below sees a certified point as the value it provably has: nonzero, of the certified sign),
+    // so a block or step is certified whatever c_prev is, and a sign change at its first point is
+    // found by the same bit logic as an evaluated one. The evaluated points and their arithmetic
+    // are those of the step-by-step scan (ART_SAMPLER_STEPWISE), so the samples do not change.
+#ifndef ART_SAMPLER_KB
+    constexpr int KB = 3;  // (the step masks of a block share 64-bit words: at most 3 steps)
+#else
+    constexpr int KB = ART_SAMPLER_KB;  // (dev A/B: 1 or 2)
+#endif
+    const int wp = (threadIdx.x >> 6) * 64 * 3;  // this wave's pair list in spair
+    for (int st0 = 0; st0 < nsteps; st0 += KB) {
+#ifdef ART_SAMPLER_SECTIONS
+      q_sec[7] += 1;
+#endif
+      const int kmax = min(KB, nsteps - st0);
+      const double S0 = st0 * 0.5;
+      const double S1 = fmin((st0 + kmax - 1) * 0.5 + 0.5, send);
+      const bool quiet = !active || (cert_ok && c_prev < 0.0 && (S1 < w_in || S0 > w_out));
+      if (__ballot(!quiet) == 0ull) {
+        // every lane outside its window: jump to one step before the earliest next window start
+        int nxt = (active && S1 < w_in && w_in < send) ? (int)floor(w_in * 2.0) - 1 : nsteps;
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) nxt = min(nxt, __shfl_xor(nxt, o));
+        if (nxt > st0 + KB) st0 = nxt - KB;
+        continue;
+      }
+      ART_QMARK(1)
+      int bc = 0;  // the whole block certified: 1 negative, 2 positive
+      if (active && quiet) {
+        bc = 1;  // outside its window after a negative point
+      } else if (active && cert_ok) {
+        const double X0[3] = {Lx[0], Lx[256], Lx[2 * 256]}, VA[3] = {Lx[3 * 256], Lx[4 * 256], Lx[5 * 256]};
+        bc = seg_cert(P, X0, VA, E, S0, S1, cert_lhs, cert_rhs);
+      }
+      const unsigned kmask = (1u << kmax) - 1u;
+      unsigned cneg = bc == 1 ? kmask : 0u, cpos = bc == 2 ? kmask : 0u;  // certified steps, bit k
+      // the steps of the lanes whose block failed, certified as items (lane u, step k), t = u kmax + k
+      const bool fail = active && cert_ok && bc == 0 && kmax > 1;
+      const unsigned long long mF = __ballot(fail);
+      if (mF != 0ull) {
+        const int nF = __popcll(mF);
+        const int fix = __popcll(mF & lt);
+        if (fail) ssrc[wb + fix] = (unsigned char)lane;
+        wave_lds_sync();
+        const int totc = nF * kmax;
+        #pragma unroll 1
+        for (int w0 = 0; w0 < totc; w0 += 64) {
+          const int t = w0 + lane;
+          int r = 0;
+          if (t < totc) {
+            const int u = t / kmax;
+            const int k = t - u * kmax;
+            const double* S = sline + wb + ssrc[wb + u];
+            const double X0[3] = {S[0], S[256], S[2 * 256]}, VA[3] = {S[3 * 256], S[4 * 256], S[5 * 256]};
+            const double s0 = (st0 + k) * 0.5;
+            r = seg_cert(P, X0, VA, S[9 * 256], s0, fmin(s0 + 0.5, send), cert_lhs, cert_rhs);
+          }
+          const unsigned long long mn = __ballot(r == 1), mp = __ballot(r == 2);
+          if (fail) {
+            const int a = fix * kmax;
+            const int lo = max(a, w0), hi = min(a + kmax, w0 + 64);
+            if (lo < hi) {
+              const unsigned long long run = (1ull << (hi - lo)) - 1ull;
+              cneg |= (unsigned)((mn >> (lo - w0)) & run) << (lo - a);
+              cpos |= (unsigned)((mp >> (lo - w0)) & run) << (lo - a);
+            }
+          }
+        }
+        wave_lds_sync();
+      }
+      ART_QMARK(2)
+      // the uncertified (lane, step) pairs, lane-major, each lane's in step order: their grid points
+      // are the items t = pair nper + j - 1, and each owner takes its pairs' runs of the ballots
+      const unsigned unc = active ? (kmask & ~(cneg | cpos)) : 0u;
+      const int m = __popc(unc);
+      const unsigned long long b0 = __ballot(m & 1), b1 = __ballot(m & 2);
+      const int off = __popcll(b0 & lt) + 2 * __popcll(b1 & lt);
+      const int npairs = __popcll(b0) + 2 * __popcll(b1);
+      // bits [20 k, 20 k + 20): signbit / nonzero-ness of step k's point j (bit 0: the point before it)
+      unsigned long long sb = 0ull, nz = 0ull;
+      if (npairs > 0) {
+#ifdef ART_SAMPLER_SECTIONS
+        q_sec[6] += 1;
+#endif
+        {
+          unsigned rem = unc;
+          for (int i = 0; rem != 0u; ++i) {
+            spair[wp + off + i] = (unsigned char)(lane << 2 | __builtin_ctz(rem));
+            rem &= rem - 1u;
+          }
+        }
+        wave_lds_sync();
+        const int tot = npairs * nper;
+#ifndef ART_NO_SAMPLER_PRIO  // the dense grid pass at the low issue priority, the rest at the high one
+        __builtin_amdgcn_s_setprio(0);
+#endif
+        #pragma unroll 1
+        for (int w0 = 0; w0 < tot; w0 += 64) {
+          const int t = w0 + lane;
+          bool neg = false, nonz = false;
+          if (t < tot) {
+            const int pr = t / nper;
+            const int j = t - pr * nper + 1;
+            const int e = spair[wp + pr];
+            const int src = e >> 2, k = e & 3;
+            const double* S = sline + wb + src;
+            const double s0 = (st0 + k) * 0.5;
+            const double s1 = fmin(s0 + 0.5, send);
+            // (s1 - s0) j / 19: from the table for a full 0.5 km step, else divided
+            const double sc = s0 + (s1 - s0 == 0.5 ? sgrid[j] : (s1 - s0) * double(j) / double(np - 1));
+            double xl[3];
+#pragma unroll
+            for (int i = 0; i < 3; ++i) xl[i] = S[i * 256] + S[(3 + i) * 256] * sc;
+            const double VL[3] = {S[6 * 256], S[7 * 256], S[8 * 256]};
+            const double v = sampler_condition_e(P, xl, VL, S[9 * 256], S[10 * 256]);
+            if (j == nper && k == kmax - 1) slast[wb + src] = v;
+            neg = signbit(v);
+            nonz = v != 0.0;
+          }
+          const unsigned long long mneg = __ballot(neg), mnz = __ballot(nonz);
+          unsigned rem = unc;
+          for (int i = 0; rem != 0u; ++i) {
+            const int k = __builtin_ctz(rem);
+            rem &= rem - 1u;
+            const int a = (off + i) * nper;
+            const int lo = max(a, w0), hi = min(a + nper, w0 + 64);
+            if (lo < hi) {
+              const unsigned long long run = (1ull << (hi - lo)) - 1ull;
+              const int at = 20 * k + (lo - a) + 1;
+              sb |= ((mneg >> (lo - w0)) & run) << at;
+              nz |= ((mnz >> (lo - w0)) & run) << at;
+            }
+          }
+        }
+#ifndef ART_NO_SAMPLER_PRIO
+        __builtin_amdgcn_s_setprio(1);
+#endif
+        wave_lds_sync();
+      }
+      ART_QMARK(3)
+      if (active) {
+        // certified steps: points 1..19 nonzero and of the certified sign
+        const unsigned long long p19 = 0xFFFFEull;
+        for (int k = 0; k < kmax; ++k) {
+          if ((cneg >> k) & 1u) { sb |= p19 << (20 * k); nz |= p19 << (20 * k); }
+          else if ((cpos >> k) & 1u) nz |= p19 << (20 * k);
+        }
+        // bit 0 of each step: the point before it (c_prev, then the previous step's point 19)
+        sb |= signbit(c_prev) ? 1ull : 0ull;
+        nz |= (c_prev != 0.0) ? 1ull : 0ull;
+        for (int k = 1; k < kmax; ++k) {
+          sb |= ((sb >> (20 * k - 1)) & 1ull) << (20 * k);
+          nz |= ((nz >> (20 * k - 1)) & 1ull) << (20 * k);
+        }
+        const int kl = kmax - 1;  // the value the next block's first bracket starts from (read for its sign)
+        if ((unc >> kl) & 1u) c_prev = slast[threadIdx.x];
+        else if ((cneg >> kl) & 1u) c_prev = -1.0;
+        else if ((cpos >> kl) & 1u) c_prev = 1.0;
+      }
+      // queue the sign changes in (point j-1, point j] of each step (signbits differ, both nonzero),
+      // step by step, so each lane's brackets stay in their order along the line
+#ifdef ART_SAMPLER_KLOOP1
+      #pragma unroll 1
+#endif
+      for (int k = 0; k < kmax; ++k) {
+        const int st = st0 + k;
+        const double s0 = st * 0.5;
+        const double s1 = fmin(s0 + 0.5, send);
+        const unsigned sbk = (unsigned)(sb >> (20 * k)) & 0xFFFFFu, nzk = (unsigned)(nz >> (20 * k)) & 0xFFFFFu;
+        unsigned br = active ? (sbk ^ (sbk << 1)) & nzk & (nzk << 1) & (((1u << np) - 1u) & ~1u) : 0u;
+        unsigned long long bm = __ballot(br != 0u);
+        if (bm == 0ull) continue;
+        // the previous step's last grid point, where a bracket at point 1 opens
+        const double ps0 = (st - 1) * 0.5;
+        const double pds = fmin(ps0 + 0.5, send) - ps0;
+        const double s_start = st == 0 ? 0.0 : ps0 + (pds == 0.5 ? sgrid[nper] : pds * double(nper) / double(np - 1));
+        while (bm != 0ull) {
+          if (qn + 64 > SQCAP) flush();
+          if (br != 0u) {
+            const int ip = __builtin_ctz(br);
+            const int slot = qn + __popcll(bm & lt);
+            sqa[wq + slot] = (ip == 1) ? s_start : s0 + (s1 - s0) * double(ip - 1) / double(np - 1);
+            sqb[wq + slot] = s0 + (s1 - s0) * double(ip) / double(np - 1);
+            sqsrc[wq + slot] = (unsigned char)lane;
+            br &= br - 1u;
+          }
+          qn += __popcll(bm);
+          bm = __ballot(br != 0u);
+        }
+      }
+      ART_QMARK(4)
+    }
+    } else {  // step by step (round 4)
     for (int st = 0; st < nsteps; ++st) {
 #ifdef ART_SAMPLER_SECTIONS
       q_sec[7] += 1;
@@ -2945,6 +3181,7 @@ __global__ __launch_bounds__(256, WPS) void sample_kernel(const KParams P, const
         bm = __ballot(br != 0u);
       }
       ART_QMARK(4)
+    }
     }
     if (qn > 0) flush();
     ART_QMARK(4)
@@ -3393,22 +3630,22 @@ hipError_t launch_helpers(const KParams& P, int64_t n, const SegIn& in, const Se
 hipError_t launch_sample(const KParams& P, double maxR, uint64_t seed, int64_t ray_offset, int64_t n, double* x,
                          double* k, double* erg, double* vifty, int32_t* w, int32_t* att, unsigned long long* queue,
                          hipStream_t s) {
-  // lines of up to 2.2 x 60 km (264 steps): the 3-wave build; longer ones: 2 waves
-  // (ART_SAMPLER_WPS=2|3|4 forces one, for A/B runs; 4 spills ~200 VGPRs)
+  // lines of up to 2.2 x 60 km (264 steps): the 3-wave build, step by step (blocks of steps: no
+  // faster there, 118 vs 119 ms per 1e7 flat samples); longer lines, mostly certified far from the
+  // conversion surface: 2 waves, blocks of 3 steps (the scan's largest-maxR point 55 -> 43 ms,
+  // profiles/r05h_ab_sampler.txt). ART_SAMPLER_WPS=2|3 and ART_SAMPLER_BLOCKS=0|1 force a build (A/B)
   int wps = maxR <= 60.0 ? 3 : 2;
+  bool blocks = maxR > 60.0;
   if (const char* e = std::getenv("ART_SAMPLER_WPS"))
-    if (e[0] == '2' || e[0] == '3' || e[0] == '4') wps = e[0] - '0';
-  const void* fn = wps == 4 ? (const void*)sample_kernel<4> : wps == 3 ? (const void*)sample_kernel<3> : (const void*)sample_kernel<2>;
-  const int grid = persistent_blocks(fn, n, 256, 1);
-  if (wps == 4)
-    hipLaunchKernelGGL(sample_kernel<4>, dim3(grid), dim3(256), 0, s, P, maxR, seed, ray_offset, n, x, k, erg, vifty, w,
-                       att, queue);
-  else if (wps == 3)
-    hipLaunchKernelGGL(sample_kernel<3>, dim3(grid), dim3(256), 0, s, P, maxR, seed, ray_offset, n, x, k, erg, vifty, w,
-                       att, queue);
-  else
-    hipLaunchKernelGGL(sample_kernel<2>, dim3(grid), dim3(256), 0, s, P, maxR, seed, ray_offset, n, x, k, erg, vifty, w,
-                       att, queue);
+    if (e[0] == '2' || e[0] == '3') wps = e[0] - '0';
+  if (const char* e = std::getenv("ART_SAMPLER_BLOCKS"))
+    if (e[0] == '0' || e[0] == '1') blocks = e[0] == '1';
+  using SFn = void (*)(const KParams, const double, const uint64_t, const int64_t, const int64_t, double*, double*,
+                       double*, double*, int32_t*, int32_t*, unsigned long long*);
+  const SFn fn = wps == 3 ? (blocks ? sample_kernel<3, true> : sample_kernel<3, false>)
+                          : (blocks ? sample_kernel<2, true> : sample_kernel<2, false>);
+  const int grid = persistent_blocks((const void*)fn, n, 256, 1);
+  hipLaunchKernelGGL(fn, dim3(grid), dim3(256), 0, s, P, maxR, seed, ray_offset, n, x, k, erg, vifty, w, att, queue);
   return hipGetLastError();
 }
 

@@ -60,6 +60,23 @@ run_step() {
       done; unset ART_LIB ;;
     shard_trace)  # 1.25e6 rays, one call at a time, traced
       ART_HOST_TRACE=1 timeout -k 10 300 python3 -u bench.py --rays 1250000 --steps 10 --warmup 2 --no-cpu-baseline --no-device --inflight 1 > ${O}_bench_1250000_if1_trace.json 2> ${O}_shard_if1_trace.err ;;
+    pytest_sampler)
+      timeout -k 10 600 python3 -u -m pytest tests/test_gpu_sampler_prob.py tests/test_gpu_scan_cert.py -m gpu -v --timeout 300 --timeout-method thread > ${O}_pytest_sampler.log 2>&1 ;;
+    ab_sampler)  # block-certified sampler (this build, 3 and 2 waves/SIMD) vs the step-by-step one, interleaved
+      for r in 1 2; do
+        timeout -k 10 300 python3 -u tools/exp_sampler_time.py > ${O}_sab_block3_r$r.jsonl 2>> ${O}_ab_sampler.err &&
+        ART_SAMPLER_WPS=2 timeout -k 10 300 python3 -u tools/exp_sampler_time.py > ${O}_sab_block2_r$r.jsonl 2>> ${O}_ab_sampler.err &&
+        ART_LIB=tools/build/libart_stepwise.so timeout -k 10 300 python3 -u tools/exp_sampler_time.py > ${O}_sab_step_r$r.jsonl 2>> ${O}_ab_sampler.err || return 1
+      done ;;
+    sec_sampler)  # sampler section split: blocks of 3, of 2, step by step; and the KB=2 build's time
+      for v in ssec ssec_kb2 ssec_step; do
+        ART_LIB=tools/build/libart_$v.so timeout -k 10 300 python3 -u tools/exp_sampler_time.py > ${O}_sec_$v.jsonl 2> ${O}_sec_$v.err || return 1
+      done &&
+      ART_LIB=tools/build/libart_kb2.so timeout -k 10 300 python3 -u tools/exp_sampler_time.py > ${O}_sab_kb2.jsonl 2>> ${O}_ab_sampler.err ;;
+    scan)  # configs[4]: the 32-point scan, 1e6 rays a point, 8 streams
+      timeout -k 10 300 python3 -u tools/exp_scan_streams.py 1000000 8 32 16 > ${O}_param_scan_1e6_8streams.jsonl 2> ${O}_scan.err ;;
+    scan_step)  # the same with the step-by-step sampler everywhere
+      ART_SAMPLER_BLOCKS=0 timeout -k 10 300 python3 -u tools/exp_scan_streams.py 1000000 8 32 16 > ${O}_param_scan_1e6_8streams_step.jsonl 2> ${O}_scan_step.err ;;
     pytest_edges)
       timeout -k 10 400 python3 -u -m pytest tests/test_edges.py -m gpu -v --timeout 300 --timeout-method thread > ${O}_pytest_edges.log 2>&1 ;;
     smoke)
