@@ -77,6 +77,20 @@ run_step() {
       timeout -k 10 300 python3 -u tools/exp_scan_streams.py 1000000 8 32 16 > ${O}_param_scan_1e6_8streams.jsonl 2> ${O}_scan.err ;;
     scan_step)  # the same with the step-by-step sampler everywhere
       ART_SAMPLER_BLOCKS=0 timeout -k 10 300 python3 -u tools/exp_scan_streams.py 1000000 8 32 16 > ${O}_param_scan_1e6_8streams_step.jsonl 2> ${O}_scan_step.err ;;
+    ab_hprio)  # helper waves at issue priority 2 (dev build) vs this build; and a first init pass of 65536 rays
+      for r in 1 2; do
+        for lib in base hp; do
+          if [ $lib = hp ]; then export ART_LIB=tools/build/libart_hprio.so; else unset ART_LIB; fi
+          timeout -k 10 300 python3 -u bench.py --rays 1250000 --no-cpu-baseline --no-device --steps 10 --warmup 2 --inflight 1 > ${O}_ahp_1250000_${lib}_r$r.json 2>> ${O}_ab_hprio.err &&
+          ART_HOST_INIT_RAYS=65536 timeout -k 10 300 python3 -u bench.py --rays 1250000 --no-cpu-baseline --no-device --steps 10 --warmup 2 --inflight 1 > ${O}_ahp_1250000_init64k_${lib}_r$r.json 2>> ${O}_ab_hprio.err &&
+          timeout -k 10 300 python3 -u bench.py --no-cpu-baseline --no-device --steps 10 --warmup 2 > ${O}_ahp_1e7_${lib}_r$r.json 2>> ${O}_ab_hprio.err || { unset ART_LIB; return 1; }
+        done
+      done; unset ART_LIB ;;
+    ab_scan)  # the scan: default sampler choice vs blocks of steps for every line, interleaved
+      for r in 1 2; do
+        timeout -k 10 300 python3 -u tools/exp_scan_streams.py 1000000 8 32 16 > ${O}_scan_default_r$r.jsonl 2>> ${O}_ab_scan.err &&
+        ART_SAMPLER_BLOCKS=1 timeout -k 10 300 python3 -u tools/exp_scan_streams.py 1000000 8 32 16 > ${O}_scan_blocks_r$r.jsonl 2>> ${O}_ab_scan.err || return 1
+      done ;;
     pytest_edges)
       timeout -k 10 400 python3 -u -m pytest tests/test_edges.py -m gpu -v --timeout 300 --timeout-method thread > ${O}_pytest_edges.log 2>&1 ;;
     smoke)
