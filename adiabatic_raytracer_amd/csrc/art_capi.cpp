@@ -1318,7 +1318,7 @@ int propagate_host_maskless(DeviceCtx* c, HostLane* H, bool overlap, const art_p
     for (int u = 0; u < nu && !stop.load(); ++u) {
       while (recorded.load(std::memory_order_acquire) <= u && !stop.load()) std::this_thread::sleep_for(std::chrono::microseconds(5));
       if (stop.load()) break;
-      hipError_t q;  // polled: a blocking event wait woke up to 2 ms late (profiles/r05e_shard_if1_trace.err)
+      hipError_t q;  // (polled every 5 us, as the piece flags are)
       while ((q = hipEventQuery(ev_up[u])) == hipErrorNotReady && !stop.load())
         std::this_thread::sleep_for(std::chrono::microseconds(5));
       if (stop.load()) break;

@@ -2364,9 +2364,6 @@ __global__ __launch_bounds__(256) void helper_kernel(const KParams P, const int6
   __shared__ double hfl[2 * FLUX_HELPER_BINS];  // (HK_TILES with SegOut::flux_hist) this block's flux counts
   __shared__ int last_out, complete;
   const int tid = threadIdx.x;
-#ifdef ART_HELPER_PRIO
-  if (mode == HK_TILES) __builtin_amdgcn_s_setprio(ART_HELPER_PRIO);  // (dev A/B) above the integrator's bulk waves
-#endif
   const bool flb = mode == HK_TILES && out.flux_hist != nullptr;
   if (flb)
     for (int b = tid; b < 2 * out.flux_nbins; b += 256) hfl[b] = 0.0;

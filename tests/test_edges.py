@@ -296,15 +296,17 @@ EXTRA = {"layer": dict(theta_m=0.2, mass_a=1e-5, flat=True, bndry_lyr=1.0),
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("cfg,species,cap,shift", [("flat", 1, 1, 11), ("flat", 0, 3, 12), ("gr", 1, 2, 11),
-                                                    ("layer", 1, 1, 11), ("isotropic", 1, 1, 12)])
-def test_streamed_host_pipeline_is_bit_exact(cfg, species, cap, shift, monkeypatch):
+@pytest.mark.parametrize("cfg,species,cap,shift,direct", [("flat", 1, 1, 11, 0), ("flat", 0, 3, 12, 0), ("gr", 1, 2, 11, 0),
+                                                           ("layer", 1, 1, 11, 0), ("isotropic", 1, 1, 12, 0),
+                                                           ("flat", 0, 3, 12, 1), ("gr", 1, 2, 11, 1)])
+def test_streamed_host_pipeline_is_bit_exact(cfg, species, cap, shift, direct, monkeypatch):
     """art_propagate_host's default for large batches is the streamed pipeline: one integrator
     launch over the whole batch while pieces of its inputs are still being uploaded and
     initialised (a wave waits for its rays' fresh state), each piece finalized and downloaded
     once its last ray is done (a signal the download stream waits on). With pieces of 2^11 or
     2^12 rays (10 or 5 of them) it returns exactly the single launch's outputs, every crossing
-    slot included, and the same statistics."""
+    slot included, and the same statistics. `direct`: the pieces' output blobs in pinned host
+    memory, written by the helpers over PCIe (ART_HOST_DIRECT=1, no download copies)."""
     from dataclasses import replace
     import adiabatic_raytracer_amd as A
     p = A.Params(**(CONFIGS[cfg] if cfg in CONFIGS else EXTRA[cfg]))
@@ -317,6 +319,7 @@ def test_streamed_host_pipeline_is_bit_exact(cfg, species, cap, shift, monkeypat
     monkeypatch.setenv("ART_HOST_MODE", "stream")
     monkeypatch.setenv("ART_HOST_PIECE_SHIFT", str(shift))
     monkeypatch.setenv("ART_HOST_CHUNK_MIN", "1000")
+    monkeypatch.setenv("ART_HOST_DIRECT", str(direct))
     A.raytracer.host_path_counters(reset=True)
     for _ in range(2):  # the second call reuses the streams, signals and staging
         got = A.propagate_batch(q, *args, max_crossings=mc, capacity=cap, flux_nbins=50)

@@ -1,10 +1,12 @@
 #!/bin/bash
 # Round-end evidence for profiles/: the GPU test suite, smoke, the PMC passes of this library
-# build (so bench.py reports roofline.traffic), the default bench line (the host path), a
-# rocprofv3 kernel-trace summary of the same command, configs[3] as one GR batch, and the scan /
-# sampler / tail-ray / host-path / small-batch / event / section side figures.
-# Usage: TAG=r04f bash tools/gpu_final.sh   (writes gpurun_out/TAG_*; stops at the first failure)
-TAG=${TAG:-r04final}
+# build (so bench.py reports roofline.traffic), the default bench line (the host path, with its
+# in-kernel span stamps), a rocprofv3 kernel-trace summary of the same command (and one with the
+# memory-copy trace: the download copies as blit kernels), the 8-GPU shard size on one GPU,
+# configs[3] as one GR batch with its PMC set, and the scan / sampler / tail-ray / host-path /
+# small-batch / event / section side figures.
+# Usage: TAG=r05final bash tools/gpu_final.sh   (writes gpurun_out/TAG_*; stops at the first failure)
+TAG=${TAG:-r05final}
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
@@ -21,8 +23,15 @@ step bench
 timeout -k 10 600 python3 -u bench.py > gpurun_out/${TAG}_bench_flat1e7.json 2> gpurun_out/${TAG}_bench.err || exit 1
 step rocprof
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_prof -o prof --output-format csv -- python3 bench.py --steps 5 --no-cpu-baseline > gpurun_out/${TAG}_bench_prof.json 2>&1 || exit 1
+step rocprof_copies
+timeout -k 10 600 rocprofv3 --kernel-trace --memory-copy-trace --stats -d gpurun_out/${TAG}_profmc -o prof --output-format csv -- python3 bench.py --steps 5 --no-cpu-baseline --no-device > gpurun_out/${TAG}_bench_profmc.json 2> gpurun_out/${TAG}_profmc.err || exit 1
+step shard
+timeout -k 10 300 python3 -u bench.py --rays 1250000 --steps 20 --warmup 5 --no-cpu-baseline > gpurun_out/${TAG}_bench_1250000.json 2> gpurun_out/${TAG}_shard.err || exit 1
+timeout -k 10 300 python3 -u bench.py --rays 1250000 --steps 20 --warmup 5 --no-cpu-baseline --no-device --inflight 1 > gpurun_out/${TAG}_bench_1250000_inflight1.json 2>> gpurun_out/${TAG}_shard.err || exit 1
 step gr
 timeout -k 10 600 python3 -u bench.py --config gr --rays 1000000 --steps 5 --no-cpu-baseline > gpurun_out/${TAG}_bench_gr1e6.json 2> gpurun_out/${TAG}_gr.err || exit 1
+step pmc_gr
+bash tools/pmc_gr.sh gpurun_out/${TAG}_pmc_gr > gpurun_out/${TAG}_pmc_gr.log 2>&1 || exit 1
 step scan
 timeout -k 10 300 python3 -u tools/exp_scan_streams.py 1000000 8 32 16 > gpurun_out/${TAG}_param_scan_1e6_8streams.jsonl 2> gpurun_out/${TAG}_scan.err || exit 1
 step sampler

@@ -91,6 +91,18 @@ run_step() {
         timeout -k 10 300 python3 -u tools/exp_scan_streams.py 1000000 8 32 16 > ${O}_scan_default_r$r.jsonl 2>> ${O}_ab_scan.err &&
         ART_SAMPLER_BLOCKS=1 timeout -k 10 300 python3 -u tools/exp_scan_streams.py 1000000 8 32 16 > ${O}_scan_blocks_r$r.jsonl 2>> ${O}_ab_scan.err || return 1
       done ;;
+    sweep_init)  # the first init pass's size (ART_HOST_INIT_RAYS; default 2 rays per integrator lane = 258048)
+      for r in 1 2; do
+        for ir in 32768 65536 131072 258048; do
+          ART_HOST_INIT_RAYS=$ir timeout -k 10 300 python3 -u bench.py --rays 1250000 --no-cpu-baseline --no-device --steps 10 --warmup 2 --inflight 1 > ${O}_si_1250000_if1_${ir}_r$r.json 2>> ${O}_sweep_init.err &&
+          ART_HOST_INIT_RAYS=$ir timeout -k 10 300 python3 -u bench.py --rays 1250000 --no-cpu-baseline --no-device --steps 10 --warmup 2 --inflight 2 > ${O}_si_1250000_if2_${ir}_r$r.json 2>> ${O}_sweep_init.err &&
+          ART_HOST_INIT_RAYS=$ir timeout -k 10 300 python3 -u bench.py --no-cpu-baseline --no-device --steps 10 --warmup 2 > ${O}_si_1e7_${ir}_r$r.json 2>> ${O}_sweep_init.err || return 1
+        done
+      done ;;
+    fetch_n)  # device-resident launch: FETCH_SIZE per ray at 1e6, 2.5e6 and 1e7 rays (do the init records' re-reads hit the 256 MiB Infinity Cache?)
+      for n in 1000000 2500000 10000000; do
+        timeout -s KILL 200 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d ${O}_fetchn/n$n -o p --output-format csv -- python3 tools/exp_sections.py $n > ${O}_fetchn_$n.log 2>&1 || return 1
+      done ;;
     pytest_edges)
       timeout -k 10 400 python3 -u -m pytest tests/test_edges.py -m gpu -v --timeout 300 --timeout-method thread > ${O}_pytest_edges.log 2>&1 ;;
     smoke)
