@@ -1268,12 +1268,14 @@ int propagate_host_maskless(DeviceCtx* c, HostLane* H, bool overlap, const art_p
     std::lock_guard<std::mutex> rlk(g_ring_mu);
     int r = take_slot(c, &L);
     if (r) return r;
-    // every block slot initialises two rays per integrator lane before the integrator starts (258k
-    // rays; the first unit alone left the integrator's first waves waiting on 8 helpers: 33 ms
-    // against 18 per 1.25e6-ray call), then the helpers keep ahead (ART_HOST_INIT_RAYS: tests and
-    // A/B, another amount)
+    // every block slot initialises the first upload unit's rays before the integrator starts, then
+    // the helpers keep ahead. (Round 4 took 258k rays, two per integrator lane: the first unit alone
+    // left the integrator waiting on 8 helpers, 33 ms against 18 per 1.25e6-ray call. With the
+    // units gathered from the call's start, the helpers keep up, and the first unit alone starts
+    // the integrator ~1 ms sooner: 1.25e6 rays 17.2 -> 16.2 ms, 1e7 95.3 -> 94.1 ms, two boxes,
+    // profiles/r05l_init_pass_sweep.txt. ART_HOST_INIT_RAYS: tests and A/B, another amount)
     const int64_t first =
-        serial ? n : std::min(n, (int64_t)std::max(1, env_int("ART_HOST_INIT_RAYS", (slots - helpers) * 4 * 64 * 2)));
+        serial ? n : std::min(n, (int64_t)std::max(1, env_int("ART_HOST_INIT_RAYS", (int)(ulo[1] - ulo[0]))));
     if (env_int("ART_HOST_INITPASS", 1))  // (dev: 0 leaves the first piece to the helpers)
       HIP_OK(art::launch_helpers(K, n, in, so, iblocks, first, 0, words + 1, H->m_comp));
     HIP_OK(hipEventRecord(L->ev0, H->m_comp));
