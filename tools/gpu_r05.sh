@@ -1,5 +1,8 @@
 #!/bin/bash
 # Round-5 GPU session steps. Usage: TAG=r05a bash tools/gpu_r05.sh STEP [STEP ...]
+# (Dev session log of round 5. Variant libraries named by the steps are built with
+# `python adiabatic_raytracer_amd/build.py --variant tools/build/libart_X.so -DSWITCH`; the steps whose
+# switch was removed after its A/B are kept as the record of how the r05* profiles were made.)
 # Every GPU step runs under its own time limit; the first failure ends the session.
 TAG=${TAG:-r05}
 set -o pipefail
