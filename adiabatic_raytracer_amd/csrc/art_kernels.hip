@@ -2598,13 +2598,8 @@ __device__ inline double line_rmin2(const double* x0, const double* va, double s
 // point of it provably has a negative condition, 2 when every point provably has a positive one,
 // 0 otherwise. The bounds are derived at sample_kernel's step loop; both hold for a segment of any
 // length (a block of steps as well as one step) and whatever the sign of the point before it.
-#ifdef ART_SEGCERT_NOINLINE
-#define ART_SEGCERT_ATTR __attribute__((noinline))
-#else
-#define ART_SEGCERT_ATTR inline
-#endif
-__device__ ART_SEGCERT_ATTR int seg_cert(const KParams& P, const double* X0, const double* VA, double E, double s0,
-                                         double s1, double cert_lhs, double cert_rhs) {
+__device__ inline int seg_cert(const KParams& P, const double* X0, const double* VA, double E, double s0, double s1,
+                               double cert_lhs, double cert_rhs) {
   const double rm2 = line_rmin2(X0, VA, s0, s1);
   const double rmin = sqrt(rm2);
   double xa[3], xb[3];
@@ -2650,6 +2645,7 @@ __global__ __launch_bounds__(256, WPS) void sample_kernel(const KParams P, const
   __shared__ unsigned char sqsrc[4 * SQCAP], sqok[4 * SQCAP];
   __shared__ double sgrid[32];  // (0.5 j)/19: a full step's grid offsets, the same rounding as the division
   __shared__ unsigned char spair[4 * 64 * 3];  // a wave's (lane, step of the block) pairs to scan: lane << 2 | step
+  __shared__ unsigned sbm[256];  // (step-by-step scan) a lane's sign changes of the step not queued yet
   const int lane = threadIdx.x & 63;
   const int wb = threadIdx.x & ~63;
   const int wq = (threadIdx.x >> 6) * SQCAP;
@@ -2836,12 +2832,10 @@ __global__ __launch_bounds__(256, WPS) void sample_kernel(const KParams P, const
     // so a block or step is certified whatever c_prev is, and a sign change at its first point is
     // found by the same bit logic as an evaluated one. The evaluated points and their arithmetic
     // are those of the step-by-step scan (ART_SAMPLER_STEPWISE), so the samples do not change.
-#ifndef ART_SAMPLER_KB
-    constexpr int KB = 3;  // (the step masks of a block share 64-bit words: at most 3 steps)
-#else
-    constexpr int KB = ART_SAMPLER_KB;  // (dev A/B: 1 or 2)
-#endif
-    const int wp = (threadIdx.x >> 6) * 64 * 3;  // this wave's pair list in spair
+    // (the step masks of a block share 64-bit words: at most 3 steps; blocks of 2 measured slower,
+    // 128 vs 119 ms per 1e7 flat samples, profiles/r05h_ab_sampler.txt)
+    constexpr int KB = 3;
+    const int wp = (threadIdx.x >> 6) * 64 * KB;  // this wave's pair list in spair
     for (int st0 = 0; st0 < nsteps; st0 += KB) {
 #ifdef ART_SAMPLER_SECTIONS
       q_sec[7] += 1;
@@ -2993,9 +2987,6 @@ __global__ __launch_bounds__(256, WPS) void sample_kernel(const KParams P, const
       }
       // queue the sign changes in (point j-1, point j] of each step (signbits differ, both nonzero),
       // step by step, so each lane's brackets stay in their order along the line
-#ifdef ART_SAMPLER_KLOOP1
-      #pragma unroll 1
-#endif
       for (int k = 0; k < kmax; ++k) {
         const int st = st0 + k;
         const double s0 = st * 0.5;
@@ -3025,12 +3016,22 @@ __global__ __launch_bounds__(256, WPS) void sample_kernel(const KParams P, const
       ART_QMARK(4)
     }
     } else {  // step by step (round 4)
-    for (int st = 0; st < nsteps; ++st) {
+    // The bracket queue is resolved (flush: Illinois with its three inlined conditions) at the top
+    // of this loop and after it, not inside the insertion below: a queue that fills up there ends
+    // the pass, the rest wait in sbm, and the loop comes back to the same step after resolving it.
+    // Inside the insertion the flush's registers stacked on the step's live state: 71 spilled VGPRs
+    // in the 3-wave build, 51 now; 10^7 flat samples 118 -> 115 ms, bit-identical
+    // (profiles/r05q_ab_sampler_flush.txt). (The block scan, 2 waves/SIMD, does not spill.)
+    bool sres = false;  // (wave-uniform) this step's brackets wait behind a full queue
+    for (int st = 0; st < nsteps;) {
+      const double s0 = st * 0.5;
+      const double s1 = fmin(s0 + 0.5, send);
+      if (sres) {
+        flush();
+      } else {
 #ifdef ART_SAMPLER_SECTIONS
       q_sec[7] += 1;
 #endif
-      const double s0 = st * 0.5;
-      const double s1 = fmin(s0 + 0.5, send);
       const bool quiet = !active || (cert_ok && c_prev < 0.0 && (s1 < w_in || s0 > w_out));
       if (__ballot(!quiet) == 0ull) {
         // every lane is certified outside its window: jump to one step before the earliest
@@ -3038,7 +3039,7 @@ __global__ __launch_bounds__(256, WPS) void sample_kernel(const KParams P, const
         int nxt = (active && s1 < w_in && w_in < send) ? (int)floor(w_in * 2.0) - 1 : nsteps;
 #pragma unroll
         for (int o = 32; o >= 1; o >>= 1) nxt = min(nxt, __shfl_xor(nxt, o));
-        if (nxt > st + 1) st = nxt - 1;
+        st = nxt > st + 1 ? nxt : st + 1;
         continue;
       }
       // Certified-negative step: with the axion shell imposed (w normalised), the condition
@@ -3096,7 +3097,10 @@ __global__ __launch_bounds__(256, WPS) void sample_kernel(const KParams P, const
       const unsigned long long mU = __ballot(unc);
       const int nU = __popcll(mU);
       ART_QMARK(2)
-      if (nU == 0) continue;  // all certified: no point, no bracket, c_prev unchanged
+      if (nU == 0) {  // all certified: no point, no bracket, c_prev unchanged
+        ++st;
+        continue;
+      }
 #ifdef ART_SAMPLER_SECTIONS
       q_sec[6] += 1;
 #endif
@@ -3161,14 +3165,26 @@ __global__ __launch_bounds__(256, WPS) void sample_kernel(const KParams P, const
         c_prev = slast[threadIdx.x];
       }
       ART_QMARK(3)
+      if (__ballot(br != 0u) == 0ull) {
+        ++st;
+        continue;
+      }
+      sbm[threadIdx.x] = br;
+      }
       // the previous step's last grid point, where a bracket at point 1 opens
       const double ps0 = (st - 1) * 0.5;
       const double pds = fmin(ps0 + 0.5, send) - ps0;
       const double s_start = st == 0 ? 0.0 : ps0 + (pds == 0.5 ? sgrid[nper] : pds * double(nper) / double(np - 1));
       // queue the brackets, each lane's in its order along the line
+      unsigned br = sbm[threadIdx.x];
       unsigned long long bm = __ballot(br != 0u);
+      sres = false;
       while (bm != 0ull) {
-        if (qn + 64 > SQCAP) flush();
+        if (qn + 64 > SQCAP) {  // (the rest wait in sbm; the loop's top resolves the queue)
+          sres = true;
+          sbm[threadIdx.x] = br;
+          break;
+        }
         if (br != 0u) {
           const int ip = __builtin_ctz(br);
           const int slot = qn + __popcll(bm & lt);
@@ -3181,6 +3197,7 @@ __global__ __launch_bounds__(256, WPS) void sample_kernel(const KParams P, const
         bm = __ballot(br != 0u);
       }
       ART_QMARK(4)
+      if (!sres) ++st;
     }
     }
     if (qn > 0) flush();

@@ -106,6 +106,31 @@ run_step() {
       for n in 1000000 2500000 10000000; do
         timeout -s KILL 200 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d ${O}_fetchn/n$n -o p --output-format csv -- python3 tools/exp_sections.py $n > ${O}_fetchn_$n.log 2>&1 || return 1
       done ;;
+    ab_if_1e7)  # the 1e7 headline: one call at a time vs two in flight, interleaved
+      for r in 1 2; do
+        for f in 1 2; do
+          timeout -k 10 300 python3 -u bench.py --no-cpu-baseline --no-device --steps 10 --warmup 2 --inflight $f > ${O}_if_1e7_${f}_r$r.json 2>> ${O}_ab_if.err || return 1
+        done
+      done ;;
+    ab_sblocks)  # sampler: the default choice (step by step below maxR 60 km) vs blocks for every line, interleaved; and the section split of blocks
+      for r in 1 2; do
+        timeout -k 10 300 python3 -u tools/exp_sampler_time.py > ${O}_sb_default_r$r.jsonl 2>> ${O}_ab_sblocks.err &&
+        ART_SAMPLER_BLOCKS=1 timeout -k 10 300 python3 -u tools/exp_sampler_time.py > ${O}_sb_blocks_r$r.jsonl 2>> ${O}_ab_sblocks.err || return 1
+      done &&
+      ART_SAMPLER_BLOCKS=1 ART_LIB=tools/build/libart_ssec.so timeout -k 10 300 python3 -u tools/exp_sampler_time.py > ${O}_sec_blocks.jsonl 2> ${O}_sec_blocks.err ;;
+    ab_sfin)  # sampler: this build vs the round-5 final library (tools/build/libart_fin.so), interleaved; and blocks forced for every line
+      for r in 1 2; do
+        timeout -k 10 300 python3 -u tools/exp_sampler_time.py > ${O}_sf_new_r$r.jsonl 2>> ${O}_ab_sfin.err &&
+        ART_LIB=tools/build/libart_fin.so timeout -k 10 300 python3 -u tools/exp_sampler_time.py > ${O}_sf_fin_r$r.jsonl 2>> ${O}_ab_sfin.err &&
+        ART_SAMPLER_BLOCKS=1 timeout -k 10 300 python3 -u tools/exp_sampler_time.py > ${O}_sf_newblocks_r$r.jsonl 2>> ${O}_ab_sfin.err || return 1
+      done ;;
+    ab_sill)  # sampler: this build vs the 3-site Illinois variant vs the round-5 final library, interleaved
+      for r in 1 2; do
+        for lib in base ill3 fin; do
+          if [ $lib = base ]; then unset ART_LIB; else export ART_LIB=tools/build/libart_$lib.so; fi
+          timeout -k 10 300 python3 -u tools/exp_sampler_time.py > ${O}_si_${lib}_r$r.jsonl 2>> ${O}_ab_sill.err || { unset ART_LIB; return 1; }
+        done
+      done; unset ART_LIB ;;
     pytest_edges)
       timeout -k 10 400 python3 -u -m pytest tests/test_edges.py -m gpu -v --timeout 300 --timeout-method thread > ${O}_pytest_edges.log 2>&1 ;;
     smoke)
