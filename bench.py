@@ -97,6 +97,42 @@ def host_cores():
     return n
 
 
+def bind_to_gpu_node(device):
+    """Binds this rank (its main thread, and every thread it starts later: libart's copy pool,
+    gatherers, lane workers) to the CPUs of the NUMA node its GPU hangs off, so the pageable host
+    arrays and the pinned staging are first touched there; the host path measured up to 3.9 ms
+    slower per 1e7-ray call from the far node (profiles/r05r_numa_binding.txt). Returns the node,
+    or None when sysfs does not tell (nothing is changed then). ART_BENCH_NO_NUMA=1: no binding."""
+    if os.environ.get("ART_BENCH_NO_NUMA"):
+        return None
+    import glob
+    import torch
+    try:
+        bus = int(torch.cuda.get_device_properties(device).pci_bus_id)
+        for d in glob.glob("/sys/bus/pci/devices/*"):
+            parts = os.path.basename(d).split(":")
+            if len(parts) != 3 or int(parts[1], 16) != bus:
+                continue
+            cls = open(os.path.join(d, "class")).read().strip()
+            if not (cls.startswith("0x03") or cls.startswith("0x12")):  # display / processing accelerator
+                continue
+            node = int(open(os.path.join(d, "numa_node")).read().strip())
+            if node < 0:
+                return None
+            cpus = set()
+            for part in open(f"/sys/devices/system/node/node{node}/cpulist").read().strip().split(","):
+                lo, _, hi = part.partition("-")
+                cpus.update(range(int(lo), int(hi or lo) + 1))
+            cpus &= os.sched_getaffinity(0)
+            if not cpus:
+                return None
+            os.sched_setaffinity(0, cpus)
+            return node
+    except (OSError, ValueError, AttributeError):
+        return None
+    return None
+
+
 def host_arrays(inp, n):
     """This rank's batch as a Julia caller holds it (MainRunner.jl:179-190 hands host arrays
     to propagate): pageable numpy inputs, and output arrays allocated and faulted in once."""
@@ -188,6 +224,7 @@ def main():
         local = int(os.environ["ART_BENCH_DEVICE"])
     backend = os.environ.get("ART_BENCH_BACKEND", "nccl")
     torch.cuda.set_device(local)
+    numa_node = bind_to_gpu_node(local)
     if world > 1:
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -377,7 +414,7 @@ def main():
                        "m_a_eV": params.mass_a, "theta_m": params.theta_m, "omega_pul": params.omega_pul,
                        "B0_G": params.B0, "rNS_km": params.rNS, "abstol": params.abstol, "reltol": params.reltol,
                        "interp_points": params.interp_points, "parallelism": f"rays sharded x{world}",
-                       "host_calls_in_flight": args.inflight,
+                       "host_calls_in_flight": args.inflight, "host_numa_node": numa_node,
                        "host_path": ("streamed pipeline" if streamed else
                                      "single launch" if cnt["single"] == args.steps else str(cnt)),
                        "host_path_counters": cnt, "host_path_counters_warmup": cnt_w},

@@ -131,6 +131,14 @@ run_step() {
           timeout -k 10 300 python3 -u tools/exp_sampler_time.py > ${O}_si_${lib}_r$r.jsonl 2>> ${O}_ab_sill.err || { unset ART_LIB; return 1; }
         done
       done; unset ART_LIB ;;
+    ab_numa)  # bench bound to the GPU's NUMA node (default) vs unbound (ART_BENCH_NO_NUMA=1), interleaved
+      for r in 1 2 3; do
+        for b in bound unbound; do
+          if [ $b = unbound ]; then export ART_BENCH_NO_NUMA=1; else unset ART_BENCH_NO_NUMA; fi
+          timeout -k 10 300 python3 -u bench.py --no-cpu-baseline --no-device --steps 10 --warmup 2 > ${O}_an_1e7_${b}_r$r.json 2>> ${O}_ab_numa.err &&
+          timeout -k 10 300 python3 -u bench.py --rays 1250000 --no-cpu-baseline --no-device --steps 10 --warmup 2 > ${O}_an_1250000_${b}_r$r.json 2>> ${O}_ab_numa.err || { unset ART_BENCH_NO_NUMA; return 1; }
+        done
+      done; unset ART_BENCH_NO_NUMA ;;
     pytest_edges)
       timeout -k 10 400 python3 -u -m pytest tests/test_edges.py -m gpu -v --timeout 300 --timeout-method thread > ${O}_pytest_edges.log 2>&1 ;;
     smoke)
