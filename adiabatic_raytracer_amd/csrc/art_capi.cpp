@@ -112,6 +112,7 @@ struct DeviceCtx {
   // asynchronous host calls: tickets in submission order (ticket t runs on lane t % HOST_LANES);
   // finished calls' results until art_host_wait takes them
   std::atomic<int64_t> next_ticket{0};
+  std::atomic<int64_t> done_ticket{-1};  // the highest ticket whose call has ended
   std::mutex res_m;
   std::condition_variable res_cv;
   std::set<int64_t> pending;  // submitted, not yet waited for
@@ -1040,9 +1041,10 @@ constexpr int STREAM_FALLBACK = 1 << 20;
 // ~10% of the integrator (profiles/r04g_stream_anatomy.jsonl); it is gone. Per-ray results
 // equal the single launch's bit for bit.
 // The HostLane words the GPU reads and writes over PCIe: [0] the ready counter | [8, 8 + 64)
-// the piece flags | [72] helper blocks started | [HSIG_DONE, ...) SegOut::done_host (the flag,
-// the statistics, the flux)
-constexpr int HSIG_NFLAG = 64, HSIG_DONE = 80;
+// the piece flags | [72] helper blocks started | [76] the last integrator fully resident on the
+// GPU (ticket + 1; never reset) | [HSIG_DONE, ...) SegOut::done_host (the flag, the statistics,
+// the flux)
+constexpr int HSIG_NFLAG = 64, HSIG_RESIDENT = 76, HSIG_DONE = 80;
 constexpr size_t HSIG_WORDS = HSIG_DONE + art::DONE_FLUX + 2 * art::FLUX_HELPER_BINS;
 
 int lane_setup(DeviceCtx* c, HostLane* H) {
@@ -1063,6 +1065,7 @@ int lane_setup(DeviceCtx* c, HostLane* H) {
   }
   if (!H->hsig) {
     HIP_OK(hipHostMalloc((void**)&H->hsig, sizeof(unsigned long long) * HSIG_WORDS, hipHostMallocCoherent | hipHostMallocMapped));
+    std::memset(H->hsig, 0, sizeof(unsigned long long) * HSIG_WORDS);  // ([HSIG_RESIDENT] is never reset)
     HIP_OK(hipHostGetDevicePointer((void**)&H->hsig_dev, H->hsig, 0));
   }
   if (!H->abort_host) {
@@ -1086,7 +1089,8 @@ int latch_launch(DeviceCtx* c, LaunchRec* L, const unsigned long long* st) {
   return ART_OK;
 }
 
-int propagate_host_maskless(DeviceCtx* c, HostLane* H, bool overlap, const art_params* p, int64_t n, const double* x0,
+int propagate_host_maskless(DeviceCtx* c, HostLane* H, bool overlap, int64_t ticket, const art_params* p, int64_t n,
+                            const double* x0,
                             const double* k0, const double* erg, const double* dw, const double* ln_t0,
                             const int8_t* species, int32_t max_crossings, art_segment_out* out, art_crossing_buf* xc,
                             const FluxArgs& fx) {
@@ -1264,6 +1268,18 @@ int propagate_host_maskless(DeviceCtx* c, HostLane* H, bool overlap, const art_p
   LaunchRec* L = nullptr;
   bool launched = false;
   auto helpers_in = [&] { return serial || __atomic_load_n(hflag + HSIG_NFLAG, __ATOMIC_ACQUIRE) >= (unsigned long long)helpers; };
+  // A call in flight launches its init pass and integrator only once the previous call's integrator
+  // is fully resident (its last-starting wave stores ticket + 1 into its lane's word) or that call
+  // has ended: launched earlier, both integrators' blocks took the slots the call before them freed,
+  // ran side by side at half speed each, and their downloads and scatters piled up at the end
+  // (1.25e6 rays: calls of 28 instead of 14 ms, profiles/r05t_ab_helpers.txt). Bounded: 200 ms.
+  auto prev_resident = [&] {
+    if (!overlap || ticket <= 0 || c->done_ticket.load() >= ticket - 1 || clk() - t_start > 200.0) return true;
+    for (const HostLane& O : c->lanes)
+      if (&O != H && O.hsig && __atomic_load_n(O.hsig + HSIG_RESIDENT, __ATOMIC_ACQUIRE) >= (unsigned long long)ticket)
+        return true;
+    return false;
+  };
   auto launch_main = [&]() -> int {
     std::lock_guard<std::mutex> rlk(g_ring_mu);
     int r = take_slot(c, &L);
@@ -1280,6 +1296,11 @@ int propagate_host_maskless(DeviceCtx* c, HostLane* H, bool overlap, const art_p
       HIP_OK(art::launch_helpers(K, n, in, so, iblocks, first, 0, words + 1, H->m_comp));
     HIP_OK(hipEventRecord(L->ev0, H->m_comp));
     int grid = 0;
+    if (overlap && ticket >= 0) {  // (see prev_resident)
+      so.resident_host = H->hsig_dev + HSIG_RESIDENT;
+      so.resident_value = (unsigned long long)ticket + 1ull;
+      so.waves_total = (int32_t)std::min((n + 255) / 256, (int64_t)iblocks) * 4;
+    }
     HIP_OK(art::launch_integrator_streamed(K, n, in, so, max_crossings, words, words + 1, iblocks, H->m_comp, &grid));
     L->grid = grid;
     HIP_OK(hipEventRecord(L->ev1, H->m_comp));
@@ -1302,7 +1323,7 @@ int propagate_host_maskless(DeviceCtx* c, HostLane* H, bool overlap, const art_p
     launched = true;
     return ART_OK;
   };
-  if (helpers_in() || !overlap) {
+  if ((helpers_in() && prev_resident()) || !overlap) {
     const double tw = clk();
     while (!helpers_in()) {
       if (clk() - tw > 5000.0) break;  // (never seen: the device is shared or wedged; handled below)
@@ -1397,10 +1418,10 @@ int propagate_host_maskless(DeviceCtx* c, HostLane* H, bool overlap, const art_p
   int perr = 0;
   bool int_logged = false;  // (trace)
   for (int u = 0; u < nu && !perr; ++u) {
-    if (!launched && helpers_in() && launch_main() != ART_OK) perr = 1;
+    if (!launched && helpers_in() && prev_resident() && launch_main() != ART_OK) perr = 1;
     while (!perr && gathered.load(std::memory_order_acquire) <= u) {  // (the gatherer is ahead of the H2D copies)
       if (progress() < 0) perr = 1;
-      if (!launched && helpers_in() && launch_main() != ART_OK) perr = 1;
+      if (!launched && helpers_in() && prev_resident() && launch_main() != ART_OK) perr = 1;
       std::this_thread::sleep_for(std::chrono::microseconds(5));
     }
     if (perr) break;
@@ -1418,7 +1439,7 @@ int propagate_host_maskless(DeviceCtx* c, HostLane* H, bool overlap, const art_p
   }
   if (!perr && !launched) {  // the helpers wait for CU slots the previous call still holds
     const double tw = clk();
-    while (!helpers_in() && clk() - tw < 5000.0) {
+    while (!(helpers_in() && prev_resident()) && clk() - tw < 5000.0) {
       if (progress() < 0) break;
       std::this_thread::sleep_for(std::chrono::microseconds(20));
     }
@@ -1679,7 +1700,7 @@ int propagate_host_impl(const art_params* p, int64_t n, const double* x0, const 
   g_host_cnt[HC_CALLS] += 1;
   const HostPath hp = host_path(p, n, htr);
   if (hp == HP_STREAM) {
-    rc = propagate_host_maskless(c, &c->lanes[0], false, p, n, x0, k0, erg, dw, ln_t0, species, max_crossings, out, xc, fx);
+    rc = propagate_host_maskless(c, &c->lanes[0], false, -1, p, n, x0, k0, erg, dw, ln_t0, species, max_crossings, out, xc, fx);
     if (rc != STREAM_FALLBACK) {
       if (rc == ART_OK) g_host_cnt[HC_STREAMED] += 1;
       return rc;
@@ -1718,7 +1739,7 @@ void lane_worker(DeviceCtx* c, HostLane* H) {
 
 // Ticket t runs on lane t % HOST_LANES once that lane's previous call has ended; its result waits
 // in c->results for art_host_wait.
-int64_t submit_async(DeviceCtx* c, std::function<int(HostLane*)> body) {
+int64_t submit_async(DeviceCtx* c, std::function<int(HostLane*, int64_t)> body) {
   const int64_t t = c->next_ticket++;
   HostLane* H = &c->lanes[t % HOST_LANES];
   {
@@ -1731,7 +1752,9 @@ int64_t submit_async(DeviceCtx* c, std::function<int(HostLane*)> body) {
     H->busy = true;
     H->job = [c, H, t, body] {
       g_err.clear();
-      const int rc = body(H);
+      const int rc = body(H, t);
+      for (int64_t d = c->done_ticket.load(); d < t && !c->done_ticket.compare_exchange_weak(d, t);) {
+      }
       std::lock_guard<std::mutex> lk2(c->res_m);
       c->results[t] = {rc, g_err};
       c->res_cv.notify_all();
@@ -1783,7 +1806,7 @@ int art_propagate_host_flux_async(const art_params* p, int64_t n, const double* 
     const int rc1 = empty ? ART_OK : propagate_host_impl(p, n, x0, k0, erg, dw, ln_t0, species, max_crossings, out, xc,
                                                           TrajArgs(), fx);
     const std::string e1 = g_err;
-    *ticket = submit_async(c, [rc1, e1](HostLane*) {
+    *ticket = submit_async(c, [rc1, e1](HostLane*, int64_t) {
       g_err = e1;
       return rc1;
     });
@@ -1794,8 +1817,8 @@ int art_propagate_host_flux_async(const art_params* p, int64_t n, const double* 
   art_segment_out oc = *out;
   const bool has_xc = xc != nullptr;
   art_crossing_buf xcc = has_xc ? *xc : art_crossing_buf{};
-  *ticket = submit_async(c, [=](HostLane* H) mutable {
-    int r = propagate_host_maskless(c, H, true, &pc, n, x0, k0, erg, dw, ln_t0, species, max_crossings, &oc,
+  *ticket = submit_async(c, [=](HostLane* H, int64_t t) mutable {
+    int r = propagate_host_maskless(c, H, true, t, &pc, n, x0, k0, erg, dw, ln_t0, species, max_crossings, &oc,
                                     has_xc ? &xcc : nullptr, fx);
     if (r == STREAM_FALLBACK) {  // the batch again as one launch, on this lane's stream and staging
       g_host_cnt[HC_GIVEUPS] += 1;

@@ -98,6 +98,12 @@ struct SegOut {
   unsigned long long* done_host;
   unsigned long long *exit_count, *waves_started, *waves_done;
   int32_t exit_expected;
+  // (calls in flight) the wave that starts last of the integrator's waves_total stores
+  // resident_value into host-mapped *resident_host: the next call launches its own init pass and
+  // integrator only then, so its blocks queue behind this launch's instead of sharing the GPU with it
+  unsigned long long* resident_host;
+  unsigned long long resident_value;
+  int32_t waves_total;
   // Small batches (art_capi.cpp, propagate_device_impl): 1 = every fresh ray goes straight to
   // tail_kernel, one wave per ray (pack_fresh_kernel writes their CONT_REC records to cont),
   // instead of one lane per ray of the persistent integrator

@@ -717,8 +717,12 @@ __global__ __launch_bounds__(BLOCK, WPS) void propagate_kernel(const KParams P_i
   for (int j = threadIdx.x; j < npts; j += BLOCK) thgrid[j] = double(j) / double(npts - 1);
   if constexpr (DON == 3) {
     pend_lds[threadIdx.x >> 6][threadIdx.x & 63] = 0u;
-    if (out.waves_started && (threadIdx.x & 63) == 0)
-      __hip_atomic_fetch_add(out.waves_started, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (out.waves_started && (threadIdx.x & 63) == 0) {
+      const unsigned long long old =
+          __hip_atomic_fetch_add(out.waves_started, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (out.resident_host && old + 1ull == (unsigned long long)out.waves_total)  // (a vector store to host memory)
+        __hip_atomic_store(out.resident_host, out.resident_value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
   }
   span_stamp(stats, false);
   __syncthreads();

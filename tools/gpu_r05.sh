@@ -139,6 +139,21 @@ run_step() {
           timeout -k 10 300 python3 -u bench.py --rays 1250000 --no-cpu-baseline --no-device --steps 10 --warmup 2 > ${O}_an_1250000_${b}_r$r.json 2>> ${O}_ab_numa.err || { unset ART_BENCH_NO_NUMA; return 1; }
         done
       done; unset ART_BENCH_NO_NUMA ;;
+    ab_helpers)  # helper blocks beside the streamed integrator: 6 / 8 (default) / 12, interleaved
+      for r in 1 2 3; do
+        for h in 6 8 12; do
+          ART_HOST_HELPERS=$h timeout -k 10 300 python3 -u bench.py --no-cpu-baseline --no-device --steps 10 --warmup 2 > ${O}_ah_1e7_${h}_r$r.json 2>> ${O}_ab_helpers.err &&
+          ART_HOST_HELPERS=$h timeout -k 10 300 python3 -u bench.py --rays 1250000 --no-cpu-baseline --no-device --steps 10 --warmup 2 > ${O}_ah_1250000_${h}_r$r.json 2>> ${O}_ab_helpers.err || return 1
+        done
+      done ;;
+    ab_gate)  # calls in flight: the next call's launch gated on the previous integrator being resident (this build) vs not (libart_nogate.so), interleaved
+      for r in 1 2 3; do
+        for lib in base nogate; do
+          if [ $lib = base ]; then unset ART_LIB; else export ART_LIB=tools/build/libart_$lib.so; fi
+          timeout -k 10 300 python3 -u bench.py --rays 1250000 --no-cpu-baseline --no-device --steps 20 --warmup 3 > ${O}_ag_1250000_${lib}_r$r.json 2>> ${O}_ab_gate.err || { unset ART_LIB; return 1; }
+        done
+      done; unset ART_LIB &&
+      timeout -k 10 300 python3 -u bench.py --no-cpu-baseline --no-device --steps 10 --warmup 2 > ${O}_ag_1e7_base.json 2>> ${O}_ab_gate.err ;;
     pytest_edges)
       timeout -k 10 400 python3 -u -m pytest tests/test_edges.py -m gpu -v --timeout 300 --timeout-method thread > ${O}_pytest_edges.log 2>&1 ;;
     smoke)
