@@ -1362,6 +1362,41 @@ __host__ __device__ inline T sampler_condition_e(const KParams& P, const T* x, c
   return 0.5 * (wp2 * (1.0 - kn * iE2) - P.mass_a2) * iE2;
 }
 
+// The SIGN of sampler_condition_e at x without evaluating it (the sampler's grid needs only the
+// signs of its points and whether they are nonzero): 1 negative, 2 positive, 0 undecided (then
+// evaluate the condition). GJ plasma without a boundary layer, outside r_lim (r_lim2 =
+// (max(10 km, rNS) (1 + 1e-9))²: the exterior branch above). With G = |x|² B̂-direction
+// = 3 M x - |x|² m̂ (M = m̂·x, m̂ = (sinθm, 0, cosθm)): b = ẑ·G/|x|², and the algebra of
+// sampler_condition_e's k∥ gives p²/(D β) = (v̂l·G)²/W, W = |x|² (3M² + |x|²) (p = sinθ v̂l·B,
+// D = sin²θ |v̂l|², β = |B|²), so the condition has the sign of
+//   T1 - T2 = wp2n |ẑ·G| (W r - κ r (v̂l·G)²) - m_a² |x|⁶ W,  κ r = r (1 - m_a²/E²) + rs m_a²/E²
+// (the condition times |x|⁴ r² W 2E² > 0): one square root, no division. Decided only where
+// |T1 - T2| exceeds 1e-9 of S, the sum of the magnitudes before cancellation, while both
+// evaluations round at ~1e-14 of it; the 1e-9 band (and r = 0, the z axis, where the condition
+// is NaN) goes to the full evaluation. tests/test_corecheck.py checks the signs against the
+// condition and the oracle.
+template <class T>
+__host__ __device__ inline int sampler_sign_fast(const KParams& P, const T* x, const T* vl, double mE2,
+                                                 double r_lim2) {
+  const T rho2 = x[0] * x[0] + x[1] * x[1];
+  const T R2 = rho2 + x[2] * x[2];
+  if (!(R2 > r_lim2) || !(rho2 > 1e-100 * R2)) return 0;
+  const T r = msqrt(R2);
+  const T M = P.sm * x[0] + P.cm * x[2];
+  const T zs = 3.0 * M * x[2], zc = R2 * P.cm;
+  const T l = vl[0] * x[0] + vl[1] * x[1] + vl[2] * x[2];
+  const T vm = P.sm * vl[0] + P.cm * vl[2];
+  const T V = 3.0 * M * l - R2 * vm;
+  const T W = R2 * (3.0 * M * M + R2);
+  const T kr = P.isotropic ? 0.0 : r * (1.0 - mE2) + P.rs_gr * mE2;
+  const T wz = P.wp2n * mabs(zs - zc);
+  const T T2 = P.mass_a2 * (R2 * R2) * (R2 * W);
+  const T d = wz * (W * r - kr * (V * V)) - T2;
+  const T S = P.wp2n * (mabs(zs) + mabs(zc)) * (W * r + kr * (V * V)) + T2;
+  if (!(mabs(d) > 1e-9 * S)) return 0;
+  return d < 0.0 ? 1 : 2;
+}
+
 // ωp from GJ_Model_ωp_vec (no zeroIn) at Cartesian x, t = 0 (sampler affect!, :1587)
 template <class T>
 __host__ __device__ inline T wp_cart(const KParams& P, const T* x) {

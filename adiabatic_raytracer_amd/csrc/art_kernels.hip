@@ -2667,6 +2667,10 @@ __global__ __launch_bounds__(256, WPS) void sample_kernel(const KParams P, const
   const double cert_lhs = 2.0 * P.wp2n, cert_rhs = P.mass_a2 * (1.0 - 1e-6);
   // r_win³ = 2 wp2n / (m_a² (1 - 1e-6)) with a margin: ωp² < m_a² (1 - 1e-6) beyond it
   const double r_win2 = cert_ok ? pow(cert_lhs / cert_rhs, 2.0 / 3.0) * (1.0 + 3e-6) : 0.0;
+  // sampler_sign_fast's domain (the condition's exterior branch: r > 10 km, r >= rNS) with a margin,
+  // and the radius below which both ends of a step put all of it inside the star
+  const double r_lim = fmax(10.0, P.rNS) * (1.0 + 1e-9), r_lim2 = r_lim * r_lim;
+  const double r_in2 = (P.rNS * (1.0 - 1e-9)) * (P.rNS * (1.0 - 1e-9));
   const unsigned long long lt = (1ull << lane) - 1ull;
   if (threadIdx.x < np) sgrid[threadIdx.x] = 0.5 * double(threadIdx.x) / double(np - 1);
   __syncthreads();
@@ -2944,7 +2948,9 @@ __global__ __launch_bounds__(256, WPS) void sample_kernel(const KParams P, const
 #pragma unroll
             for (int i = 0; i < 3; ++i) xl[i] = S[i * 256] + S[(3 + i) * 256] * sc;
             const double VL[3] = {S[6 * 256], S[7 * 256], S[8 * 256]};
-            const double v = sampler_condition_e(P, xl, VL, S[9 * 256], S[10 * 256]);
+            const int fs = cert_ok ? sampler_sign_fast(P, xl, VL, P.mass_a2 * S[10 * 256], r_lim2) : 0;
+            double v = fs == 1 ? -1.0 : 1.0;  // (a decided point: only its sign and nonzero-ness are read)
+            if (fs == 0) v = sampler_condition_e(P, xl, VL, S[9 * 256], S[10 * 256]);
             if (j == nper && k == kmax - 1) slast[wb + src] = v;
             neg = signbit(v);
             nonz = v != 0.0;
@@ -3098,17 +3104,30 @@ __global__ __launch_bounds__(256, WPS) void sample_kernel(const KParams P, const
         }
       }
       const bool unc = active && !cert;
-      const unsigned long long mU = __ballot(unc);
-      const int nU = __popcll(mU);
+      // A step wholly inside the star (both ends below rNS, so the whole segment is) holds no
+      // crossing affect! keeps (rr > rNS, :1585-1597): its brackets would all be resolved and
+      // dropped, so none is queued, and only its last point is evaluated -- the value the next
+      // step's first bracket starts from. (~40% of the flat workload's uncertified steps.)
+      bool inner = false;
+      if (unc && cert_ok) {
+        const double X0[3] = {Lx[0], Lx[256], Lx[2 * 256]}, VA[3] = {Lx[3 * 256], Lx[4 * 256], Lx[5 * 256]};
+        double xa[3], xb[3];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) { xa[i] = X0[i] + VA[i] * s0; xb[i] = X0[i] + VA[i] * s1; }
+        inner = fmax(xa[0] * xa[0] + xa[1] * xa[1] + xa[2] * xa[2], xb[0] * xb[0] + xb[1] * xb[1] + xb[2] * xb[2]) < r_in2;
+      }
+      const unsigned long long mU = __ballot(unc && !inner), mI = __ballot(inner);
+      const int nU = __popcll(mU), nI = __popcll(mI);
       ART_QMARK(2)
-      if (nU == 0) {  // all certified: no point, no bracket, c_prev unchanged
+      if (nU + nI == 0) {  // all certified: no point, no bracket, c_prev unchanged
         ++st;
         continue;
       }
 #ifdef ART_SAMPLER_SECTIONS
       q_sec[6] += 1;
 #endif
-      const int uix = __popcll(mU & lt);  // this lane's rank among the uncertified ones
+      // this lane's rank among the uncertified ones (the inner steps' lanes after the others)
+      const int uix = inner ? nU + __popcll(mI & lt) : __popcll(mU & lt);
       if (unc) ssrc[wb + uix] = (unsigned char)lane;
       // bit j: signbit / nonzero-ness of point j (bit 0: the step start)
       unsigned sb = signbit(c_prev) ? 1u : 0u, nz = (c_prev != 0.0) ? 1u : 0u;
@@ -3122,7 +3141,8 @@ __global__ __launch_bounds__(256, WPS) void sample_kernel(const KParams P, const
       // atomics each, ~13 lanes deep on one word, and divided by the variable nU: 3.3 LDS
       // bank-conflict cycles per LDS instruction. Samples bit-identical, time unchanged: the
       // kernel is VALU-bound, profiles/r04aq_sampler_pmc.txt).
-      const int tot = nU * nper;
+      // items: the other lanes' 19 points each, then the inner lanes' last points
+      const int totN = nU * nper, tot = totN + nI;
 #ifndef ART_NO_SAMPLER_PRIO  // the dense grid pass at the low issue priority, the rest of a step (certificate,
       __builtin_amdgcn_s_setprio(0);  // brackets: short dependent chains) at the high one: 118.5 -> 117.1 ms
 #endif                                // per 1e7 samples (profiles/r04c_sampler_prio.jsonl)
@@ -3131,9 +3151,15 @@ __global__ __launch_bounds__(256, WPS) void sample_kernel(const KParams P, const
         const int t = w0 + lane;
         bool neg = false, nonz = false;
         if (t < tot) {
-          const int u = t / nper;
-          const int j = t - u * nper + 1;
-          const int src = ssrc[wb + u];
+          int src, j;
+          if (t < totN) {
+            const int u = t / nper;
+            j = t - u * nper + 1;
+            src = ssrc[wb + u];
+          } else {
+            j = nper;
+            src = ssrc[wb + nU + (t - totN)];
+          }
           const double* S = sline + wb + src;
           // (s1 - s0) j / 19: from the table for a full 0.5 km step (wave-uniform), else divided
           const double sc = s0 + (s1 - s0 == 0.5 ? sgrid[j] : (s1 - s0) * double(j) / double(np - 1));
@@ -3141,13 +3167,17 @@ __global__ __launch_bounds__(256, WPS) void sample_kernel(const KParams P, const
 #pragma unroll
           for (int i = 0; i < 3; ++i) xl[i] = S[i * 256] + S[(3 + i) * 256] * sc;
           const double VL[3] = {S[6 * 256], S[7 * 256], S[8 * 256]};
-          const double v = sampler_condition_e(P, xl, VL, S[9 * 256], S[10 * 256]);
+          // the point's sign without the condition where it is decided (sampler_sign_fast), else the
+          // condition itself; a decided point carries ±1 (only its sign and nonzero-ness are read)
+          const int fs = cert_ok ? sampler_sign_fast(P, xl, VL, P.mass_a2 * S[10 * 256], r_lim2) : 0;
+          double v = fs == 1 ? -1.0 : 1.0;
+          if (fs == 0) v = sampler_condition_e(P, xl, VL, S[9 * 256], S[10 * 256]);
           if (j == nper) slast[wb + src] = v;
           neg = signbit(v);
           nonz = v != 0.0;
         }
         const unsigned long long mneg = __ballot(neg), mnz = __ballot(nonz);
-        if (unc) {
+        if (unc && !inner) {
           const int a = uix * nper;
           const int lo = max(a, w0), hi = min(a + nper, w0 + 64);
           if (lo < hi) {
@@ -3165,7 +3195,7 @@ __global__ __launch_bounds__(256, WPS) void sample_kernel(const KParams P, const
       // this lane's sign changes in (point j-1, point j]: signbits differ, both values nonzero
       unsigned br = 0u;
       if (unc) {
-        br = (sb ^ (sb << 1)) & nz & (nz << 1) & (((1u << np) - 1u) & ~1u);
+        if (!inner) br = (sb ^ (sb << 1)) & nz & (nz << 1) & (((1u << np) - 1u) & ~1u);
         c_prev = slast[threadIdx.x];
       }
       ART_QMARK(3)

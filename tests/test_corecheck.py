@@ -135,6 +135,63 @@ def test_sampler_condition(oracle_lib):
                 assert abs(a - b) <= 1e-10 * (abs(b) + 1e-3)
 
 
+@pytest.mark.parametrize("kw", [dict(theta_m=0.2, mass_a=1e-5), dict(theta_m=0.0, mass_a=1e-6, B0=2e14),
+                                dict(theta_m=1.2, mass_a=3e-6, B0=5e13, omega_pul=2.0),
+                                dict(theta_m=0.5, mass_a=1e-5, isotropic=True), dict(theta_m=0.3, mass_a=1e-5, rNS=12.0)])
+def test_sampler_sign_fast(kw, oracle_lib):
+    """sampler_sign_fast (the sampler grid's signs without the condition) never disagrees with the
+    condition where it decides: on the 0.5 km grid of sampler-like lines through the conversion
+    region and at points 1e-12..1e-3 km on either side of the grid's sign changes (bisected to
+    the root), against the product's condition and, on a subset, the oracle's."""
+    p = oracle_lib.make_params(**kw)
+    rng = np.random.default_rng(11)
+    maxR = 1.2 * (2.0 * (4.0 * np.pi * abs(2.0 * kw.get("omega_pul", 1.0) / np.sqrt(4.0 * np.pi / 137.0) * 1.95e-2
+                                            * 6.582119e-16) / 137.0 / 5.0e5 * 0.5 * kw.get("B0", 1e14)
+                         * kw.get("rNS", 10.0) ** 3) / kw["mass_a"] ** 2) ** (1.0 / 3.0)
+    n = 300
+    va = rng.normal(size=(n, 3)); va /= np.linalg.norm(va, axis=1, keepdims=True)
+    vl = rng.normal(size=(n, 3)); vl /= np.linalg.norm(vl, axis=1, keepdims=True)
+    off = rng.normal(size=(n, 3)); off -= (off * va).sum(1, keepdims=True) * va
+    off *= (np.sqrt(rng.random(n)) * maxR / np.linalg.norm(off, axis=1))[:, None]
+    x0 = off - 1.1 * maxR * va
+    E = 1.0000002692622573 * kw["mass_a"] * (1.0 + 1e-8 * rng.random(n))
+    s = np.arange(1, int(2.2 * maxR / 0.5) * 19 + 1) * (0.5 / 19)
+    xs = (x0[:, None, :] + va[:, None, :] * s[None, :, None]).reshape(-1, 3)
+    c, g = cc.sampler_signs(p, xs, np.repeat(vl, len(s), 0), np.repeat(E, len(s)))
+    r = np.linalg.norm(xs, axis=1)
+    assert (((g == 1) & ~(c < 0)) | ((g == 2) & ~(c > 0))).sum() == 0
+    ext = r > max(10.0, kw.get("rNS", 10.0)) * (1 + 1e-8)
+    assert (g[ext] != 0).mean() > 0.999  # decided almost everywhere outside the star
+    assert (g[~ext] == 0).all()
+    c2 = c.reshape(n, -1)
+    i, k = np.nonzero(np.signbit(c2[:, 1:]) != np.signbit(c2[:, :-1]))
+    assert len(i) > 20
+    sa, sb = s[k].copy(), s[k + 1].copy()
+
+    def f(ss):
+        return cc.sampler_signs(p, x0[i] + va[i] * ss[:, None], vl[i], E[i])
+    fa = f(sa)[0]
+    for _ in range(70):
+        sm = 0.5 * (sa + sb)
+        fm = f(sm)[0]
+        same = np.signbit(fm) == np.signbit(fa)
+        sa, fa, sb = np.where(same, sm, sa), np.where(same, fm, fa), np.where(same, sb, sm)
+    decided = 0
+    for lg in np.arange(-12.0, -2.5, 0.5):
+        for sg in (-1.0, 1.0):
+            ss = sa + sg * 10.0 ** lg
+            cn, gn = f(ss)
+            assert (((gn == 1) & ~(cn < 0)) | ((gn == 2) & ~(cn > 0))).sum() == 0
+            decided += int((gn != 0).sum())
+            if lg in (-8.0, -6.0):
+                xo = x0[i] + va[i] * ss[:, None]
+                for q in range(0, len(gn), max(1, len(gn) // 40)):
+                    if gn[q] != 0:
+                        o = oracle_lib.sampler_condition(p, xo[q], vl[i][q], E[i][q])
+                        assert (o < 0) if gn[q] == 1 else (o > 0)
+    assert decided > 0
+
+
 def test_metric_derivatives_finite_difference():
     rs = 2.9532
     for r in [9.0, 9.99, 10.0, 10.01, 12.0, 50.0]:

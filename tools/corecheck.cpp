@@ -35,6 +35,16 @@ double cc_sampler_condition(const art_params* p, const double* x, const double* 
   KParams K = make_kparams(*p);
   return sampler_condition(K, x, vl, E);
 }
+// n points: the condition (sampler_condition) and sampler_sign_fast's verdict on each
+void cc_sampler_signs(const art_params* p, int64_t n, const double* x, const double* vl, const double* E, double* cond,
+                      int* sgn) {
+  KParams K = make_kparams(*p);
+  const double rl = (K.rNS > 10.0 ? K.rNS : 10.0) * (1.0 + 1e-9);
+  for (int64_t i = 0; i < n; ++i) {
+    cond[i] = sampler_condition(K, x + 3 * i, vl + 3 * i, E[i]);
+    sgn[i] = sampler_sign_fast(K, x + 3 * i, vl + 3 * i, K.mass_a2 / (E[i] * E[i]), rl * rl);
+  }
+}
 }
 
 extern "C" {

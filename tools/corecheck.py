@@ -77,6 +77,16 @@ def sampler_condition(p, x, vl, E):
     return lib().cc_sampler_condition(C.byref(p), P(x), P(vl), C.c_double(E))
 
 
+def sampler_signs(p, x, vl, E):
+    """(condition, sampler_sign_fast verdict) at each of the n points x (n, 3)"""
+    x, vl, E = (np.ascontiguousarray(a, np.float64) for a in (x, vl, E))
+    n = len(E)
+    cond, sgn = np.zeros(n), np.zeros(n, np.int32)
+    lib().cc_sampler_signs(C.byref(p), C.c_int64(n), P(x), P(vl), P(E), P(cond),
+                           sgn.ctypes.data_as(C.POINTER(C.c_int32)))
+    return cond, sgn
+
+
 def attempt_uniforms(seed, ray, attempt):
     U = np.zeros(10)
     lib().cc_attempt_uniforms(C.c_uint64(seed), C.c_uint64(ray), C.c_uint32(attempt), P(U))

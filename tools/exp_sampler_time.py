@@ -1,5 +1,6 @@
 """Dev: sample_kernel time (HIP events via torch) for the 1e7-ray flat forward roots and for
 the 32-point scan's slowest-to-sample point (m_a = 1e-6, B0 = 2e14, P = 0.5 s: maxR 342 km)."""
+import hashlib
 import json
 import os
 import sys
@@ -28,4 +29,9 @@ for name, kw, n in cases:
     s = inp["sample"]
     print(json.dumps({"case": name, "rays": n, "max_r": A.Params(**kw).max_r(), "ms": ms,
                       "attempts_mean": float(s["attempts"].double().mean()),
-                      "x_sum": float(s["x"].double().sum()), "weights_sum": int(s["weights"].sum())}), flush=True)
+                      "x_sum": float(s["x"].double().sum()), "weights_sum": int(s["weights"].sum()),
+                      # every sampled array, bit for bit
+                      "sha": hashlib.sha256(b"".join(v.contiguous().cpu().numpy().tobytes()
+                                                     for _, v in sorted(s.items()) if torch.is_tensor(v))
+                                            ).hexdigest()[:16],
+                      "keys": sorted(k for k, v in s.items() if torch.is_tensor(v))}), flush=True)

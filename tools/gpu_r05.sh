@@ -200,6 +200,14 @@ run_step() {
       done ;;
     pmc_gr)  # configs[3]: bulk, continuation and tail kernels of one batch, and ray 717277 alone
       bash tools/pmc_gr.sh ${O}_pmc_gr > ${O}_pmc_gr.log 2>&1 ;;
+    ab_fastsign)  # sampler grid signs from sampler_sign_fast + inner steps (this build, 3 and 2 waves/SIMD) vs tools/build/libart_base.so, interleaved
+      for r in 1 2; do
+        ART_LIB=tools/build/libart_base.so timeout -k 10 300 python3 -u tools/exp_sampler_time.py > ${O}_fs_base_r$r.jsonl 2>> ${O}_ab_fastsign.err &&
+        timeout -k 10 300 python3 -u tools/exp_sampler_time.py > ${O}_fs_new3_r$r.jsonl 2>> ${O}_ab_fastsign.err &&
+        ART_SAMPLER_WPS=2 timeout -k 10 300 python3 -u tools/exp_sampler_time.py > ${O}_fs_new2_r$r.jsonl 2>> ${O}_ab_fastsign.err || return 1
+      done ;;
+    scan_base)  # the 32-point scan with tools/build/libart_base.so
+      ART_LIB=tools/build/libart_base.so timeout -k 10 300 python3 -u tools/exp_scan_streams.py 1000000 8 32 16 > ${O}_scan_base.jsonl 2> ${O}_scan_base.err ;;
     pmc)  # the full PMC set of this build (bench.py's roofline.traffic)
       bash tools/pmc_passes.sh ${O}_pmc 10000000 > ${O}_pmc.log 2>&1 ;;
     *) echo "unknown step $1"; return 2 ;;
