@@ -44,4 +44,32 @@ t = time.perf_counter()
 dispatch(live, lambda i: engs[i][0].forward_roots(rays, seed=1769), ss)
 torch.cuda.synchronize()
 t_conc = time.perf_counter() - t
-print(json.dumps({"setup_s": t_setup, "sum_sample_alone_s": sum(alone) / 1e3, "sample_8streams_s": t_conc}), flush=True)
+# the same dispatch with every output allocated beforehand on its stream's pool (the launches alone)
+import ctypes as C  # noqa: E402
+from adiabatic_raytracer_amd.engine import _p, _stream  # noqa: E402
+pre = {}
+t = time.perf_counter()
+for q, i in enumerate(live):
+    with torch.cuda.stream(ss[q % len(ss)]):
+        e = engs[i][0]
+        pre[i] = {k: e.empty(3 * rays) for k in ("x", "k_init", "vifty")} | {"erg": e.empty(rays)} | \
+            {k: e.empty(rays, dtype=torch.int32) for k in ("weights", "attempts")}
+torch.cuda.synchronize()
+t_alloc = time.perf_counter() - t
+
+
+def launch(i):
+    e, mr = engs[i]
+    o = pre[i]
+    rc = e.lib.art_sample_conversion_points_device(C.byref(e.cp), float(mr), 1769, 0, rays,
+                                                   *[_p(o[k]) for k in ("x", "k_init", "erg", "vifty", "weights", "attempts")],
+                                                   _stream())
+    assert rc == 0
+
+
+t = time.perf_counter()
+dispatch(live, launch, ss)
+torch.cuda.synchronize()
+t_pre = time.perf_counter() - t
+print(json.dumps({"setup_s": t_setup, "sum_sample_alone_s": sum(alone) / 1e3, "sample_8streams_s": t_conc,
+                  "alloc_s": t_alloc, "sample_8streams_preallocated_s": t_pre}), flush=True)

@@ -13,6 +13,9 @@ if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < min(16, max(4, streams))
     os.environ["GPU_MAX_HW_QUEUES"] = str(min(16, max(4, streams)))
 npts = int(sys.argv[3]) if len(sys.argv) > 3 else 32
 donate = int(sys.argv[4]) if len(sys.argv) > 4 else 0
+reps = int(sys.argv[5]) if len(sys.argv) > 5 else 1  # (> 1: the later runs reuse the caching allocator's blocks)
+for _ in range(reps - 1):
+    print(json.dumps(run_points(scan_grid()[:npts], rays, streams=streams, donate=donate)[1] | {"warm-up": True}), flush=True)
 recs, summ = run_points(scan_grid()[:npts], rays, streams=streams, donate=donate)
 for i, r in enumerate(recs):
     print(json.dumps({k: r.get(k) for k in ("mass_a", "B0", "omega_pul", "kernel_ms", "accepted", "attempts")} | {"point": i}))
