@@ -206,6 +206,19 @@ run_step() {
         timeout -k 10 300 python3 -u tools/exp_sampler_time.py > ${O}_fs_new3_r$r.jsonl 2>> ${O}_ab_fastsign.err &&
         ART_SAMPLER_WPS=2 timeout -k 10 300 python3 -u tools/exp_sampler_time.py > ${O}_fs_new2_r$r.jsonl 2>> ${O}_ab_fastsign.err || return 1
       done ;;
+    ab_sgrid)  # the 32-point scan with the sampler's grid at 1/d of the block slots (ART_SAMPLER_GRID_DIV), interleaved
+      for r in 1 2; do
+        for d in 1 2 4 8; do
+          ART_SAMPLER_GRID_DIV=$d timeout -k 10 300 python3 -u tools/exp_scan_streams.py 1000000 8 32 16 > ${O}_sgrid_${d}_r$r.jsonl 2>> ${O}_ab_sgrid.err || return 1
+        done
+      done ;;
+    ab_brclass)  # brackets classified when found (this build) vs tools/build/libart_prev.so (fast signs only), interleaved
+      for r in 1 2; do
+        ART_LIB=tools/build/libart_prev.so timeout -k 10 300 python3 -u tools/exp_sampler_time.py > ${O}_bc_prev_r$r.jsonl 2>> ${O}_ab_brclass.err &&
+        timeout -k 10 300 python3 -u tools/exp_sampler_time.py > ${O}_bc_new_r$r.jsonl 2>> ${O}_ab_brclass.err &&
+        ART_LIB=tools/build/libart_prev.so timeout -k 10 300 python3 -u tools/exp_scan_streams.py 1000000 8 32 16 > ${O}_bc_scan_prev_r$r.jsonl 2>> ${O}_ab_brclass.err &&
+        timeout -k 10 300 python3 -u tools/exp_scan_streams.py 1000000 8 32 16 > ${O}_bc_scan_new_r$r.jsonl 2>> ${O}_ab_brclass.err || return 1
+      done ;;
     scan_base)  # the 32-point scan with tools/build/libart_base.so
       ART_LIB=tools/build/libart_base.so timeout -k 10 300 python3 -u tools/exp_scan_streams.py 1000000 8 32 16 > ${O}_scan_base.jsonl 2> ${O}_scan_base.err ;;
     pmc)  # the full PMC set of this build (bench.py's roofline.traffic)
