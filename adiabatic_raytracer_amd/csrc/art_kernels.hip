@@ -2778,6 +2778,9 @@ __global__ __launch_bounds__(256, WPS) void sample_kernel(const KParams P, const
     // resolve the queued brackets: Illinois on the exact line (the lane that found one owns
     // it), then each owner counts its valid crossings in queue order and keeps the randInx-th
     auto flush = [&]() {
+#ifdef ART_SSEC_FLUSH  // (dev: the flushes' cycles in the "out" bucket instead of "brackets")
+      ART_QMARK(4)
+#endif
       wave_lds_sync();
       #pragma unroll 1
       for (int t = lane; t < qn; t += 64) {
@@ -2827,6 +2830,9 @@ __global__ __launch_bounds__(256, WPS) void sample_kernel(const KParams P, const
       }
       qn = 0;
       wave_lds_sync();
+#ifdef ART_SSEC_FLUSH
+      ART_QMARK(5)
+#endif
     };
 
     ART_QMARK(0)
