@@ -2863,6 +2863,7 @@ __global__ __launch_bounds__(256, WPS) void sample_kernel(const KParams P, const
         int nxt = (active && S1 < w_in && w_in < send) ? (int)floor(w_in * 2.0) - 1 : nsteps;
 #pragma unroll
         for (int o = 32; o >= 1; o >>= 1) nxt = min(nxt, __shfl_xor(nxt, o));
+        nxt = __builtin_amdgcn_readfirstlane(nxt);  // (wave-uniform: keeps the step counter and kmax scalar)
         if (nxt > st0 + KB) st0 = nxt - KB;
         continue;
       }
@@ -3025,7 +3026,7 @@ __global__ __launch_bounds__(256, WPS) void sample_kernel(const KParams P, const
             sqsrc[wq + slot] = (unsigned char)lane;
             br &= br - 1u;
           }
-          qn += __popcll(bm);
+          qn = __builtin_amdgcn_readfirstlane(qn + __popcll(bm));  // (wave-uniform)
           bm = __ballot(br != 0u);
         }
       }
@@ -3055,6 +3056,7 @@ __global__ __launch_bounds__(256, WPS) void sample_kernel(const KParams P, const
         int nxt = (active && s1 < w_in && w_in < send) ? (int)floor(w_in * 2.0) - 1 : nsteps;
 #pragma unroll
         for (int o = 32; o >= 1; o >>= 1) nxt = min(nxt, __shfl_xor(nxt, o));
+        nxt = __builtin_amdgcn_readfirstlane(nxt);  // (wave-uniform: keeps the step counter scalar)
         st = nxt > st + 1 ? nxt : st + 1;
         continue;
       }
@@ -3233,7 +3235,7 @@ __global__ __launch_bounds__(256, WPS) void sample_kernel(const KParams P, const
           sqsrc[wq + slot] = (unsigned char)lane;
           br &= br - 1u;
         }
-        qn += __popcll(bm);
+        qn = __builtin_amdgcn_readfirstlane(qn + __popcll(bm));  // (wave-uniform)
         bm = __ballot(br != 0u);
       }
       ART_QMARK(4)
