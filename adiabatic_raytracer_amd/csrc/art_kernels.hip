@@ -2604,26 +2604,28 @@ __device__ inline double line_rmin2(const double* x0, const double* va, double s
 // length (a block of steps as well as one step) and whatever the sign of the point before it.
 __device__ inline int seg_cert(const KParams& P, const double* X0, const double* VA, double E, double s0, double s1,
                                double cert_lhs, double cert_rhs) {
+  // The radii's square root and the three reciprocals in single precision (v_sqrt_f32, v_rcp_f32 of
+  // the rounded operand: relative error < 3e-7 each): every bound below is widened by 2e-6 (db, the
+  // negative test) or 1e-6 (g^rr, bmin, rmin > 10) to stay conservative, and the negative test's
+  // own 1e-6 margin on m_a² is kept whole; a certified segment is still provably one-signed.
   const double rm2 = line_rmin2(X0, VA, s0, s1);
-  const double rmin = sqrt(rm2);
+  const double rmin = (double)__builtin_amdgcn_sqrtf((float)rm2);
   double xa[3], xb[3];
 #pragma unroll
   for (int i = 0; i < 3; ++i) { xa[i] = X0[i] + VA[i] * s0; xb[i] = X0[i] + VA[i] * s1; }
   const double ra2 = xa[0] * xa[0] + xa[1] * xa[1] + xa[2] * xa[2];
   const double rb2 = xb[0] * xb[0] + xb[1] * xb[1] + xb[2] * xb[2];
-  // (reciprocals from frcp, <= 1 ulp: the margins, 1e-9 relative and 1e-12 absolute on db and 1e-6
-  // on m_a², dwarf that; a certified segment is still provably one-signed)
-  const double ba = (P.cm * (3.0 * xa[2] * xa[2] - ra2) + 3.0 * P.sm * xa[0] * xa[2]) * frcp(ra2);
-  const double bb = (P.cm * (3.0 * xb[2] * xb[2] - rb2) + 3.0 * P.sm * xb[0] * xb[2]) * frcp(rb2);
-  const double irmin = frcp(rmin);
+  const double ba = (P.cm * (3.0 * xa[2] * xa[2] - ra2) + 3.0 * P.sm * xa[0] * xa[2]) * (double)__builtin_amdgcn_rcpf((float)ra2);
+  const double bb = (P.cm * (3.0 * xb[2] * xb[2] - rb2) + 3.0 * P.sm * xb[0] * xb[2]) * (double)__builtin_amdgcn_rcpf((float)rb2);
+  const double irmin = (double)__builtin_amdgcn_rcpf((float)rmin);
   const double al = (s1 - s0) * irmin;
-  const double db = 0.75 * al * al * (1.0 + 1e-9) + 1e-12;
-  const double bmax = fmin(2.0, fmax(fabs(ba), fabs(bb)) + db);
-  if (cert_lhs * 0.5 * bmax < cert_rhs * (rm2 * rmin)) return 1;
-  if (rmin > 10.0) {
-    const double bmin = (ba * bb > 0.0) ? fmin(fabs(ba), fabs(bb)) - db : -1.0;
+  const double db = 0.75 * al * al * (1.0 + 2e-6) + 1e-12;
+  const double bmax = fmin(2.0, fmax(fabs(ba), fabs(bb)) * (1.0 + 1e-6) + db);
+  if (cert_lhs * 0.5 * bmax < cert_rhs * (rm2 * rmin) * (1.0 - 2e-6)) return 1;
+  if (rmin > 10.0 * (1.0 + 1e-6)) {
+    const double bmin = (ba * bb > 0.0) ? fmin(fabs(ba), fabs(bb)) * (1.0 - 1e-6) - db : -1.0;
     const double rmax2 = fmax(ra2, rb2);
-    const double grr = 1.0 - P.rs_gr * irmin * (1.0 + 1e-15);  // (rounded down: a smaller g^rr)
+    const double grr = 1.0 - P.rs_gr * irmin * (1.0 + 1e-6);  // (rounded down: a smaller g^rr)
     if (bmin > 0.0 && P.wp2n * bmin * grr > E * E * (1.0 + 1e-6) * (rmax2 * sqrt(rmax2))) return 2;
   }
   return 0;
@@ -3088,26 +3090,27 @@ __global__ __launch_bounds__(256, WPS) void sample_kernel(const KParams P, const
       if (active && !quiet && cert_ok && c_prev != 0.0 && !isnan(c_prev)) {
         const double X0[3] = {Lx[0], Lx[256], Lx[2 * 256]}, VA[3] = {Lx[3 * 256], Lx[4 * 256], Lx[5 * 256]};
         const double rm2 = line_rmin2(X0, VA, s0, s1);
-        const double rmin = sqrt(rm2);
+        const double rmin = (double)__builtin_amdgcn_sqrtf((float)rm2);
         double xa[3], xb[3];
 #pragma unroll
         for (int i = 0; i < 3; ++i) { xa[i] = X0[i] + VA[i] * s0; xb[i] = X0[i] + VA[i] * s1; }
         const double ra2 = xa[0] * xa[0] + xa[1] * xa[1] + xa[2] * xa[2];
         const double rb2 = xb[0] * xb[0] + xb[1] * xb[1] + xb[2] * xb[2];
-        // (reciprocals from frcp, <= 1 ulp: the certificate's margins, 1e-9 relative and 1e-12
-        // absolute on db and 1e-6 on m_a², dwarf that; a certified step is still provably one-signed)
-        const double ba = (P.cm * (3.0 * xa[2] * xa[2] - ra2) + 3.0 * P.sm * xa[0] * xa[2]) * frcp(ra2);
-        const double bb = (P.cm * (3.0 * xb[2] * xb[2] - rb2) + 3.0 * P.sm * xb[0] * xb[2]) * frcp(rb2);
-        const double irmin = frcp(rmin);
+        // (the square root and reciprocals in single precision, < 3e-7 relative each, with the bounds
+        // widened as in seg_cert; the 1e-6 margin on m_a² kept whole: a certified step is still
+        // provably one-signed)
+        const double ba = (P.cm * (3.0 * xa[2] * xa[2] - ra2) + 3.0 * P.sm * xa[0] * xa[2]) * (double)__builtin_amdgcn_rcpf((float)ra2);
+        const double bb = (P.cm * (3.0 * xb[2] * xb[2] - rb2) + 3.0 * P.sm * xb[0] * xb[2]) * (double)__builtin_amdgcn_rcpf((float)rb2);
+        const double irmin = (double)__builtin_amdgcn_rcpf((float)rmin);
         const double al = (s1 - s0) * irmin;
-        const double db = 0.75 * al * al * (1.0 + 1e-9) + 1e-12;
+        const double db = 0.75 * al * al * (1.0 + 2e-6) + 1e-12;
         if (c_prev < 0.0) {
-          const double bmax = fmin(2.0, fmax(fabs(ba), fabs(bb)) + db);
-          cert = cert_lhs * 0.5 * bmax < cert_rhs * (rm2 * rmin);
-        } else if (rmin > 10.0) {
-          const double bmin = (ba * bb > 0.0) ? fmin(fabs(ba), fabs(bb)) - db : -1.0;
+          const double bmax = fmin(2.0, fmax(fabs(ba), fabs(bb)) * (1.0 + 1e-6) + db);
+          cert = cert_lhs * 0.5 * bmax < cert_rhs * (rm2 * rmin) * (1.0 - 2e-6);
+        } else if (rmin > 10.0 * (1.0 + 1e-6)) {
+          const double bmin = (ba * bb > 0.0) ? fmin(fabs(ba), fabs(bb)) * (1.0 - 1e-6) - db : -1.0;
           const double rmax2 = fmax(ra2, rb2);
-          const double grr = 1.0 - P.rs_gr * irmin * (1.0 + 1e-15);  // (rounded down: a smaller g^rr)
+          const double grr = 1.0 - P.rs_gr * irmin * (1.0 + 1e-6);  // (rounded down: a smaller g^rr)
           cert = bmin > 0.0 && P.wp2n * bmin * grr > E * E * (1.0 + 1e-6) * (rmax2 * sqrt(rmax2));
         }
       }
