@@ -84,6 +84,7 @@ SIGNATURES = {
     "art_recent_kernel_span_ms": (C.c_int, [_i32, _v]),
     "art_set_tail_donation": (C.c_int, [_i32]),
     "art_set_graduation": (C.c_int, [_i32]),
+    "art_set_sampler_waves": (C.c_int, [_i32]),
     "art_flux_histogram_phi_device": (C.c_int, [_i64, _v, _v, _v, _i32, _v, _v]),
     "art_flux_histogram_phi_range_device": (C.c_int, [_i64, _v, _v, _v, _i32, _d, _d, _v, _v]),
     "art_comm_unique_id": (C.c_int, [_v]),

@@ -98,6 +98,7 @@ struct DeviceCtx {
   int64_t launches = 0;          // propagate launches issued so far
   int32_t donate = -1;           // tail donation (art_set_tail_donation): lanes per wave, 0 = off, -1 = by geometry
   int32_t graduate = -1;         // graduation (art_set_graduation): attempts, 0 = off, -1 = the default (2048)
+  int32_t sampler_waves = 0;     // art_set_sampler_waves: 0 = by line length, 2 or 3
   std::vector<std::pair<void*, size_t>> pool;  // host-entry staging buffers (grow-only, used under g_mu by the
                                                // synchronous *_host calls only)
   // the chunked host pipeline of art_propagate_host (propagate_host_chunked): its compute
@@ -676,6 +677,16 @@ int art_set_graduation(int32_t attempts) {
   int rc = current_ctx(&c);
   if (rc) return rc;
   c->graduate = attempts;
+  return ART_OK;
+}
+
+int art_set_sampler_waves(int32_t waves) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (waves != 0 && waves != 2 && waves != 3) return fail(ART_E_INVALID, "sampler waves must be 0, 2 or 3");
+  DeviceCtx* c;
+  int rc = current_ctx(&c);
+  if (rc) return rc;
+  c->sampler_waves = waves;
   return ART_OK;
 }
 
@@ -1938,7 +1949,7 @@ int sample_device_impl(const art_params* p, double max_r, uint64_t seed, int64_t
   HIP_OK(hipMemsetAsync(q, 0, sizeof(unsigned long long), s));
   HIP_OK(hipMemsetAsync(q, 0, 256, s));
   HIP_OK(art::launch_sample(kparams(*p), max_r, seed, ray_offset, n, x, k_init, erg_inf, vifty, weights,
-                            attempts, (unsigned long long*)q, s));
+                            attempts, (unsigned long long*)q, s, c->sampler_waves));
 #ifdef ART_SAMPLER_SECTIONS  // (dev build: the sampler's section cycles to stderr)
   {
     unsigned long long w[16];

@@ -154,7 +154,7 @@ hipError_t launch_helpers(const KParams& P, int64_t n, const SegIn& in, const Se
 int64_t small_tail_limit();
 hipError_t launch_sample(const KParams& P, double maxR, uint64_t seed, int64_t ray_offset, int64_t n, double* x,
                          double* k, double* erg, double* vifty, int32_t* w, int32_t* att, unsigned long long* queue,
-                         hipStream_t s);
+                         hipStream_t s, int waves);
 hipError_t launch_prob(const KParams& P, int64_t nc, const double* pos, const double* kpos, const double* erg,
                        int64_t n_groups, const int64_t* gstart, double* out, hipStream_t s);
 hipError_t launch_flux(const KParams& P, int64_t n, const double* x_end, const double* k_end, const int32_t* status,

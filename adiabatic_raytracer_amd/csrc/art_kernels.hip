@@ -3691,12 +3691,13 @@ hipError_t launch_helpers(const KParams& P, int64_t n, const SegIn& in, const Se
 
 hipError_t launch_sample(const KParams& P, double maxR, uint64_t seed, int64_t ray_offset, int64_t n, double* x,
                          double* k, double* erg, double* vifty, int32_t* w, int32_t* att, unsigned long long* queue,
-                         hipStream_t s) {
+                         hipStream_t s, int waves) {
   // lines of up to 2.2 x 60 km (264 steps): the 3-wave build, step by step (blocks of steps: no
   // faster there, 118 vs 119 ms per 1e7 flat samples); longer lines, mostly certified far from the
   // conversion surface: 2 waves, blocks of 3 steps (the scan's largest-maxR point 55 -> 43 ms,
-  // profiles/r05h_ab_sampler.txt). ART_SAMPLER_WPS=2|3 and ART_SAMPLER_BLOCKS=0|1 force a build (A/B)
-  int wps = maxR <= 60.0 ? 3 : 2;
+  // profiles/r05h_ab_sampler.txt). waves (art_set_sampler_waves) = 2 or 3 takes that build for every
+  // line; ART_SAMPLER_WPS=2|3 and ART_SAMPLER_BLOCKS=0|1 force a build (A/B)
+  int wps = waves == 2 || waves == 3 ? waves : (maxR <= 60.0 ? 3 : 2);
   bool blocks = maxR > 60.0;
   if (const char* e = std::getenv("ART_SAMPLER_WPS"))
     if (e[0] == '2' || e[0] == '3') wps = e[0] - '0';

@@ -91,6 +91,12 @@ class Engine:
         default (2048 attempts). Bit-identical results."""
         check(self.lib.art_set_graduation(int(attempts)))
 
+    def set_sampler_waves(self, waves: int) -> None:
+        """Waves per SIMD of the sampler (art_set_sampler_waves, include/art.h): 0 = by line
+        length (the default), 3 = the 3-wave build for every line (several sampler launches in
+        flight). Bit-identical samples."""
+        check(self.lib.art_set_sampler_waves(int(waves)))
+
     def kernel_ms(self) -> float:
         """Duration of the last propagate kernel (HIP events on its stream); synchronizes."""
         check(self.lib.art_synchronize())

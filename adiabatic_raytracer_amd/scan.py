@@ -99,6 +99,9 @@ def run_points(kws: list[dict], rays: int, seed: int = 1769, nbins: int = 50, de
             engs.append(Engine(p, device=device))
             engs[-1].set_tail_donation(donate)
             engs[-1].set_graduation(0 if len(ss) > 1 else -1)  # (passes in flight: off)
+            # samplers in flight: the 3-wave build for every line (per device; 0.503-0.508 -> 0.484 s
+            # of sampling, profiles/r05ah_scan_sampler_waves.txt)
+            engs[-1].set_sampler_waves(3 if len(ss) > 1 else 0)
     # Longest expected drain first: a point's kernel time grows with its conversion radius
     # (maxR: 29 km -> 20 ms ... 342 km -> 835 ms per 1e6 rays, profiles/r02b_scan_order.txt),
     # and the longest single ray bounds the whole scan, so it should start at once.
@@ -121,7 +124,8 @@ def run_points(kws: list[dict], rays: int, seed: int = 1769, nbins: int = 50, de
     torch.cuda.synchronize()
     wall = time.perf_counter() - t1
     if live:
-        engs[live[0]].set_graduation(-1)  # (the device's default again)
+        engs[live[0]].set_graduation(-1)  # (the device's defaults again)
+        engs[live[0]].set_sampler_waves(0)
     k = len(order)
     ms = (C.c_double * max(1, k))()
     got = A._lib.load().art_recent_kernel_ms(k, ms)

@@ -182,6 +182,13 @@ int art_set_tail_donation(int32_t lanes);
  * wave while the other batches fill the CUs it frees; -1 (the default) = 2048 attempts (or
  * ART_GRADUATE). Per device; results are bit-identical either way. */
 int art_set_graduation(int32_t attempts);
+/* Waves per SIMD of the conversion-point sampler (art_sample_conversion_points*): 0 (the default)
+ * chooses by line length -- 3 for lines up to 2.2 x 60 km, walked step by step, else 2 with blocks
+ * of 3 steps, the faster builds for one launch at a time; 3 takes the 3-wave build for every line,
+ * which packs better beside other sampler launches in flight on other streams (the 32-point scan's
+ * sampling on 8 streams: 0.503-0.508 -> 0.484 s, profiles/r05ah_scan_sampler_waves.txt). Per
+ * device; samples are bit-identical either way. No reference counterpart (an execution policy). */
+int art_set_sampler_waves(int32_t waves);
 /* The Vern6 tableau the kernel uses: c[9], A[81] row-major, b[9], bhat[9]. */
 int art_vern6_tableau(double* c, double* A, double* b, double* bhat);
 
