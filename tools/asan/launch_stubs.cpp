@@ -17,7 +17,7 @@ hipError_t launch_helpers(const KParams&, int64_t, const SegIn&, const SegOut&, 
 }
 int64_t small_tail_limit() { return 0; }
 hipError_t launch_sample(const KParams&, double, uint64_t, int64_t, int64_t, double*, double*, double*, double*, int32_t*,
-                         int32_t*, unsigned long long*, hipStream_t) { return hipErrorNoDevice; }
+                         int32_t*, unsigned long long*, hipStream_t, int) { return hipErrorNoDevice; }
 hipError_t launch_prob(const KParams&, int64_t, const double*, const double*, const double*, int64_t, const int64_t*,
                        double*, hipStream_t) { return hipErrorNoDevice; }
 hipError_t launch_flux(const KParams&, int64_t, const double*, const double*, const int32_t*, const int8_t*,
