@@ -48,6 +48,8 @@ def test_invalid_params_fail_loudly():
     lib = A.load_library()
     rc = lib.art_get_prob_nonad_host(C.byref(c), 0, None, None, None, 0, None, None)
     assert rc == -4 and b"melrose" in lib.art_last_error()
+    # execution policies validate their argument before touching a device
+    assert lib.art_set_sampler_waves(5) == -1 and b"sampler waves" in lib.art_last_error()  # ART_E_INVALID
 
 
 def test_find_conversion_surface_matches_oracle(oracle_lib):

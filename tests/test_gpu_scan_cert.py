@@ -58,3 +58,28 @@ def test_sampler_certificate_is_bit_exact(cfg, monkeypatch):
     b = A.sample_conversion_points(p, n, seed=1769)
     for k in ("x", "k_init", "erg", "vifty", "weights", "attempts"):
         assert np.array_equal(a[k], b[k], equal_nan=True), (cfg, k)
+
+
+@pytest.mark.parametrize("cfg", ["flat", "scan_longest"])
+def test_sampler_waves_are_bit_exact(cfg):
+    """art_set_sampler_waves (include/art.h) only picks the sampler's build: the 3-wave build for
+    every line (what the scan takes with samplers in flight), the 2-wave one and the default choice
+    by line length give bit-identical samples, for short lines (step by step) and the scan's long
+    ones (blocks of steps at 2 waves by default)."""
+    import adiabatic_raytracer_amd as A
+    from adiabatic_raytracer_amd import Engine
+    from adiabatic_raytracer_amd.scan import scan_grid
+    kw = max(scan_grid(), key=lambda g: A.Params(**g).max_r()) if cfg == "scan_longest" else CONFIGS[cfg]
+    eng = Engine(A.Params(**kw))
+    n = 20000 if cfg == "flat" else 4000
+    out = {}
+    try:
+        for w in (0, 3, 2):
+            eng.set_sampler_waves(w)
+            s = eng.sample(n, seed=1769)
+            out[w] = {k: v.cpu().numpy() for k, v in s.items()}
+    finally:
+        eng.set_sampler_waves(0)
+    for w in (3, 2):
+        for k in ("x", "k_init", "erg", "vifty", "weights", "attempts"):
+            assert np.array_equal(out[0][k], out[w][k], equal_nan=True), (cfg, w, k)
