@@ -6,6 +6,11 @@
 # configs[3] as one GR batch with its PMC set, and the scan / sampler / tail-ray / host-path /
 # small-batch / event / section side figures.
 # Usage: TAG=r05fin bash tools/gpu_final.sh [STEP ...]   (no steps: all of them, in order)
+# Before a call, on the CPU: build the library (python -c "import __graft_entry__ as g; g.build()") and
+# the two section-timing variants the `sections` step loads from the same source (a variant built from
+# older source lacks newer symbols and fails to load):
+#   python adiabatic_raytracer_amd/build.py --variant tools/build/libart_sect.so -DART_SECTION_TIMING
+#   python adiabatic_raytracer_amd/build.py --variant tools/build/libart_ssec.so -DART_SAMPLER_SECTIONS
 # Writes gpurun_out/TAG_*; every GPU step has its own time limit; the first failure ends the run.
 TAG=${TAG:-r05fin}
 set -o pipefail
