@@ -310,11 +310,21 @@ int env_int(const char* name, int dflt) {
 
 // (a heap object, not a function-local static: art_shutdown joins its threads before the HIP
 // runtime's own teardown, and no static destructor of libart is left to run after it)
-CopyPool* g_copy_pool = nullptr;
+// Created under its own lock: the gatherer threads of two asynchronous calls may ask for it
+// at the same time, outside g_mu.
+std::atomic<CopyPool*> g_copy_pool{nullptr};
+std::mutex g_copy_pool_mu;
 CopyPool& copy_pool() {
+  CopyPool* cp = g_copy_pool.load(std::memory_order_acquire);
+  if (cp) return *cp;
+  std::lock_guard<std::mutex> lk(g_copy_pool_mu);
+  cp = g_copy_pool.load(std::memory_order_relaxed);
   // ART_HOST_THREADS: worker threads besides the caller (default 7)
-  if (!g_copy_pool) g_copy_pool = new CopyPool(std::max(0, env_int("ART_HOST_THREADS", 7)));
-  return *g_copy_pool;
+  if (!cp) {
+    cp = new CopyPool(std::max(0, env_int("ART_HOST_THREADS", 7)));
+    g_copy_pool.store(cp, std::memory_order_release);
+  }
+  return *cp;
 }
 
 // Every HIP object a device context holds, released in dependency order (the streams drained
@@ -374,8 +384,8 @@ void shutdown_locked() {
   for (auto& c : all)
     if (c) release_ctx(*c);
   all.clear();
-  delete g_copy_pool;
-  g_copy_pool = nullptr;
+  std::lock_guard<std::mutex> lk(g_copy_pool_mu);
+  delete g_copy_pool.exchange(nullptr);
 }
 
 void shutdown_at_exit() {

@@ -229,12 +229,27 @@ class HostCall:
 
     def __init__(self, ticket, out, keep):
         self.ticket, self.out, self._keep = ticket, out, keep
+        self._waited = False
 
     def wait(self) -> dict:
-        check(_lib.load().art_host_wait(self.ticket))
-        self.out["flux"] = self.out["flux"].reshape(2, -1)
-        self._keep = None
+        if not self._waited:
+            self._waited = True
+            check(_lib.load().art_host_wait(self.ticket))
+            self.out["flux"] = self.out["flux"].reshape(2, -1)
+            self._keep = None
         return self.out
+
+    def __del__(self):
+        # the library's worker writes through raw pointers into the arrays this object holds:
+        # a call dropped without wait() (an exception between submit and wait) must not free
+        # them while the GPU and the host threads still write into them
+        if not getattr(self, "_waited", True):
+            self._waited = True
+            try:
+                _lib.load().art_host_wait(self.ticket)
+            except Exception:  # noqa: BLE001 -- interpreter shutdown: nothing left to report to
+                pass
+            self._keep = None
 
 
 def propagate_batch_async(params: Params, x0, k0, erg, dw, ln_t0, species, flux_nbins, max_crossings=-1,

@@ -1,0 +1,136 @@
+"""Comparison of a forward-segment run against the converged-truth fixtures
+(tests/golden/truth_*.npz, made by tests/golden/make_truth_fixture.py). TEST INFRASTRUCTURE.
+
+Used twice with the same bounds: by tests/test_truth.py for the oracle (CPU) and by
+tests/test_gpu_truth.py for the HIP engine (through the C ABI). The bounds are the
+north_star's "stated FP64 tolerance" of the physics outputs:
+they are set from the measured distributions of the reference's own accuracy class (Vern6 at
+abstol 1e-6 / reltol 1e-7, RayTracer.jl:383-384) against the truth, not from the engine's
+agreement with the oracle.
+"""
+import os
+
+import numpy as np
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+CASES = ("flat", "gr", "gr_oblique", "scan")
+ST_SUCCESS, ST_CROSSING, ST_HIT_NS, ST_TRUTH_SINGULAR = 0, 1, 2, -1
+QS = (50, 90, 99, 100)
+
+# The stated tolerance, one table for the four configurations: bounds on the 50th / 90th /
+# 99th percentile of each output's relative error against the truth. REFERENCE is the
+# reference's own accuracy class (Vern6 at abstol 1e-6 / reltol 1e-7, RayTracer.jl:383-384):
+# set from the measured oracle-vs-truth maxima over the four configurations with a margin of
+# 3-10x (DESIGN.md §5 has the measured values). The p99 tails are the solver tolerance, not
+# the event scan: crossings downstream of a kink of |B_z| (a force discontinuity) and slow
+# photons near the plasma cutoff (dr/dτ -> 0, so t moves while x does not) carry it, and every
+# percentile falls ~100x per 100x tighter tolerance. TIGHT is the same run at abstol 1e-10 /
+# reltol 1e-11: the Hermite scan plus re-step polish converge to the truth's 50-point
+# interpolant scan, so a semantic error of the event logic cannot hide in the tolerance.
+TOL = {
+    "reference": {
+        "crossing position": (1e-7, 3e-5, 1e-3),
+        "crossing k": (3e-6, 3e-3, 1e-1),
+        "crossing t": (5e-6, 1e-2, 5e-1),
+        "crossing dw": (1e-10, 1e-8, 1e-7),
+        "P_nonAD": (1e-5, 1e-2, 5e-1),
+        "end position": (3e-6, 3e-5, 3e-4),
+        "end k": (3e-6, 3e-5, 3e-4),
+        "end u7": (1e-9, 1e-8, 1e-7),
+    },
+    "tight": {
+        "crossing position": (1e-10, 1e-10, 1e-9),
+        "crossing k": (1e-9, 1e-8, 1e-7),
+        "crossing t": (1e-8, 1e-8, 1e-6),
+        "crossing dw": (1e-13, 1e-13, 1e-12),
+        "P_nonAD": (1e-8, 1e-8, 3e-6),
+        "end position": (3e-9, 1e-8, 1e-7),
+        "end k": (3e-9, 1e-8, 1e-7),
+        "end u7": (1e-12, 1e-12, 1e-11),
+    },
+}
+NUMERICS = {"reference": dict(abstol=1e-6, reltol=1e-7), "tight": dict(abstol=1e-10, reltol=1e-11)}
+# segment status and crossing detection (REFERENCE measured at most 1 of 1024 rays per
+# configuration, a near-tangent ray whose true condition stays within 4e-9 of zero; TIGHT none)
+MAX_STATUS_MISMATCH = {"reference": 0.01, "tight": 0.002}  # fraction of rays (truth not singular)
+MAX_MISSED_CROSSING = {"reference": 0.01, "tight": 0.002}  # truth crosses, the run does not
+MAX_EXTRA_CROSSING = {"reference": 0.01, "tight": 0.002}   # the run crosses, the truth does not
+MAX_FLUX_L1 = {"reference": 0.01, "tight": 0.002}          # Σ|Δ bin| / Σ bins, 50-bin photon flux
+
+
+def load(case):
+    z = np.load(os.path.join(GOLDEN, f"truth_{case}.npz"))
+    d = {k: z[k] for k in z.files}
+    d["params"] = {k[len("params_"):]: z[k].item() for k in z.files if k.startswith("params_")}
+    d["n"] = int(d["erg"].size)
+    return d
+
+
+def _pct(e):
+    e = np.asarray(e, np.float64)
+    return [float(v) for v in np.percentile(e, QS)] if e.size else [0.0] * len(QS)
+
+
+def _vec_rel(a, b, n):
+    a, b = np.asarray(a)[:3 * n].reshape(3, n), np.asarray(b)[:3 * n].reshape(3, n)
+    return np.abs(a - b).max(0) / np.linalg.norm(b, axis=0)
+
+
+def flux_of(status, x_end, k_end, rNS, nbins=50):
+    """The photon flux of art_flux_histogram (plot/flux.py:38-48) with unit weights."""
+    n = status.size
+    x, k = np.asarray(x_end).reshape(3, n), np.asarray(k_end).reshape(3, n)
+    sel = (status != ST_CROSSING) & (status != ST_TRUTH_SINGULAR) & (np.linalg.norm(x, axis=0) > 1.1 * rNS)
+    return np.histogram(np.arctan2(k[1, sel], k[0, sel]), nbins, range=(-np.pi, np.pi))[0].astype(np.float64)
+
+
+def compare(z, out):
+    """Errors of the run `out` (propagate_batch / oracle.propagate dict, capacity 1) against the
+    truth z. The run's flux is recomputed from its per-ray outputs over the rays whose truth is
+    not singular (test_gpu_truth.py checks the device histogram against the same recomputation
+    over all rays, bin for bin)."""
+    n = z["n"]
+    ts, gs = z["status"], np.asarray(out["status"])[:n]
+    valid = ts != ST_TRUTH_SINGULAR
+    rep = {"rays": n, "truth_singular": int((~valid).sum()),
+           "status_pairs": {f"{a}->{b}": int(((ts == a) & (gs == b)).sum())
+                            for a in (0, 1, 2) for b in range(5) if ((ts == a) & (gs == b)).any()}}
+    rep["status_mismatch"] = float(np.mean(ts[valid] != gs[valid]))
+    tc, gc = (ts == ST_CROSSING), (gs == ST_CROSSING)
+    rep["missed_crossings"] = int((tc & ~gc).sum())
+    rep["extra_crossings"] = int((valid & ~tc & gc).sum())
+    rep["truth_crossings"] = int(tc.sum())
+    rep["missed_frac"] = rep["missed_crossings"] / max(1, int(tc.sum()))
+    rep["extra_frac"] = rep["extra_crossings"] / max(1, int((valid & ~tc).sum()))
+    both = tc & gc
+    err = {}
+    err["crossing position"] = _vec_rel(out["xc_pos"], z["xc_pos"], n)[both]
+    err["crossing k"] = _vec_rel(out["xc_k"], z["xc_k"], n)[both]
+    for key, what in (("xc_t", "crossing t"), ("xc_dw", "crossing dw"), ("xc_p", "P_nonAD")):
+        a, b = np.asarray(out[key])[:n][both], z[key][both]
+        with np.errstate(divide="ignore", invalid="ignore"):
+            e = np.where(a == b, 0.0, np.abs(a - b) / np.abs(b))
+        err[what] = np.where(np.isnan(a) & np.isnan(b), 0.0, np.where(np.isnan(a) | np.isnan(b), 1.0, e))
+    ok = (ts == ST_SUCCESS) & (gs == ST_SUCCESS)
+    err["end position"] = _vec_rel(out["x_end"], z["x_end"], n)[ok]
+    err["end k"] = _vec_rel(out["k_end"], z["k_end"], n)[ok]
+    a, b = np.asarray(out["u7_end"])[:n][ok], z["u7_end"][ok]
+    err["end u7"] = np.abs(a - b) / np.abs(b)
+    rep["errors"] = {k: _pct(v) for k, v in err.items()}
+    rep["compared"] = {"crossings": int(both.sum()), "ends": int(ok.sum())}
+    f_truth = z["flux"]
+    f_run = flux_of(np.where(valid, gs, ST_TRUTH_SINGULAR), out["x_end"], out["k_end"], z["params"].get("rNS", 10.0))
+    rep["flux_l1"] = float(np.abs(f_run - f_truth).sum() / max(1.0, f_truth.sum()))
+    rep["flux_max_bin_diff"] = float(np.abs(f_run - f_truth).max())
+    return rep
+
+
+def check(rep, mode="reference"):
+    """The stated tolerance: raises AssertionError naming the quantity that exceeds it."""
+    assert rep["status_mismatch"] <= MAX_STATUS_MISMATCH[mode], ("status mismatch", rep)
+    assert rep["missed_frac"] <= MAX_MISSED_CROSSING[mode], ("missed crossings", rep)
+    assert rep["extra_frac"] <= MAX_EXTRA_CROSSING[mode], ("extra crossings", rep)
+    assert rep["flux_l1"] <= MAX_FLUX_L1[mode], ("flux", rep)
+    for what, (b50, b90, b99) in TOL[mode].items():
+        p50, p90, p99, _ = rep["errors"][what]
+        assert p50 <= b50 and p90 <= b90 and p99 <= b99, (mode, what, rep["errors"][what], TOL[mode][what])
