@@ -66,22 +66,35 @@ BYTES_PER_SEGMENT = 145 + 80
 BYTES_PER_CROSSING = 64
 
 
-def cpu_baseline(params, x0, k0, erg, seed, threads):
-    """The oracle (oracle/art_oracle.cpp, OpenMP over rays) on a bounded sample of the same
-    workload: the first rays of the same Philox-sampled forward-root batch, timed on this
-    box's host cores."""
+def cpu_baseline(params, x0, k0, erg, seed, threads, same_algorithm=True):
+    """A CPU figure on a bounded sample of the same workload (the first rays of the same
+    Philox-sampled forward-root batch), timed on this box's host cores.
+    same_algorithm: the engine's algorithm on the host (tools/cpu_same.cpp: art_core.h's
+    physics compiled for the CPU, scalar Vern6 + certified 50-point scan, OpenMP over rays);
+    else the oracle (oracle/art_oracle.cpp), whose dual-number gradients cost what the
+    reference's ForwardDiff passes do."""
     import oracle as O
     O.build()
     po = O.make_params(**params)
     n = erg.size
-    t0 = time.perf_counter()
-    r = O.propagate(po, x0, k0, erg, -1.0, -30.0, 1, max_crossings=-1, nthreads=threads)
+    if same_algorithm:
+        sys.path.insert(0, os.path.join(HERE, "tools"))
+        import cpu_same
+        cpu_same.build()
+        t0 = time.perf_counter()
+        r = cpu_same.propagate(po, x0, k0, erg, -1.0, -30.0, 1, max_crossings=-1, nthreads=threads)
+        what = ("the engine's algorithm on the host (tools/cpu_same.cpp: art_core.h compiled for the CPU, scalar "
+                "Vern6 + certified 50-point scan + re-step polish, OpenMP over rays)")
+    else:
+        t0 = time.perf_counter()
+        r = O.propagate(po, x0, k0, erg, -1.0, -30.0, 1, max_crossings=-1, nthreads=threads)
+        what = "oracle restatement (C++/OpenMP, dual-number gradients like the reference's ForwardDiff)"
     dt = time.perf_counter() - t0
     steps = int(r["n_accept"].sum())
     return {"value": steps / dt, "unit": "ray-steps/s", "cores": threads, "kind": "port",
+            "variant": "same-algorithm" if same_algorithm else "forwarddiff-restatement",
             "sample": f"first {n} forward-root photon segments of the seed-{seed} batch, {steps} accepted Vern6 "
-                      f"steps in {dt:.1f} s on {threads} thread(s); oracle restatement (C++/OpenMP, dual-number "
-                      f"gradients like ForwardDiff)"}
+                      f"steps in {dt:.1f} s on {threads} thread(s); {what}"}
 
 
 def host_cores():
@@ -180,8 +193,12 @@ def main():
     ap.add_argument("--streams", type=int, default=0,
                     help="device-resident side figure: batches in flight (HIP streams); 0: 1 for per-GPU batches "
                          "of >= 8e6 rays, else 4 (16 for the GR configs)")
-    ap.add_argument("--cpu-rays", type=int, default=int(os.environ.get("ART_CPU_RAYS", "500000")))
-    ap.add_argument("--cpu-rays-1t", type=int, default=int(os.environ.get("ART_CPU_RAYS_1T", "24000")))
+    # CPU samples (about 5-15 s each on the GPU box's 16 cores): the same-algorithm port on all
+    # cores and on one, then the dual-number oracle on all cores and on one
+    ap.add_argument("--cpu-rays", type=int, default=int(os.environ.get("ART_CPU_RAYS", "3000000")))
+    ap.add_argument("--cpu-rays-1t", type=int, default=int(os.environ.get("ART_CPU_RAYS_1T", "300000")))
+    ap.add_argument("--cpu-rays-oracle", type=int, default=int(os.environ.get("ART_CPU_RAYS_ORACLE", "250000")))
+    ap.add_argument("--cpu-rays-oracle-1t", type=int, default=int(os.environ.get("ART_CPU_RAYS_ORACLE_1T", "12000")))
     ap.add_argument("--donate", type=int, default=-1,
                     help="tail donation lanes for the device-resident passes in flight; -1: auto")
     ap.add_argument("--inflight", type=int, default=0,
@@ -448,6 +465,9 @@ def main():
             "status_counts": np.bincount(host_status, minlength=5).tolist(),
             "attempts_per_ray": attempt_dist,
             "flux_hist_sum": float(flux_red["host"].sum()),
+            "flux_hist": np.asarray(flux_red["host"].cpu() if hasattr(flux_red["host"], "cpu") else flux_red["host"],
+                                    np.float64).reshape(-1).tolist(),
+            "totals": {"rays": int(total_rays), "accepted_steps_per_pass": int(host_steps_total // args.steps)},
             "ic_sampling_s": sample_s,
         }
         if dev:
@@ -483,11 +503,14 @@ def main():
                 ks = h["k0"].reshape(3, n)[:, :m].reshape(-1).copy()
                 return xs, ks, h["erg"][:m].copy()
             cfg = CONFIGS[args.config] | {"integrator": 0}
-            m = min(args.cpu_rays, n)
-            line["cpu_baseline"] = cpu_baseline(cfg, *sample(m), args.seed, threads)
+            line["cpu_baseline"] = cpu_baseline(cfg, *sample(min(args.cpu_rays, n)), args.seed, threads)
             # and one core: the reference's own model is one single-threaded process per ray batch
-            m1 = min(args.cpu_rays_1t, n)
-            line["cpu_baseline"]["one_thread"] = cpu_baseline(cfg, *sample(m1), args.seed, 1)
+            line["cpu_baseline"]["one_thread"] = cpu_baseline(cfg, *sample(min(args.cpu_rays_1t, n)), args.seed, 1)
+            # the ForwardDiff-like restatement (the reference's per-RHS cost: three dual-number passes)
+            fd = cpu_baseline(cfg, *sample(min(args.cpu_rays_oracle, n)), args.seed, threads, same_algorithm=False)
+            fd["one_thread"] = cpu_baseline(cfg, *sample(min(args.cpu_rays_oracle_1t, n)), args.seed, 1,
+                                            same_algorithm=False)
+            line["cpu_baseline"]["forwarddiff_restatement"] = fd
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
