@@ -8,9 +8,17 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB_DIR = os.path.join(HERE, "lib")
 LIB = os.path.join(LIB_DIR, "libart.so")
-SOURCES = ["art_kernels.hip", "art_capi.cpp", "art_forest.cpp"]
+SOURCES = ["art_kernels.hip", "art_capi.cpp", "art_forest.cpp", "art_helpers.hip"]
 HEADERS = ["art_core.h", "art_internal.h", "art_event.h"]
 ARCH = os.environ.get("ART_OFFLOAD_ARCH", "gfx950")
+# -ffp-contract=on: FMA fusion within one source expression only ("FMA contraction").
+# -amdgpu-use-amdgpu-trackers: AMDGPU's own register-pressure trackers in the machine scheduler:
+#   fewer spills of the 256-VGPR integrator and 1% faster (A/B on the 1e7-ray flat batch, round 3).
+# art_helpers.hip adds -disable-machine-licm (see its header): MachineLICM hoisted the loop's
+#   polynomial constants into ~150 VGPRs live across the helper's ray loop, which then spilled to
+#   scratch at 2 waves per SIMD. Only that translation unit: the integrator runs 3% faster with it.
+FLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=on", "-mllvm", "-amdgpu-use-amdgpu-trackers=1"]
+TU_FLAGS = {"art_helpers.hip": ["-mllvm", "-disable-machine-licm"]}
 
 
 def _hipcc():
@@ -32,26 +40,39 @@ def build(force=False, verbose=False):
     if not force and not stale():
         return LIB
     os.makedirs(LIB_DIR, exist_ok=True)
-    # AMDGPU's own register-pressure trackers in the machine scheduler: fewer spills of the
-    # 256-VGPR integrator and 1% faster (A/B on the 1e7-ray flat batch, round 3)
-    cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=on",
-           "-mllvm", "-amdgpu-use-amdgpu-trackers=1",
-           *[os.path.join(CSRC, s) for s in SOURCES], "-o", LIB + ".tmp"]
+    _compile_link(LIB, (), (), verbose)
+    return LIB
+
+
+def _compile_link(out, defines, extra, verbose=False):
+    """Each translation unit compiled on its own (in parallel, its TU_FLAGS added), then linked."""
+    obj_dir = os.path.join(os.path.dirname(os.path.abspath(out)), "obj_" + os.path.basename(out))
+    os.makedirs(obj_dir, exist_ok=True)
+    procs, objs = [], []
+    for src in SOURCES:
+        obj = os.path.join(obj_dir, src + ".o")
+        cmd = [_hipcc(), f"--offload-arch={ARCH}", *FLAGS, *TU_FLAGS.get(src, []), *[f"-D{d}" for d in defines],
+               *extra, "-c", os.path.join(CSRC, src), "-o", obj]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        procs.append(subprocess.Popen(cmd))
+        objs.append(obj)
+    bad = [p.args for p in procs if p.wait() != 0]
+    if bad:
+        raise subprocess.CalledProcessError(1, bad[0])
+    cmd = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", out + ".tmp"]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
-    os.replace(LIB + ".tmp", LIB)
-    return LIB
+    os.replace(out + ".tmp", out)
+    shutil.rmtree(obj_dir, ignore_errors=True)
 
 
 def build_variant(out, defines=(), extra=()):
     """Dev builds (tools/gpu_final.sh: the section-timing one): the same sources with extra -D defines / flags into
     `out` (e.g. tools/build/libart_x.so, loaded with ART_LIB)."""
     os.makedirs(os.path.dirname(os.path.abspath(out)), exist_ok=True)
-    cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=on",
-           "-mllvm", "-amdgpu-use-amdgpu-trackers=1", *[f"-D{d}" for d in defines], *extra,
-           *[os.path.join(CSRC, s) for s in SOURCES], "-o", out]
-    subprocess.run(cmd, check=True)
+    _compile_link(out, defines, extra)
     return out
 
 

@@ -57,6 +57,10 @@ struct LaunchRec {
   int grid = 0;
   hipStream_t stream = nullptr;
   bool pending = false;
+  // an asynchronous host call holds its record from its launch until it latches it at its end
+  // (latch_launch / finish_timing_slot): take_slot skips a held record, so the ring wrapping
+  // under other launches cannot hand it out twice
+  std::atomic<bool> held{false};
 };
 
 struct Pinned {
@@ -186,6 +190,7 @@ int current_ctx(DeviceCtx** out) {
 
 // The next launch record: waits for the launch that used the slot RING launches ago.
 int take_slot(DeviceCtx* c, LaunchRec** out) {
+  for (int k = 0; k < RING && c->ring[c->next].held.load(std::memory_order_acquire); ++k) c->next = (c->next + 1) % RING;
   LaunchRec& L = c->ring[c->next];
   if (L.pending) {
     HIP_OK(hipEventSynchronize(L.done));
@@ -500,7 +505,7 @@ bool use_small_tail(const art_params* p, int64_t n, const TrajArgs& tr) {
   return tr.ntimes == 0 && p->integrator == ART_VERN6 && n <= art::small_tail_limit();
 }
 
-// this launch's scratch: [queue head + statistics (256 B) | u0: 16n doubles of fresh state
+// this launch's scratch: [queue head + statistics (256 B) | u0: U0_REC n doubles of fresh state
 // (init_kernel -> the integrator) | END_REC n doubles of end records | X_REC cap n doubles of
 // crossing records (the integrator -> finalize_kernel) | donation records of two levels]
 struct ScratchLayout {
@@ -509,7 +514,7 @@ struct ScratchLayout {
 };
 int scratch_layout(DeviceCtx* c, int64_t n, int cap, int32_t donate, ScratchLayout* L, bool small_tail = false) {
   const size_t nd = (size_t)n;
-  L->u0b = nd * 16 * sizeof(double);
+  L->u0b = nd * art::U0_REC * sizeof(double);
   L->recb = nd * art::END_REC * sizeof(double);
   L->xrb = (size_t)cap * nd * art::X_REC * sizeof(double);
   // tail donation: at most (resident waves) x donate records of CONT_REC doubles; a small batch
@@ -624,6 +629,7 @@ int finish_timing_slot(DeviceCtx* c, LaunchRec* Lp) {
   g_last_ms = ms;
   g_last_grid = L.grid;
   for (int i = 0; i < art::N_STATS; ++i) g_last_stats[i] = L.host_stats[i];
+  L.held.store(false, std::memory_order_release);
   return ART_OK;
 }
 int finish_timing(DeviceCtx* c) { return finish_timing_slot(c, nullptr); }
@@ -760,7 +766,10 @@ int art_recent_kernel_span_ms(int32_t n, double* ms) {
     LaunchRec& L = c->ring[(int)(((int64_t)c->last - (m - 1 - j) + RING) % RING)];
     HIP_OK(hipEventSynchronize(L.done));
     const unsigned long long t0 = ~L.host_stats[art::ST_T0], t1 = L.host_stats[art::ST_T1];
-    ms[j] = (L.host_stats[art::ST_T0] == 0ull || t1 < t0) ? -1.0 : (double)(t1 - t0) / art::STAMP_TICKS_PER_MS;
+    // (-1 also for an asynchronous call still in flight: its stamps are latched at its end)
+    ms[j] = (L.held.load(std::memory_order_acquire) || L.host_stats[art::ST_T0] == 0ull || t1 < t0)
+                ? -1.0
+                : (double)(t1 - t0) / art::STAMP_TICKS_PER_MS;
   }
   return (int)m;
 }
@@ -1085,9 +1094,12 @@ int lane_setup(DeviceCtx* c, HostLane* H) {
     HIP_OK(hipStreamCreateWithFlags(&H->m_dn, hipStreamNonBlocking));
   }
   if (!H->hsig) {
-    HIP_OK(hipHostMalloc((void**)&H->hsig, sizeof(unsigned long long) * HSIG_WORDS, hipHostMallocCoherent | hipHostMallocMapped));
-    std::memset(H->hsig, 0, sizeof(unsigned long long) * HSIG_WORDS);  // ([HSIG_RESIDENT] is never reset)
-    HIP_OK(hipHostGetDevicePointer((void**)&H->hsig_dev, H->hsig, 0));
+    unsigned long long* hs = nullptr;
+    HIP_OK(hipHostMalloc((void**)&hs, sizeof(unsigned long long) * HSIG_WORDS, hipHostMallocCoherent | hipHostMallocMapped));
+    std::memset(hs, 0, sizeof(unsigned long long) * HSIG_WORDS);  // ([HSIG_RESIDENT] is never reset)
+    HIP_OK(hipHostGetDevicePointer((void**)&H->hsig_dev, hs, 0));
+    // (published last, with release: another lane's worker reads the pointer in prev_resident)
+    __atomic_store_n(&H->hsig, hs, __ATOMIC_RELEASE);
   }
   if (!H->abort_host) {
     HIP_OK(hipHostMalloc((void**)&H->abort_host, 64, hipHostMallocCoherent | hipHostMallocMapped));
@@ -1107,6 +1119,7 @@ int latch_launch(DeviceCtx* c, LaunchRec* L, const unsigned long long* st) {
   g_last_ms = ms;
   g_last_grid = L->grid;
   for (int i = 0; i < art::N_STATS; ++i) g_last_stats[i] = st[i];
+  L->held.store(false, std::memory_order_release);
   return ART_OK;
 }
 
@@ -1137,9 +1150,9 @@ int propagate_host_maskless(DeviceCtx* c, HostLane* H, bool overlap, int64_t tic
   const size_t stride = up(out_bytes((int64_t)1 << shift));
   // scratch: head [queue | stats (10) | init_next (16) fin_next (17) chunk misses (18) exit count (19) waves done (20)
   // waves started (21) |
-  // finished rays per piece from word 32 | finalized tiles per piece from word 96] | chunk flags | u0 16n | rec 16n | xrec
+  // finished rays per piece from word 32 | finalized tiles per piece from word 96] | chunk flags | u0 U0_REC n | rec 16n | xrec
   const size_t nchunk = (nd + art::CHUNK - 1) / art::CHUNK;
-  const size_t head = 2048, ccb = up(nchunk * sizeof(unsigned)), u0b = nd * 16 * sizeof(double),
+  const size_t head = 2048, ccb = up(nchunk * sizeof(unsigned)), u0b = nd * art::U0_REC * sizeof(double),
                recb = nd * art::END_REC * sizeof(double);
   const size_t xrb = (size_t)cap * nd * art::X_REC * sizeof(double);
   // ART_HOST_DIRECT=1: the pieces' output blobs in pinned host memory (fine-grained), written by the
@@ -1264,9 +1277,14 @@ int propagate_host_maskless(DeviceCtx* c, HostLane* H, bool overlap, int64_t tic
   int ncu = 0;
   HIP_OK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device));
   const int slots = std::max(2, env_int("ART_HOST_BLOCKS", 2 * ncu));  // block slots: 2 per CU
-  // helper blocks beside the integrator (ART_HOST_HELPERS, default 8): launched first, and the
-  // integrator only once every one of them is resident, so it cannot take their slots
-  const int helpers = std::min(slots - 1, std::max(1, env_int("ART_HOST_HELPERS", 8)));
+  // helper blocks beside the integrator (ART_HOST_HELPERS, default 16): launched first, and the
+  // integrator only once every one of them is resident, so it cannot take their slots. Each helper
+  // block (2 waves per SIMD, the top issue priority) shares a CU with one integrator block, so it
+  // costs one integrator block slot, not a CU: 1e7 rays, 3 rounds on one box, the integrator 92.1-
+  // 93.4 -> 88.2-89.0 ms and the call 95.3-96.0 -> 91.1-92.1 ms with 16 helpers; 8 helpers let the
+  // finalize lag (109 ms calls), 12 and 24 are between (profiles/r06j_helpers.jsonl)
+  const int hw = art::helper_waves_per_simd(K);
+  const int helpers = std::min(slots - 1, std::max(1, env_int("ART_HOST_HELPERS", hw == 2 ? 16 : 8)));
   so.helpers = helpers;
   // (dev, ART_HOST_STREAM_SERIAL=1: no persistent helpers -- every tile initialised before the
   // integrator and finalized after it, kernel by kernel: for a counter-collection run, which
@@ -1276,7 +1294,8 @@ int propagate_host_maskless(DeviceCtx* c, HostLane* H, bool overlap, int64_t tic
   // overlaps the next one (art_propagate_host_flux_async): then the next call's integrator would
   // hold those slots, and the helpers finalize alone
   const bool final_pass = serial || !overlap;
-  const int iblocks = serial ? slots : slots - helpers;
+  // (a 1-wave/SIMD helper block holds a whole CU: two integrator block slots)
+  const int iblocks = serial ? slots : slots - (hw == 2 ? helpers : 2 * helpers);
   so.exit_expected = (serial ? 0 : helpers) + (final_pass ? slots : 0);
   hipEvent_t ev_zero = H->pev[nu + np];  // (the helpers start on zeroed counters)
   HIP_OK(hipEventRecord(ev_zero, H->m_comp));
@@ -1287,6 +1306,12 @@ int propagate_host_maskless(DeviceCtx* c, HostLane* H, bool overlap, int64_t tic
   // (a lone call), else from the upload loop as soon as they are (a call overlapping the previous
   // one, whose blocks hold the slots until its drain)
   LaunchRec* L = nullptr;
+  struct ReleaseRec {  // a call that leaves before latching its record frees it for take_slot
+    LaunchRec*& L;
+    ~ReleaseRec() {
+      if (L) L->held.store(false, std::memory_order_release);
+    }
+  } release_rec{L};
   bool launched = false;
   auto helpers_in = [&] { return serial || __atomic_load_n(hflag + HSIG_NFLAG, __ATOMIC_ACQUIRE) >= (unsigned long long)helpers; };
   // A call in flight launches its init pass and integrator only once the previous call's integrator
@@ -1296,15 +1321,18 @@ int propagate_host_maskless(DeviceCtx* c, HostLane* H, bool overlap, int64_t tic
   // (1.25e6 rays: calls of 28 instead of 14 ms, profiles/r05t_ab_helpers.txt). Bounded: 200 ms.
   auto prev_resident = [&] {
     if (!overlap || ticket <= 0 || c->done_ticket.load() >= ticket - 1 || clk() - t_start > 200.0) return true;
-    for (const HostLane& O : c->lanes)
-      if (&O != H && O.hsig && __atomic_load_n(O.hsig + HSIG_RESIDENT, __ATOMIC_ACQUIRE) >= (unsigned long long)ticket)
+    for (const HostLane& O : c->lanes) {
+      unsigned long long* const os = __atomic_load_n(&O.hsig, __ATOMIC_ACQUIRE);
+      if (&O != H && os && __atomic_load_n(os + HSIG_RESIDENT, __ATOMIC_ACQUIRE) >= (unsigned long long)ticket)
         return true;
+    }
     return false;
   };
   auto launch_main = [&]() -> int {
     std::lock_guard<std::mutex> rlk(g_ring_mu);
     int r = take_slot(c, &L);
     if (r) return r;
+    L->held.store(true, std::memory_order_release);  // until this call latches it (or leaves early)
     // every block slot initialises the first upload unit's rays before the integrator starts, then
     // the helpers keep ahead. (Round 4 took 258k rays, two per integrator lane: the first unit alone
     // left the integrator waiting on 8 helpers, 33 ms against 18 per 1.25e6-ray call. With the

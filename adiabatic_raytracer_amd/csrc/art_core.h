@@ -897,43 +897,6 @@ __host__ __device__ inline int scan_certified_code(const KParams& P, const doubl
   return 0;
 }
 
-#ifdef ART_COUNT_SUB
-// dev: why a step was not certified. Bit 0: the two-sided bmin <= 0; bit 1: the positive
-// test's ratio lhs/rhs in (0.5, 1]; bit 2: the negative test's ratio in (0.5, 1]; bit 3: u7
-// too close to the shell (elo² <= cert_e2); bit 4: positive ratio <= 0.5 with bmin > 0.
-__host__ __device__ inline int scan_cert_diag(const KParams& P, const double* u0, const double* f0,
-                                              const double* u1, const double* f1, double h, double b1, double t1,
-                                              double b0) {
-  const Hull r = bernstein_hull(u0[0], f0[0], u1[0], f1[0], h);
-  const Hull e = bernstein_hull(u0[6], f0[6], u1[6], f1[6], h);
-  const double elo = e.lo > 0.0 ? e.lo : (e.hi < 0.0 ? -e.hi : 0.0);
-  const double ehi = fmax(fabs(e.lo), fabs(e.hi));
-  int d = (elo * elo > P.cert_e2) ? 0 : 8;
-  const Hull th = bernstein_hull(u0[1], f0[1], u1[1], f1[1], h);
-  const Hull ph = bernstein_hull(u0[2], f0[2], u1[2], f1[2], h);
-  const double dth = fmax(th.hi - u1[1], u1[1] - th.lo);
-  const double dps = fmax(ph.hi - u1[2], u1[2] - ph.lo) + fabs(P.omega) * t1 * h * (1.0 + 1e-12);
-  const double db = 3.0 * dth + 1.5 * fabs(P.sm) * dps + 1e-12;
-  double bmax = fmin(2.0, fabs(b1) + db), bmin = fabs(b1) - db;
-  if (b0 == b0) {
-    const double h3 = h * (1.0 / 3.0);
-    const double tvt = fabs(h3 * f0[1]) + fabs((u1[1] - h3 * f1[1]) - (u0[1] + h3 * f0[1])) + fabs(h3 * f1[1]);
-    const double tvp = fabs(h3 * f0[2]) + fabs((u1[2] - h3 * f1[2]) - (u0[2] + h3 * f0[2])) + fabs(h3 * f1[2]);
-    const double ell = (3.0 * tvt + 1.5 * fabs(P.sm) * (tvp + fabs(P.omega) * t1 * h)) * (1.0 + 1e-12) + 1e-12;
-    const double lo = 0.5 * (b0 + b1 - ell), hi = 0.5 * (b0 + b1 + ell);
-    bmax = fmin(bmax, fmax(fabs(lo), fabs(hi)));
-    bmin = fmax(bmin, lo > 0.0 ? lo : (hi < 0.0 ? -hi : 0.0));
-  }
-  if (!(bmin > 0.0)) d |= 1;
-  const double neg = P.wp2n * bmax * P.cert_fac / (P.mass_a2 * (r.lo * r.lo * r.lo));
-  if (neg >= 1.0 && neg < 2.0) d |= 4;
-  const double grr_lo = P.rs_eff == 0.0 ? 1.0 : 1.0 - P.rs_eff / r.lo;
-  const double pos = P.wp2n * bmin * grr_lo / (ehi * ehi * P.cert_fac * (r.hi * r.hi * r.hi));
-  if (pos > 0.5 && pos <= 1.0) d |= 2;
-  if (bmin > 0.0 && pos <= 0.5) d |= 16;
-  return d;
-}
-#endif
 
 template <class T>
 __host__ __device__ inline T condition(const KParams& P, const T* u, const T& tau) {

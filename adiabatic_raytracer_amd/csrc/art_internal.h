@@ -9,7 +9,9 @@ namespace art {
 struct SegIn {
   const double *x0, *k0, *erg, *dw, *lnt0;
   const int8_t* species;
-  double* u0;  // 16n device scratch filled by init_kernel: u0 (7), f(u0) (7), dt, c0
+  // device scratch filled by the init pass: one U0_REC-double fresh-state record per ray
+  // (fresh_rec below), so a refilling lane reads its ray with 10 16-byte loads from two lines
+  double* u0;
 };
 
 struct SegOut {
@@ -122,6 +124,9 @@ constexpr int FLUX_HELPER_BINS = 256;  // flux bins the helpers bin themselves (
 constexpr int DONE_STATS = 1, DONE_FLUX = 16;  // done_host layout: [0] flag | [1, 11) statistics | [16, 16 + 2 nbins) flux
 constexpr int CHUNK = 64;  // rays a persistent wave claims from the queue at once
 constexpr int HELPER_TILE = 1024;  // rays a helper block initialises or finalizes per claim
+// The fresh state of ray i at u0 + i U0_REC (init_one writes it, a refilling integrator lane
+// reads it): [u0 (7) | f(u0) (7) | dt | c0 | erg | ln t0 | species | 0], 160 bytes, 32-byte aligned.
+constexpr int U0_REC = 20;
 constexpr int END_REC = 16;
 constexpr int X_REC = 8;
 constexpr int CONT_REC = 24;  // [u (7) | f (7) | τ, dt, qpow, cprev, bstart, erg | int4 {ray, n_acc, n_rej, ncross} | int4 {iter, sprev, flags, save_k}]
@@ -149,6 +154,13 @@ hipError_t launch_integrator_streamed(const KParams& P, int64_t n, const SegIn& 
 // announce counts each block into host_flags[64] as it starts.
 hipError_t launch_helpers(const KParams& P, int64_t n, const SegIn& in, const SegOut& out, int blocks, int64_t init_limit,
                           int announce, unsigned long long* stats, hipStream_t s);
+// The helper kernel (art_helpers.hip, its own translation unit): the instantiation for these
+// parameters' geometry, and its waves per SIMD (2: a helper block shares its CU with one
+// integrator block; 1: it takes the whole CU).
+using HFn = void (*)(const KParams, const int64_t, const SegIn, const SegOut, const int, const int64_t, const int64_t,
+                     const int64_t, const int, unsigned long long*);
+HFn pick_helper(const KParams& P);
+int helper_waves_per_simd(const KParams& P);
 // The batch size up to which launch_propagate runs every ray on a wave of its own (tail_kernel):
 // ART_SMALL_TAIL, default one ray per SIMD of the device; 0 switches it off.
 int64_t small_tail_limit();

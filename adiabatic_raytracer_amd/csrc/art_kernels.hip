@@ -13,6 +13,8 @@
 //     state and its crossings (Σ ≈ 220 B per segment).
 #include <hip/hip_runtime.h>
 
+#include <atomic>
+
 #include <cstdio>
 #include <cstdlib>
 
@@ -27,22 +29,6 @@ namespace art {
 enum { ST_ATTEMPTS = 0, ST_ACCEPTED, ST_ROOT_STEPS, ST_SCAN_EVALS, ST_INTERP_EVALS, ST_RAYS, ST_INIT_RHS, ST_CERT,
        ST_NSTATS = 8 };
 
-#ifdef ART_TRACE
-// dev build: per-attempt state of ONE ray (g_trace_ray) from whichever kernel integrates it:
-// [kernel (0 bulk, 1 tail), mode, hs, tau, EEst2, y (7), kk (7)] per attempt
-__device__ int g_trace_ray = -1;
-__device__ unsigned g_trace_n = 0;
-constexpr int TRACE_REC = 21, TRACE_MAX = 4096;
-__device__ double g_trace[TRACE_MAX * TRACE_REC];
-__device__ inline void trace_attempt(int kern, int mode, double hs, double tau, double e2, const double* y,
-                                     const double* kk) {
-  const unsigned k = atomicAdd(&g_trace_n, 1u);
-  if (k >= TRACE_MAX) return;
-  double* r = g_trace + (size_t)k * TRACE_REC;
-  r[0] = kern; r[1] = mode; r[2] = hs; r[3] = tau; r[4] = e2;
-  for (int i = 0; i < 7; ++i) { r[5 + i] = y[i]; r[12 + i] = kk[i]; }
-}
-#endif
 
 // ---------------------------------------------------------------------------
 // One Verner 6(5) attempt from (u, k1 = f(u)) over h: writes u_{n+1}, its FSAL derivative
@@ -203,16 +189,20 @@ __device__ inline unsigned sign_code_nd(double N, double D) {
   return sign_code(0.5 * N / D);
 }
 
-// ode_determine_initdt (DiffEqBase) for an order-6 method; one extra RHS evaluation.
-__device__ inline double initdt(const KParams& P, bool photon, double erg, const double* u0, const double* f0,
-                                double tau0, double dtmax, int& probe) {
-  probe = 0;
-  double d0 = 0.0, d1 = 0.0, sk[7];
+// ode_determine_initdt (DiffEqBase) for an order-6 method, in two halves around its one extra RHS
+// evaluation (init_one evaluates both RHS at ONE inlined site). initdt_begin returns the step when
+// no probe is needed, else NaN with the probe point u1 = u0 + dt0 f0 at tau0 + dt0.
+struct InitDt {
+  double sk[7], d1, dt0;
+};
+__device__ inline double initdt_begin(const KParams& P, const double* u0, const double* f0, double tau0, double dtmax,
+                                      InitDt& s, double* u1) {
+  double d0 = 0.0, d1 = 0.0;
 #pragma unroll
   for (int i = 0; i < 7; ++i) {
-    sk[i] = P.abstol + fabs(u0[i]) * P.reltol;
-    d0 += (u0[i] / sk[i]) * (u0[i] / sk[i]);
-    d1 += (f0[i] / sk[i]) * (f0[i] / sk[i]);
+    s.sk[i] = P.abstol + fabs(u0[i]) * P.reltol;
+    d0 += (u0[i] / s.sk[i]) * (u0[i] / s.sk[i]);
+    d1 += (f0[i] / s.sk[i]) * (f0[i] / s.sk[i]);
   }
   d0 = sqrt(d0 / 7.0);
   d1 = sqrt(d1 / 7.0);
@@ -221,24 +211,26 @@ __device__ inline double initdt(const KParams& P, bool photon, double erg, const
   const double at = fabs(tau0);
   const double eps_t = nextafter(at, INFINITY) - at;
   if (dt0 < 10.0 * eps_t) return fmax(1e-6, P.dtmin);
-  double u1[7], f1[7];
 #pragma unroll
   for (int i = 0; i < 7; ++i) u1[i] = u0[i] + dt0 * f0[i];
-  rhs(P, photon, u1, tau0 + dt0, erg, f1);
-  probe = 1;
+  s.d1 = d1;
+  s.dt0 = dt0;
+  return NAN;
+}
+__device__ inline double initdt_end(const KParams& P, const double* f0, const double* f1, double dtmax, const InitDt& s) {
   bool same = true;
   double d2 = 0.0;
 #pragma unroll
   for (int i = 0; i < 7; ++i) {
     same = same && (f0[i] == f1[i]);
-    const double q = (f1[i] - f0[i]) / sk[i];
+    const double q = (f1[i] - f0[i]) / s.sk[i];
     d2 += q * q;
   }
-  if (same) return fmax(P.dtmin, 100.0 * dt0);
-  d2 = sqrt(d2 / 7.0) / dt0;
-  const double mx = fmax(d1, d2);
-  const double dt1 = (mx <= 1e-15) ? fmax(1e-6, dt0 * 1e-3) : pow(10.0, -(2.0 + log10(mx)) / 6.0);
-  return fmax(P.dtmin, fmin(fmin(100.0 * dt0, dt1), dtmax));
+  if (same) return fmax(P.dtmin, 100.0 * s.dt0);
+  d2 = sqrt(d2 / 7.0) / s.dt0;
+  const double mx = fmax(s.d1, d2);
+  const double dt1 = (mx <= 1e-15) ? fmax(1e-6, s.dt0 * 1e-3) : pow(10.0, -(2.0 + log10(mx)) / 6.0);
+  return fmax(P.dtmin, fmin(fmin(100.0 * s.dt0, dt1), dtmax));
 }
 
 // Root of the condition along the Hermite interpolant inside (tha, thb] (Illinois).
@@ -328,6 +320,7 @@ struct StageTable {
   double e_f, e_A, e_L[LDS_SLOTS], e_k;  // error weights (Vern6): btilde of f, kA(=k8), L, k9
 };
 
+#ifndef ART_HELPER_TU  // (art_helpers.hip compiles the helper kernel alone, see there)
 __constant__ StageTable c_vern6 = {
     // {cf = a_{s+2,1}, cA (k2 for slots 0..6, k8 for slot 7), ct, lmask, storeA, storeL}
     {{Vern6::a21, 0.0, Vern6::c2, 0x0, 1, -1, 0},
@@ -359,6 +352,7 @@ __constant__ StageTable c_rk4 = {
      {0, 0, 0, 0, 0}, {0, 0, 0, 0, 0}, {0, 0, 0, 0, 0}, {0, 0, 0, 0, 0}},
     0.0, 0.0, {0, 0, 0, 0, 0}, 0.0};
 
+#endif
 enum LaneMode { M_IDLE = 0, M_STEP = 2, M_ROOT = 3 };
 
 // Lanes per block of the persistent integrator. A block retires only when all its waves are
@@ -464,34 +458,46 @@ __device__ inline KParams specialize(const KParams& P) {
 // each chunk it claims): u0 (RayTracer.jl:179-216: k_norm_Cart onto the axion shell, Cartesian
 // -> (r, θ, φ), covariant celerity), f(u0) with the hamiltonian's in-place clamp (:531), the
 // initial dt (ode_determine_initdt, order 6, with its probe RHS; RK4: the fixed step) and the
-// condition value that seeds the callback's sign memory, into in.u0 = 16n doubles
-// [u0 (7) | f0 (7) | dt | c0]. Returns the RHS evaluations it took.
+// condition value that seeds the callback's sign memory, into the ray's fresh-state record
+// (U0_REC doubles at in.u0 + i U0_REC: [u0 (7) | f0 (7) | dt | c0 | erg | ln t0 | species | 0]),
+// ten 16-byte stores. Returns the RHS evaluations it took.
 __device__ inline unsigned init_one(const KParams& P, int64_t n, int64_t i, const SegIn& in) {
   const double xs[3] = {in.x0[i], in.x0[n + i], in.x0[2 * n + i]};
   const double ks[3] = {in.k0[i], in.k0[n + i], in.k0[2 * n + i]};
   const double erg = in.erg[i], tau = in.lnt0[i];
   const bool photon = in.species[i] != ART_AXION;
-  double u[7], f[7];
+  double u[7], f[7], y[7];
   initial_state(P, xs, ks, erg, in.dw[i], u);
-  rhs(P, photon, u, tau, erg, f);
-  unsigned nrhs = 1;
-  if (photon && u[0] < P.rNS) u[0] = P.rNS;  // hamiltonian's in-place clamp (:531)
-  double dt;
-  if (P.integrator == ART_RK4) {
-    dt = (P.ln_t_end - tau) / P.n_fixed;
-  } else {
-    int probe = 0;
-    dt = initdt(P, photon, erg, u, f, tau, P.ln_t_end - tau, probe);
-    nrhs += probe;
+  // pass 0: f(u0); pass 1 (Vern6, when initdt asks for it): its probe f(u1). One inlined RHS site:
+  // with two, the helper kernel needed more than the 256 VGPRs of 2 waves per SIMD and spilled
+  double dt = P.integrator == ART_RK4 ? (P.ln_t_end - tau) / P.n_fixed : NAN;
+  InitDt ids;
+  unsigned nrhs = 0;
+#pragma unroll
+  for (int c = 0; c < 7; ++c) y[c] = u[c];
+  double ty = tau;
+  for (int pass = 0; pass < 2; ++pass) {
+    double r[7];
+    rhs(P, photon, y, ty, erg, r);
+    ++nrhs;
+    if (pass == 0) {
+#pragma unroll
+      for (int c = 0; c < 7; ++c) f[c] = r[c];
+      if (photon && u[0] < P.rNS) u[0] = P.rNS;  // hamiltonian's in-place clamp (:531)
+      if (P.integrator == ART_RK4) break;
+      dt = initdt_begin(P, u, f, tau, P.ln_t_end - tau, ids, y);
+      if (!isnan(dt)) break;
+      ty = tau + ids.dt0;
+    } else {
+      dt = initdt_end(P, f, r, P.ln_t_end - tau, ids);
+    }
   }
   const double c0 = condition_t(P, u, fexp(tau));
+  const double v[U0_REC] = {u[0], u[1], u[2], u[3], u[4], u[5], u[6], f[0], f[1], f[2],
+                            f[3], f[4], f[5], f[6], dt,   c0,   erg,  tau,  photon ? 1.0 : 0.0, 0.0};
+  double2* rq = reinterpret_cast<double2*>(in.u0 + i * U0_REC);
 #pragma unroll
-  for (int c = 0; c < 7; ++c) {
-    in.u0[c * n + i] = u[c];
-    in.u0[(7 + c) * n + i] = f[c];
-  }
-  in.u0[14 * n + i] = dt;
-  in.u0[15 * n + i] = c0;
+  for (int c = 0; c < U0_REC / 2; ++c) rq[c] = make_double2(v[2 * c], v[2 * c + 1]);
   return nrhs;
 }
 
@@ -562,7 +568,7 @@ __device__ inline void finalize_one(const KParams& P, int64_t n, int64_t i, int6
   if (out.ntimes >= 2) {  // saveat: start (u0 back-transformed), interior to Cartesian, end
     double u0[7], xs[3], ks[3];
 #pragma unroll
-    for (int c = 0; c < 7; ++c) u0[c] = in.u0[c * n + i];
+    for (int c = 0; c < 7; ++c) u0[c] = in.u0[i * U0_REC + c];
     back_transform(P, u0, erg, xs, ks);
     const int mt = out.traj_n[o];
     for (int k = 0; k < mt; ++k) {
@@ -681,6 +687,7 @@ __device__ inline bool chunk_wait(const SegOut& out, int wnext, int leader) {
   return __shfl(ok, leader) != 0;
 }
 
+#ifndef ART_HELPER_TU
 // DON: the tail-donation instantiations (SegOut::donate / cont_mode honoured); the others
 // carry none of that code, so a lone pass pays nothing for it
 // WPS: waves per SIMD the registers are budgeted for (the default 2; the GR continuation
@@ -748,13 +755,9 @@ __global__ __launch_bounds__(BLOCK, WPS) void propagate_kernel(const KParams P_i
   int save_k = 1;  // SAVE: the next interior saveat index
   bool exhausted = false;
   unsigned s_att = 0, s_acc = 0, s_root = 0, s_scan = 0, s_interp = 0, s_rays = 0, s_cert = 0;
-#ifdef ART_SLOT_TIMING
-#define ART_SECTION_TIMING
-#endif
 #ifdef ART_SECTION_TIMING
   // dev build: s_memtime cycles per main-loop section, summed over the wave's iterations
-  // (ART_SLOT_TIMING: also the stage slots' parts, 8 combination, 9 RHS, 10 the rest)
-  unsigned long long t_sec[11] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long t_sec[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   unsigned long long t_last = __builtin_amdgcn_s_memtime();
 #define ART_TMARK(k)                                                  \
   {                                                                   \
@@ -765,30 +768,6 @@ __global__ __launch_bounds__(BLOCK, WPS) void propagate_kernel(const KParams P_i
 #else
 #define ART_TMARK(k)
 #endif
-#ifdef ART_SLOT_TIMING
-#define ART_SMARK(k) ART_TMARK(k)
-#else
-#define ART_SMARK(k)
-#endif
-#ifdef ART_COUNT_SUB
-  // dev: uncertified steps; all-positive ones; all-negative ones failing on u7 (cert_e2); all-
-  // positive positive-test near misses; all-negative ones; ones with a sign change; all-negative
-  // negative-test near misses
-  unsigned s_sub[7] = {0, 0, 0, 0, 0, 0, 0};
-#endif
-#ifdef ART_COUNT_PASSES
-  // dev: wave-level counts (lane 0): main iterations, grid passes, iterations with a grid pass,
-  // cooperative passes, iterations that refill, iterations with a code walk, fallback iterations
-  unsigned s_pc[7] = {0, 0, 0, 0, 0, 0, 0};
-#define ART_PC(k) \
-  if (lane == 0) s_pc[k] += 1;
-#else
-#define ART_PC(k)
-#endif
-#ifdef ART_COUNT_LOOPS
-  unsigned s_lane_it = 0, s_main_it = 0;  // dev counters: wave iterations of the per-lane and main loops
-  unsigned s_ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // per-lane evaluations by phase
-#endif
 #pragma unroll
   for (int i = 0; i < 7; ++i) { u[i] = 0.0; f[i] = 0.0; }
 
@@ -796,9 +775,6 @@ __global__ __launch_bounds__(BLOCK, WPS) void propagate_kernel(const KParams P_i
     // ---- refill idle lanes from the wave's chunk (one atomicAdd per 64 rays) ----
     if (!exhausted) {
       unsigned long long need = __ballot(mode == M_IDLE);
-#ifdef ART_COUNT_PASSES
-      if (need != 0ull) ART_PC(4)
-#endif
       while (need != 0ull) {
         if (wnext >= wend) {
           unsigned long long base = 0;
@@ -811,11 +787,7 @@ __global__ __launch_bounds__(BLOCK, WPS) void propagate_kernel(const KParams P_i
           cready = false;
         }
         int lim = wend;
-#ifndef ART_S_NOCHUNK  // (dev A/B: no chunk flags polled)
         if constexpr (DON == 3) {
-#else
-        if constexpr (DON == 99) {
-#endif
           // the chunk's fresh state (the helpers' chunk flag); while it is not in, a wave with
           // other rays goes on integrating them, and an empty wave waits (bounded)
           if (!cready) {
@@ -869,20 +841,29 @@ __global__ __launch_bounds__(BLOCK, WPS) void propagate_kernel(const KParams P_i
           ray = wnext + rank;
           mode = M_STEP;
           // fresh segment: u0, f(u0), the initial dt and the initial condition value, all
-          // precomputed by init_kernel
-          erg = in.erg[ray];
-          photon = in.species[ray] != ART_AXION;
+          // precomputed by the init pass, with erg, ln t0 and the species: one 160-byte record
+          const double2* rq = reinterpret_cast<const double2*>(in.u0 + (int64_t)ray * U0_REC);
+          double v[U0_REC - 2];
+#pragma unroll
+          for (int i = 0; i < U0_REC / 2 - 1; ++i) {
+            const double2 q = rq[i];
+            v[2 * i] = q.x;
+            v[2 * i + 1] = q.y;
+          }
+          const double sp = rq[U0_REC / 2 - 1].x;
 #pragma unroll
           for (int i = 0; i < 7; ++i) {
-            u[i] = in.u0[i * n + ray];
-            f[i] = in.u0[(7 + i) * n + ray];
+            u[i] = v[i];
+            f[i] = v[7 + i];
           }
-          dt = in.u0[14 * n + ray];
-          cprev = in.u0[15 * n + ray];
+          dt = v[14];
+          cprev = v[15];
+          erg = v[16];
+          tau = v[17];
+          photon = sp != 0.0;
           cprev_ok = true;
           bstart = NAN;
           sprev = isnan(cprev) ? 0 : sgn(cprev);
-          tau = in.lnt0[ray];
           n_acc = n_rej = ncross = iter = 0;
           save_k = 1;
           just_evented = false;
@@ -901,11 +882,7 @@ __global__ __launch_bounds__(BLOCK, WPS) void propagate_kernel(const KParams P_i
     const bool outlier = __ballot(iter >= ART_PRIO_ITERS) != 0ull;
     if (outlier) __builtin_amdgcn_s_setprio(2);
     else __builtin_amdgcn_s_setprio(0);
-    ART_PC(0)
     ART_TMARK(0)  // refill
-#ifdef ART_COUNT_LOOPS
-    if (lane == 0) s_main_it += 1;
-#endif
 
     // ---- this iteration's step size ----
     ART_LBOOL2 last = false, forced = false;
@@ -926,18 +903,10 @@ __global__ __launch_bounds__(BLOCK, WPS) void propagate_kernel(const KParams P_i
     // scalar-load latency hides behind the RHS instead of opening the next slot: 1e7 flat device
     // launch 84.0 -> 83.4 ms (3 interleaved pairs, profiles/r05c_ab_prefetch.jsonl); the GR build
     // (slot loop unrolled by two) lost 0.5% with it (profiles/r05d_ab_gr_prefetch.txt)
-#ifndef ART_NO_SLOT_PREFETCH
     constexpr bool PF = GEOM == GEOM_FLAT;
-#else
-    constexpr bool PF = false;
-#endif
     SlotRow Rnext = T.row[0];
 #pragma unroll SUNROLL
     for (int s = 0; s < NSLOT; ++s) {
-#ifdef ART_PRIO_GLUE  // (dev A/B) the stage combination's LDS reads at the high priority
-      if (outlier) __builtin_amdgcn_s_setprio(3);
-      else __builtin_amdgcn_s_setprio(1);
-#endif
       const SlotRow R = PF ? Rnext : T.row[s];
       const double cf = R.cf, cA = R.cA;
       double acc[7];
@@ -963,18 +932,12 @@ __global__ __launch_bounds__(BLOCK, WPS) void propagate_kernel(const KParams P_i
       for (int i = 0; i < 7; ++i) y[i] = u[i] + hs * acc[i];
       const double ty = tau + R.ct * hs;
       if constexpr (PF) Rnext = T.row[s + 1 < NSLOT ? s + 1 : s];
-      ART_SMARK(8)
-#ifdef ART_PRIO_GLUE
-      if (outlier) __builtin_amdgcn_s_setprio(2);
-      else __builtin_amdgcn_s_setprio(0);
-#endif
       // Every lane evaluates the photon RHS -- idle lanes (a draining wave) on stale state,
       // whose results nothing reads -- so the slot has no divergent control flow. Axion
       // segments (the tree driver's batches) take a wave-uniform detour and a select.
       double aux[2];
       if constexpr (GEOM != GEOM_ANY) rhs_photon_gj(P, y, ty, erg, kk, aux);
       else rhs_photon(P, y, ty, erg, kk, aux);
-      ART_SMARK(9)
       if (s == NSLOT - 1) {  // the end point's b and t for the scan certificate (lastv and codes are free)
         lastv[threadIdx.x] = aux[0];
         lastt[threadIdx.x] = aux[1];
@@ -994,10 +957,8 @@ __global__ __launch_bounds__(BLOCK, WPS) void propagate_kernel(const KParams P_i
 #pragma unroll
         for (int i = 0; i < 7; ++i) L[(sl * 7 + i) * BLOCK] = kk[i];
       }
-      ART_SMARK(10)
     }
     ART_TMARK(1)  // step size and stage slots
-#ifndef ART_NO_PRIO_PHASE
     // The rest of the iteration -- error norm, controller, certificate, scan, walk, refill --
     // is latency-bound (short dependent chains, LDS round trips, the loads of a refill), the
     // stage slots issue-bound. At a higher issue priority than the partner wave's stage slots,
@@ -1009,7 +970,6 @@ __global__ __launch_bounds__(BLOCK, WPS) void propagate_kernel(const KParams P_i
     // 81.42 (profiles/r04c_ab_grid_prio.txt). ART_NO_PRIO_PHASE switches it off (A/B).
     if (outlier) __builtin_amdgcn_s_setprio(3);
     else __builtin_amdgcn_s_setprio(1);
-#endif
     // y = u_{n+1}, kk = f(u_{n+1}) for stepping lanes
     // EEst² = mean of the 7 squared scaled errors: the controller needs EEst only through
     // EEst <= 1 and its logarithm (ln EEst = ½ ln EEst²), so no square root is taken
@@ -1031,9 +991,6 @@ __global__ __launch_bounds__(BLOCK, WPS) void propagate_kernel(const KParams P_i
           acc += q * q;
         }
         EEst2 = acc * (1.0 / 7.0);
-#ifdef ART_TRACE
-        if (ray == g_trace_ray) trace_attempt(0, mode, hs, tau, EEst2, y, kk);
-#endif
       }
     }
 
@@ -1102,9 +1059,6 @@ __global__ __launch_bounds__(BLOCK, WPS) void propagate_kernel(const KParams P_i
     const int ccode =
         !scan ? 0 : (cbs ? scan_certified_code(P, u, f, y, kk, hs, bend, lastt[threadIdx.x], bstart) : 3);
     const ART_LBOOL2 cert = ccode != 0;
-#ifdef ART_COUNT_SUB
-    const int cdiag = (scan && !cert) ? scan_cert_diag(P, u, f, y, kk, hs, bend, lastt[threadIdx.x], bstart) : 0;
-#endif
     s_cert += cert ? 1u : 0u;
     // every lane parks (u, f, y, kk, h, τ) in its LDS slots (free after the error estimate):
     // the scan reads the interpolants from there, and the registers stay free until the
@@ -1128,7 +1082,6 @@ __global__ __launch_bounds__(BLOCK, WPS) void propagate_kernel(const KParams P_i
     double gN0 = 0.0, gD0 = 1.0, gN1 = 0.0, gD1 = 1.0;
     ART_TMARK(2)  // error norm, controller, certificate and parking
     if ((smask | rmask) != 0ull) {
-      ART_PC(2)
       const int ns = __popcll(smask), nr = __popcll(rmask);
       if (grid) {
         srcl[wbase + __popcll(smask & ((1ull << lane) - 1ull))] = lane;
@@ -1142,13 +1095,8 @@ __global__ __launch_bounds__(BLOCK, WPS) void propagate_kernel(const KParams P_i
       const int tg = ns * nper, total = tg + nr;
       const int dj = ns ? 64 / ns : 0, dc = ns ? 64 % ns : 0;
       int c = ns ? lane % ns : 0, j = ns ? lane / ns + 1 : 0;
-#ifdef ART_PRIO_GRID0  // (dev A/B) the grid pass, dense VALU work, at the stage slots' priority
-      if (outlier) __builtin_amdgcn_s_setprio(2);
-      else __builtin_amdgcn_s_setprio(0);
-#endif
 #pragma unroll 1
       for (int w0 = 0; w0 < total; w0 += 64) {
-        ART_PC(1)
         const int t = w0 + lane;
         if (t < total) {  // one evaluation site for both kinds of item (no divergent second copy)
           const bool gi = t < tg;
@@ -1179,10 +1127,6 @@ __global__ __launch_bounds__(BLOCK, WPS) void propagate_kernel(const KParams P_i
           j += 1;
         }
       }
-#ifdef ART_PRIO_GRID0
-      if (outlier) __builtin_amdgcn_s_setprio(3);
-      else __builtin_amdgcn_s_setprio(1);
-#endif
       wave_lds_sync();
     }
 
@@ -1204,29 +1148,6 @@ __global__ __launch_bounds__(BLOCK, WPS) void propagate_kernel(const KParams P_i
 #pragma unroll
       for (int w = 0; w < SCAN_WORDS; ++w)
         cw[w] = cert ? 0x55555555u * (unsigned)ccode : codes[w * BLOCK + threadIdx.x];
-#ifdef ART_COUNT_SUB
-      // dev: what the uncertified steps are (see s_sub)
-      if (!cert) {
-        s_sub[0] += 1;
-        bool allp = true, alln = true, chg = false;
-        int ls = 0;
-        for (int q = 0; q < nper; ++q) {
-          const unsigned c0 = (cw[q >> 4] >> (2 * (q & 15))) & 3u;
-          allp = allp && c0 == 1u;
-          alln = alln && c0 == 2u;
-          const int si = c0 == 1u ? 1 : (c0 == 2u ? -1 : 0);
-          if (c0 == 3u) ls = 0;
-          if (si != 0 && ls != 0 && si != ls) chg = true;
-          if (si != 0) ls = si;
-        }
-        s_sub[1] += allp ? 1u : 0u;
-        s_sub[2] += (alln && (cdiag & 8)) ? 1u : 0u;  // all-negative, u7 too close to the shell
-        s_sub[3] += (allp && (cdiag & 2)) ? 1u : 0u;
-        s_sub[4] += alln ? 1u : 0u;
-        s_sub[5] += chg ? 1u : 0u;
-        s_sub[6] += (alln && (cdiag & 4)) ? 1u : 0u;  // all-negative, negative test within 2x
-      }
-#endif
       // fast path: every grid point has the previous sign (or the previous sign is unknown
       // and every point has one common nonzero sign)
       const unsigned s0 = cw[0] & 3u;
@@ -1267,12 +1188,6 @@ __global__ __launch_bounds__(BLOCK, WPS) void propagate_kernel(const KParams P_i
     ART_LBOOL2 hit = false, root_done = false;
     // a crossing in (θ_last, θ_ip]: polish it on the true trajectory (mode ROOT), from t_int
     auto open_root = [&](double t_int) {
-#ifdef ART_TRACE
-      if (ray == g_trace_ray) {
-        const double v[7] = {double(ip), double(last_j), last_c, i_cg, t_int, double(lc_ok), thgrid[ip]};
-        trace_attempt(10, mode, hs, tau, 0.0, v, v);
-      }
-#endif
       const double thg = thgrid[ip];
       const double last_th = thgrid[last_j];
       hit = true;
@@ -1356,9 +1271,6 @@ __global__ __launch_bounds__(BLOCK, WPS) void propagate_kernel(const KParams P_i
       polish(lastv[threadIdx.x]);
     }
     ART_TMARK(4)  // sign-code fast paths
-#ifdef ART_COUNT_PASSES
-    if (__ballot(ph == 2) != 0ull) ART_PC(5)
-#endif
     if (ph == 2) walk();
     ART_TMARK(5)  // code walk
     // (c0) The values a bracket (ph 5: at the change point and, when unknown, at the last
@@ -1403,7 +1315,6 @@ __global__ __launch_bounds__(BLOCK, WPS) void propagate_kernel(const KParams P_i
       const unsigned long long b1 = __ballot(nq >= 1), b2 = __ballot(nq == 2);
       const int total = __popcll(b1) + __popcll(b2);
       if (total > 0 && total <= 64) {
-        ART_PC(3)
         const int off = __popcll(b1 & lt) + __popcll(b2 & lt);
         wave_lds_sync();  // the walk's lastv reads are done
         if (nq >= 1) {
@@ -1446,12 +1357,6 @@ __global__ __launch_bounds__(BLOCK, WPS) void propagate_kernel(const KParams P_i
     //     point, 6 value at the bracket start, 7 value at the step's last nonzero point.
 #pragma unroll 1
     while (ph != 0) {
-#ifdef ART_COUNT_LOOPS
-      if (lane == __ffsll((long long)__ballot(1)) - 1) s_lane_it += 1;
-#endif
-#ifdef ART_COUNT_PASSES
-      if (lane == __ffsll((long long)__ballot(1)) - 1) s_pc[6] += 1;
-#endif
       if (ph == 2) {
         walk();
         if (ph == 0) break;
@@ -1460,9 +1365,6 @@ __global__ __launch_bounds__(BLOCK, WPS) void propagate_kernel(const KParams P_i
       if (ph == 3) th = i_tr;
       else if (ph == 5) th = thgrid[ip];
       else if (ph == 6 || ph == 7) th = thgrid[last_j];
-#ifdef ART_COUNT_LOOPS
-      s_ph[ph] += 1;
-#endif
       const double ci = scan_point_lds(P, L, BLOCK, th);
       if (ph == 1) {
         s_root += 1;
@@ -1588,11 +1490,7 @@ __global__ __launch_bounds__(BLOCK, WPS) void propagate_kernel(const KParams P_i
       ray = -1;
       mode = M_IDLE;
     }
-#ifndef ART_S_NOCOUNT  // (dev A/B: no piece counts)
     if constexpr (DON == 3) {
-#else
-    if constexpr (DON >= 99) {
-#endif
       // the streamed host pipelines: each finishing lane counts its ray into its wave's LDS
       // histogram over the pieces; every ART_STREAM_FLUSH + 1 iterations (and once the queue is
       // drained) the wave releases its stores and adds the histogram to the pieces' global
@@ -1651,28 +1549,13 @@ __global__ __launch_bounds__(BLOCK, WPS) void propagate_kernel(const KParams P_i
 
   // wave-reduce the statistics and add them once per wave (DON = 3: before the wave counts itself
   // done and flushes its last piece counts, so the helper that ends the call finds them complete)
-#if defined(ART_SLOT_TIMING)
-  if (lane == 0) {  // [refill etc, combination, RHS, slot rest, norm..park, grid, fast+walk+coop, fallback]
-    const unsigned long long v[8] = {t_sec[0], t_sec[8] + t_sec[1], t_sec[9], t_sec[10], t_sec[2], t_sec[3],
-                                     t_sec[4] + t_sec[5] + t_sec[6], t_sec[7]};
-#pragma unroll
-    for (int k = 0; k < 8; ++k) atomicAdd(&stats[k], v[k]);
-  }
-#elif defined(ART_SECTION_TIMING)
+#if defined(ART_SECTION_TIMING)
   if (lane == 0) {
 #pragma unroll
     for (int k = 0; k < 8; ++k) atomicAdd(&stats[k], t_sec[k]);
   }
 #else
-#if defined(ART_COUNT_PASSES)
-  const unsigned v[7] = {s_pc[0], s_pc[1], s_pc[2], s_pc[3], s_pc[4], s_pc[5], s_pc[6]};
-#elif defined(ART_COUNT_LOOPS)
-  const unsigned v[7] = {s_main_it, s_lane_it, s_ph[1], s_ph[3], s_ph[5], s_ph[6], s_ph[7]};
-#elif defined(ART_COUNT_SUB)
-  const unsigned v[7] = {s_sub[0], s_sub[1], s_sub[2], s_sub[3], s_sub[4], s_sub[5], s_sub[6]};
-#else
   const unsigned v[7] = {s_att, s_acc, s_root, s_scan, s_interp, s_rays, s_cert};
-#endif
   const int slot[7] = {ST_ATTEMPTS, ST_ACCEPTED, ST_ROOT_STEPS, ST_SCAN_EVALS, ST_INTERP_EVALS, ST_RAYS, ST_CERT};
 #pragma unroll
   for (int k = 0; k < 7; ++k) {
@@ -1749,23 +1632,12 @@ __device__ inline double scan_point_regs(const KParams& P, const double* u0, con
 template <int GEOM>
 __device__ inline void tail_rhs(const KParams& P, int lane, const double* y, double ty, double t, double erg,
                                 double* kk, double* aux) {
-#if defined(ART_TAIL_PLAIN_RHS)
-  rhs(P, true, y, ty, erg, kk);  // dev A/B: the bulk kernel's RHS call
-  if (GEOM != GEOM_ANY) rhs_photon_gj(P, y, ty, erg, kk, aux); else rhs_photon(P, y, ty, erg, kk, aux);
-  return;
-#elif defined(ART_TAIL_PLAIN_T)
-  t = fexp(ty);
-#endif
   if constexpr (GEOM != GEOM_ANY) {
     const double arg = (lane == 1) ? psi_of(P, y[2], t) : y[1];
     double sn, cs;
     msincos(arg, sn, cs);
     const double st = rdlane(sn, 0), ct = rdlane(cs, 0), sp = rdlane(sn, 1), cp = rdlane(cs, 1);
-#ifdef ART_TAIL_RHS_UNI  // (dev A/B: the RHS's own branches wave-uniform too)
-    rhs_photon_gj_tr<double, true>(P, y, t, st, ct, sp, cp, erg, kk, aux);
-#else
     rhs_photon_gj_tr(P, y, t, st, ct, sp, cp, erg, kk, aux);
-#endif
   } else {
     rhs_photon(P, y, ty, erg, kk, aux);
   }
@@ -1782,11 +1654,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
   // that visible to the compiler (a scalar branch on lane 0's value instead of an exec-mask
   // branch with its saved masks -- SGPRs the kernel otherwise spills to VGPR lanes); the values
   // and the arithmetic do not change
-#ifndef ART_TAIL_NO_UNI
   auto U = [](bool c) { return __builtin_amdgcn_readfirstlane((int)c) != 0; };
-#else
-  auto U = [](bool c) { return c; };  // (dev A/B)
-#endif
   const int64_t nq = (int64_t)*out.cont_count;
   (void)max_rays;
   __builtin_amdgcn_s_setprio(3);  // the rays that set the launch's end
@@ -1973,9 +1841,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
           acc += q * q;
         }
         EEst2 = acc * (1.0 / 7.0);
-#ifdef ART_TRACE
-        if (lane == 0 && ray == g_trace_ray) trace_attempt(1, mode, hs, tau, EEst2, y, kk);
-#endif
       }
       // ---- controller (STEP) ----
       bool scan = false;
@@ -2087,12 +1952,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
       bool hit = false, root_done = false;
       auto thg = [&](int j) { return double(j) / double(npts - 1); };
       auto open_root = [&](double t_int) {
-#ifdef ART_TRACE
-        if (lane == 0 && ray == g_trace_ray) {
-          const double v[7] = {double(ip), double(last_j), last_c, i_cg, t_int, double(lc_ok), thg(ip)};
-          trace_attempt(11, mode, hs, tau, 0.0, v, v);
-        }
-#endif
         const double tg = thg(ip), lth = thg(last_j);
         hit = true;
         hroot = hs;
@@ -2320,12 +2179,12 @@ __global__ __launch_bounds__(256) void pack_fresh_kernel(const int64_t n, const 
   double v[20];
 #pragma unroll
   for (int i = 0; i < 7; ++i) {
-    v[i] = in.u0[i * n + ray];
-    v[7 + i] = in.u0[(7 + i) * n + ray];
+    v[i] = in.u0[ray * U0_REC + i];
+    v[7 + i] = in.u0[ray * U0_REC + 7 + i];
   }
-  const double cprev = in.u0[15 * n + ray];
+  const double cprev = in.u0[ray * U0_REC + 15];
   v[14] = in.lnt0[ray];
-  v[15] = in.u0[14 * n + ray];
+  v[15] = in.u0[ray * U0_REC + 14];
   v[16] = qpow_init;
   v[17] = cprev;
   v[18] = NAN;
@@ -2340,6 +2199,7 @@ __global__ __launch_bounds__(256) void pack_fresh_kernel(const int64_t n, const 
   ri[1] = make_int4(0, sprev, photon | 2 /* cprev_ok */, 1 /* save_k */);
 }
 
+#endif  // ART_HELPER_TU
 // Every initialisation and finalization of the library runs in helper_kernel, through ONE call
 // site of init_one and ONE of finalize_one: their arithmetic (the right-hand side's "fast"
 // contraction included) is then the same machine code for every path -- the single launch, the
@@ -2360,14 +2220,27 @@ __global__ __launch_bounds__(256) void pack_fresh_kernel(const int64_t n, const 
 //            then the flag (MI355X_MICROARCH.md, inter-workgroup visibility); readers poll the
 //            flag and take one agent-scope acquire.
 enum { HK_INIT = 0, HK_FIN = 1, HK_TILES = 2 };
-__global__ __launch_bounds__(256) void helper_kernel(const KParams P, const int64_t n, const SegIn in, const SegOut out,
-                                                     const int mode, const int64_t i0, const int64_t i1,
-                                                     const int64_t init_limit, const int announce,
-                                                     unsigned long long* __restrict__ stats) {
+// Instantiated per geometry like the integrator (the same folded physics), for 2 waves per SIMD:
+// a helper wave then shares a SIMD with one integrator wave, so the streamed pipeline's persistent
+// helpers take one integrator block slot each instead of a whole CU. The builds need 158-203
+// VGPRs and no scratch (-disable-machine-licm, build.py); helper_waves_per_simd checks that at
+// run time, because a scratch-spilling persistent helper stalled the next launch on another
+// queue for seconds (the runtime growing that queue's scratch while the helpers held theirs).
+#ifdef ART_HELPER_TU
+template <int GEOM>
+__global__ __launch_bounds__(256, 2) void helper_kernel(
+    const KParams P_in, const int64_t n, const SegIn in, const SegOut out, const int mode, const int64_t i0,
+    const int64_t i1, const int64_t init_limit, const int announce, unsigned long long* __restrict__ stats) {
+  const KParams P = specialize<GEOM>(P_in);
   __shared__ long long cmd[2];  // HK_TILES: [what, tile]: 0 nothing now, 1 initialise, 2 finalize, 3 done
   __shared__ double hfl[2 * FLUX_HELPER_BINS];  // (HK_TILES with SegOut::flux_hist) this block's flux counts
   __shared__ int last_out, complete;
   const int tid = threadIdx.x;
+  // the persistent helpers share their SIMDs with integrator waves (2 waves per SIMD): their claims,
+  // hand-offs and tiles run at the top issue priority, so the initialisation keeps ahead of the
+  // integrator's chunk claims (at the integrator's priorities the idle polls starved and the calls
+  // gave up); between polls they sleep
+  if (mode == HK_TILES) __builtin_amdgcn_s_setprio(3);
   const bool flb = mode == HK_TILES && out.flux_hist != nullptr;
   if (flb)
     for (int b = tid; b < 2 * out.flux_nbins; b += 256) hfl[b] = 0.0;
@@ -2477,8 +2350,14 @@ __global__ __launch_bounds__(256) void helper_kernel(const KParams P, const int6
         cmd[1] = t;
       }
       __syncthreads();
-      what = cmd[0];
-      t = cmd[1];
+      // (block-uniform: said so, so the tile's SegOut and bounds stay in scalar registers --
+      // read as per-lane values they took ~100 VGPRs across the tile loop)
+      what = (long long)__builtin_amdgcn_readfirstlane((int)cmd[0]);
+      {
+        const unsigned long long tw = (unsigned long long)cmd[1];
+        t = (long long)(((unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane((int)(tw >> 32)) << 32) |
+                        (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)tw));
+      }
       __syncthreads();
       if (what == 3) break;
       if (what == 0) {
@@ -2487,16 +2366,19 @@ __global__ __launch_bounds__(256) void helper_kernel(const KParams P, const int6
       }
     }
     const int64_t t1 = t + TS < (mode == HK_TILES ? n : i1) ? t + TS : (mode == HK_TILES ? n : i1);
-    SegOut ol = out;
-    int64_t ob = i0, m = i1 - i0;
-    if (mode == HK_TILES && what == 2) {
-      const int p = (int)(t >> out.piece_shift);
-      ol = piece_blob(out, n, p, m);
-      ob = (int64_t)p << out.piece_shift;
-    }
-    for (int64_t i = t + tid; i < t1; i += 256) {  // (one call site of each)
-      if (what == 1) nrhs += init_one(P, n, i, in);
-      else finalize_one(P, n, i, i - ob, m, in, ol, flb ? hfl : nullptr, out.flux_nbins);
+    if (what == 1) {  // (one call site of each)
+#pragma unroll 1
+      for (int64_t i = t + tid; i < t1; i += 256) nrhs += init_one(P, n, i, in);
+    } else {
+      SegOut ol = out;
+      int64_t ob = i0, m = i1 - i0;
+      if (mode == HK_TILES) {
+        const int p = (int)(t >> out.piece_shift);
+        ol = piece_blob(out, n, p, m);
+        ob = (int64_t)p << out.piece_shift;
+      }
+#pragma unroll 1
+      for (int64_t i = t + tid; i < t1; i += 256) finalize_one(P, n, i, i - ob, m, in, ol, flb ? hfl : nullptr, out.flux_nbins);
     }
     if (mode == HK_TILES) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -2568,6 +2450,30 @@ __global__ __launch_bounds__(256) void helper_kernel(const KParams P, const int6
   }
 }
 
+// the helper instantiation of the integrator's geometry (launch_propagate, launch_integrator_streamed)
+HFn pick_helper(const KParams& P) {
+  const bool flat = P.rs_eff == 0.0 && !(P.bndry_lyr > 0.0) && !P.isotropic;
+  const bool sch = P.rs_eff > 0.0 && !(P.bndry_lyr > 0.0) && !P.isotropic;
+  return flat ? helper_kernel<GEOM_FLAT> : (sch ? helper_kernel<GEOM_GR> : helper_kernel<GEOM_ANY>);
+}
+int helper_waves_per_simd(const KParams& P) {
+  // 2 when the build for these parameters fits 2 waves per SIMD without scratch (read once per build)
+  static std::atomic<int> cached[3];
+  const HFn fn = pick_helper(P);
+  const int g = fn == helper_kernel<GEOM_FLAT> ? 1 : (fn == helper_kernel<GEOM_GR> ? 2 : 0);
+  int w = cached[g].load(std::memory_order_relaxed);
+  if (!w) {
+    hipFuncAttributes a{};
+    const bool ok = hipFuncGetAttributes(&a, (const void*)fn) == hipSuccess;
+    (void)hipGetLastError();
+    w = (ok && a.localSizeBytes == 0 && a.numRegs > 0 && a.numRegs <= 256) ? 2 : 1;
+    cached[g].store(w, std::memory_order_relaxed);
+  }
+  return w;
+}
+#endif  // ART_HELPER_TU
+
+#ifndef ART_HELPER_TU
 // ---------------------------------------------------------------------------
 // find_samples_new (RayTracer.jl:1480-1653) + main_runner's erg and k_init
 // (MainRunner.jl:511-529): persistent lanes, one ray per lane, one attempt per lane per outer
@@ -2780,9 +2686,6 @@ __global__ __launch_bounds__(256, WPS) void sample_kernel(const KParams P, const
     // resolve the queued brackets: Illinois on the exact line (the lane that found one owns
     // it), then each owner counts its valid crossings in queue order and keeps the randInx-th
     auto flush = [&]() {
-#ifdef ART_SSEC_FLUSH  // (dev: the flushes' cycles in the "out" bucket instead of "brackets")
-      ART_QMARK(4)
-#endif
       wave_lds_sync();
       #pragma unroll 1
       for (int t = lane; t < qn; t += 64) {
@@ -2832,9 +2735,6 @@ __global__ __launch_bounds__(256, WPS) void sample_kernel(const KParams P, const
       }
       qn = 0;
       wave_lds_sync();
-#ifdef ART_SSEC_FLUSH
-      ART_QMARK(5)
-#endif
     };
 
     ART_QMARK(0)
@@ -2936,9 +2836,7 @@ __global__ __launch_bounds__(256, WPS) void sample_kernel(const KParams P, const
         }
         wave_lds_sync();
         const int tot = npairs * nper;
-#ifndef ART_NO_SAMPLER_PRIO  // the dense grid pass at the low issue priority, the rest at the high one
         __builtin_amdgcn_s_setprio(0);
-#endif
         #pragma unroll 1
         for (int w0 = 0; w0 < tot; w0 += 64) {
           const int t = w0 + lane;
@@ -2979,9 +2877,7 @@ __global__ __launch_bounds__(256, WPS) void sample_kernel(const KParams P, const
             }
           }
         }
-#ifndef ART_NO_SAMPLER_PRIO
         __builtin_amdgcn_s_setprio(1);
-#endif
         wave_lds_sync();
       }
       ART_QMARK(3)
@@ -3154,9 +3050,7 @@ __global__ __launch_bounds__(256, WPS) void sample_kernel(const KParams P, const
       // kernel is VALU-bound, profiles/r04aq_sampler_pmc.txt).
       // items: the other lanes' 19 points each, then the inner lanes' last points
       const int totN = nU * nper, tot = totN + nI;
-#ifndef ART_NO_SAMPLER_PRIO  // the dense grid pass at the low issue priority, the rest of a step (certificate,
       __builtin_amdgcn_s_setprio(0);  // brackets: short dependent chains) at the high one: 118.5 -> 117.1 ms
-#endif                                // per 1e7 samples (profiles/r04c_sampler_prio.jsonl)
       #pragma unroll 1
       for (int w0 = 0; w0 < tot; w0 += 64) {
         const int t = w0 + lane;
@@ -3199,9 +3093,7 @@ __global__ __launch_bounds__(256, WPS) void sample_kernel(const KParams P, const
           }
         }
       }
-#ifndef ART_NO_SAMPLER_PRIO
       __builtin_amdgcn_s_setprio(1);
-#endif
       wave_lds_sync();
       // this lane's sign changes in (point j-1, point j]: signbits differ, both values nonzero
       unsigned br = 0u;
@@ -3453,13 +3345,7 @@ int persistent_blocks(const void* func, int64_t work, int block, int fallback_pe
   int dev = 0, ncu = 0, per_cu = 0;
   (void)hipGetDevice(&dev);
   (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-#ifdef ART_DEV_GRID_CUS
-  ncu = ART_DEV_GRID_CUS;  // (dev builds: a grid sized for a CU-masked stream)
-#endif
   const hipError_t oe = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, func, block, 0);
-#ifdef ART_LAUNCH_DEBUG
-  fprintf(stderr, "[art-debug] occupancy rc=%d (%s) per_cu=%d ncu=%d\n", (int)oe, hipGetErrorString(oe), per_cu, ncu);
-#endif
   if (oe != hipSuccess || per_cu < 1) {
     // The runtime's occupancy calculator returns hipErrorUnknown (and 0 blocks) for the
     // 1-wave/SIMD flat integrator (270 unified VGPRs: 256 arch + 14 AGPRs), a kernel that
@@ -3528,20 +3414,8 @@ hipError_t launch_propagate(const KParams& P, int64_t n, const SegIn& in, const 
                             hipEvent_t ev0, hipEvent_t ev1, hipStream_t fs) {
   const int64_t gr = (n + 255) / 256;
   const unsigned g1 = (unsigned)((n + 255) / 256);
-#ifdef ART_LAUNCH_DEBUG
-  // dev: every launch synchronised and checked on its own, errors named by stage
-#define ART_DBG(stage)                                                                                       \
-  {                                                                                                          \
-    const hipError_t le_ = hipGetLastError();                                                                \
-    const hipError_t se_ = hipStreamSynchronize(s);                                                          \
-    fprintf(stderr, "[art-debug] %s: last=%d (%s) sync=%d (%s)\n", stage, (int)le_, hipGetErrorString(le_), \
-            (int)se_, hipGetErrorString(se_));                                                               \
-  }
-  ART_DBG("entry")
-#else
 #define ART_DBG(stage)
-#endif
-  hipLaunchKernelGGL(helper_kernel, dim3((unsigned)(gr < 2048 ? gr : 2048)), dim3(256), 0, s, P, n, in, out_arg, (int)HK_INIT,
+  hipLaunchKernelGGL(pick_helper(P), dim3((unsigned)(gr < 2048 ? gr : 2048)), dim3(256), 0, s, P, n, in, out_arg, (int)HK_INIT,
                      (int64_t)0, n, (int64_t)-1, 0, stats);
   ART_DBG("helper_kernel (init)")
   hipError_t e = hipGetLastError();
@@ -3580,7 +3454,7 @@ hipError_t launch_propagate(const KParams& P, int64_t n, const SegIn& in, const 
       if ((e = hipStreamWaitEvent(fs, ev1, 0)) != hipSuccess) return e;
       sf = fs;
     }
-    hipLaunchKernelGGL(helper_kernel, dim3(g1), dim3(256), 0, sf, P, n, in, out, (int)HK_FIN, (int64_t)0, n,
+    hipLaunchKernelGGL(pick_helper(P), dim3(g1), dim3(256), 0, sf, P, n, in, out, (int)HK_FIN, (int64_t)0, n,
                        (int64_t)-1, 0, stats);
     return hipGetLastError();
   }
@@ -3659,7 +3533,7 @@ hipError_t launch_propagate(const KParams& P, int64_t n, const SegIn& in, const 
     if ((e = hipStreamWaitEvent(fs, ev1, 0)) != hipSuccess) return e;
     sf = fs;
   }
-  hipLaunchKernelGGL(helper_kernel, dim3(g1), dim3(256), 0, sf, P, n, in, out, (int)HK_FIN, (int64_t)0, n, (int64_t)-1,
+  hipLaunchKernelGGL(pick_helper(P), dim3(g1), dim3(256), 0, sf, P, n, in, out, (int)HK_FIN, (int64_t)0, n, (int64_t)-1,
                      0, stats);
   ART_DBG("helper_kernel (finalize)")
   return hipGetLastError();
@@ -3684,7 +3558,7 @@ hipError_t launch_integrator_streamed(const KParams& P, int64_t n, const SegIn& 
 
 hipError_t launch_helpers(const KParams& P, int64_t n, const SegIn& in, const SegOut& out, int blocks, int64_t init_limit,
                           int announce, unsigned long long* stats, hipStream_t s) {
-  hipLaunchKernelGGL(helper_kernel, dim3((unsigned)blocks), dim3(256), 0, s, P, n, in, out, (int)HK_TILES, (int64_t)0, n,
+  hipLaunchKernelGGL(pick_helper(P), dim3((unsigned)blocks), dim3(256), 0, s, P, n, in, out, (int)HK_TILES, (int64_t)0, n,
                      init_limit, announce, stats);
   return hipGetLastError();
 }
@@ -3766,22 +3640,7 @@ hipError_t launch_eval_condition(const KParams& P, int64_t n, const double* u, c
   return hipGetLastError();
 }
 
+#endif  // ART_HELPER_TU
+
 }  // namespace art
 
-#ifdef ART_TRACE
-// dev build only: trace one ray (-1: off); read back its per-attempt records (TRACE_REC doubles)
-extern "C" int art_debug_trace_set(int ray) {
-  const unsigned zero = 0;
-  if (hipMemcpyToSymbol(HIP_SYMBOL(art::g_trace_ray), &ray, sizeof ray) != hipSuccess) return -2;
-  return hipMemcpyToSymbol(HIP_SYMBOL(art::g_trace_n), &zero, sizeof zero) == hipSuccess ? 0 : -2;
-}
-extern "C" int art_debug_trace_get(double* out, int max_records, int* count) {
-  unsigned n = 0;
-  if (hipDeviceSynchronize() != hipSuccess) return -2;
-  if (hipMemcpyFromSymbol(&n, HIP_SYMBOL(art::g_trace_n), sizeof n) != hipSuccess) return -2;
-  n = n < (unsigned)art::TRACE_MAX ? n : (unsigned)art::TRACE_MAX;
-  n = n < (unsigned)max_records ? n : (unsigned)max_records;
-  *count = (int)n;
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(art::g_trace), (size_t)n * art::TRACE_REC * sizeof(double)) == hipSuccess ? 0 : -2;
-}
-#endif

@@ -88,44 +88,49 @@ def run_points(kws: list[dict], rays: int, seed: int = 1769, nbins: int = 50, de
         s_.wait_stream(main)
     t0 = time.perf_counter()
     engs, recs = [], []
-    for kw in kws:
-        p = A.Params(**kw)
-        rec = dict(kw, rays=rays, max_r_km=p.max_r())
-        recs.append(rec)
-        if rec["max_r_km"] < p.rNS:  # no conversion surface outside the star (MainRunner.jl:387-396)
-            rec["skipped"] = "maxR < rNS"
-            engs.append(None)
-        else:
-            engs.append(Engine(p, device=device))
-            engs[-1].set_tail_donation(donate)
-            engs[-1].set_graduation(0 if len(ss) > 1 else -1)  # (passes in flight: off)
-            # samplers in flight: the 3-wave build for every line (per device; 0.503-0.508 -> 0.484 s
-            # of sampling, profiles/r05ah_scan_sampler_waves.txt)
-            engs[-1].set_sampler_waves(3 if len(ss) > 1 else 0)
-    # Longest expected drain first: a point's kernel time grows with its conversion radius
-    # (maxR: 29 km -> 20 ms ... 342 km -> 835 ms per 1e6 rays, profiles/r02b_scan_order.txt),
-    # and the longest single ray bounds the whole scan, so it should start at once.
-    live = sorted((i for i, e in enumerate(engs) if e is not None), key=lambda i: -recs[i]["max_r_km"])
-    inps, outs, hists = {}, {}, {}
+    try:
+        for kw in kws:
+            p = A.Params(**kw)
+            rec = dict(kw, rays=rays, max_r_km=p.max_r())
+            recs.append(rec)
+            if rec["max_r_km"] < p.rNS:  # no conversion surface outside the star (MainRunner.jl:387-396)
+                rec["skipped"] = "maxR < rNS"
+                engs.append(None)
+            else:
+                engs.append(Engine(p, device=device))
+                engs[-1].set_tail_donation(donate)
+                engs[-1].set_graduation(0 if len(ss) > 1 else -1)  # (passes in flight: off)
+                # samplers in flight: the 3-wave build for every line (per device; 0.503-0.508 -> 0.484 s
+                # of sampling, profiles/r05ah_scan_sampler_waves.txt)
+                engs[-1].set_sampler_waves(3 if len(ss) > 1 else 0)
+        # Longest expected drain first: a point's kernel time grows with its conversion radius
+        # (maxR: 29 km -> 20 ms ... 342 km -> 835 ms per 1e6 rays, profiles/r02b_scan_order.txt),
+        # and the longest single ray bounds the whole scan, so it should start at once.
+        live = sorted((i for i, e in enumerate(engs) if e is not None), key=lambda i: -recs[i]["max_r_km"])
+        inps, outs, hists = {}, {}, {}
 
-    def sample(i):  # the samplers' tails overlap too
-        inps[i] = engs[i].forward_roots(rays, seed=seed)
+        def sample(i):  # the samplers' tails overlap too
+            inps[i] = engs[i].forward_roots(rays, seed=seed)
 
-    dispatch(live, sample, ss)
-    torch.cuda.synchronize()
-    t_sample = time.perf_counter() - t0
+        dispatch(live, sample, ss)
+        torch.cuda.synchronize()
+        t_sample = time.perf_counter() - t0
 
-    def prop(i):
-        outs[i] = engs[i].propagate(inps[i], max_crossings=-1)
-        hists[i] = engs[i].flux_histogram(outs[i], inps[i]["species"], None, nbins)
+        def prop(i):
+            outs[i] = engs[i].propagate(inps[i], max_crossings=-1)
+            hists[i] = engs[i].flux_histogram(outs[i], inps[i]["species"], None, nbins)
 
-    t1 = time.perf_counter()
-    order = dispatch(live, prop, ss)
-    torch.cuda.synchronize()
-    wall = time.perf_counter() - t1
-    if live:
-        engs[live[0]].set_graduation(-1)  # (the device's defaults again)
-        engs[live[0]].set_sampler_waves(0)
+        t1 = time.perf_counter()
+        order = dispatch(live, prop, ss)
+        torch.cuda.synchronize()
+        wall = time.perf_counter() - t1
+    finally:
+        # the device's defaults again (graduation, sampler build) for every device configured,
+        # also when a point's dispatch raised: they are per-device settings later Engines inherit
+        for e in engs:
+            if e is not None:
+                e.set_graduation(-1)
+                e.set_sampler_waves(0)
     k = len(order)
     ms = (C.c_double * max(1, k))()
     got = A._lib.load().art_recent_kernel_ms(k, ms)
