@@ -8,17 +8,17 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB_DIR = os.path.join(HERE, "lib")
 LIB = os.path.join(LIB_DIR, "libart.so")
-SOURCES = ["art_kernels.hip", "art_capi.cpp", "art_forest.cpp", "art_helpers.hip"]
+SOURCES = ["art_kernels.hip", "art_capi.cpp", "art_forest.cpp", "art_kernels_nolicm.hip"]
 HEADERS = ["art_core.h", "art_internal.h", "art_event.h"]
 ARCH = os.environ.get("ART_OFFLOAD_ARCH", "gfx950")
 # -ffp-contract=on: FMA fusion within one source expression only ("FMA contraction").
 # -amdgpu-use-amdgpu-trackers: AMDGPU's own register-pressure trackers in the machine scheduler:
 #   fewer spills of the 256-VGPR integrator and 1% faster (A/B on the 1e7-ray flat batch, round 3).
-# art_helpers.hip adds -disable-machine-licm (see its header): MachineLICM hoisted the loop's
-#   polynomial constants into ~150 VGPRs live across the helper's ray loop, which then spilled to
-#   scratch at 2 waves per SIMD. Only that translation unit: the integrator runs 3% faster with it.
+# art_kernels_nolicm.hip adds -disable-machine-licm (see its header): the helper, the non-flat
+#   integrators and the tail kernel spill nothing without MachineLICM's hoisted constants (and the GR
+#   ones run 2-3% faster); the flat integrator (art_kernels.hip) runs 3% faster with it.
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=on", "-mllvm", "-amdgpu-use-amdgpu-trackers=1"]
-TU_FLAGS = {"art_helpers.hip": ["-mllvm", "-disable-machine-licm"]}
+TU_FLAGS = {"art_kernels_nolicm.hip": ["-mllvm", "-disable-machine-licm"]}
 
 
 def _hipcc():

@@ -160,6 +160,15 @@ hipError_t launch_helpers(const KParams& P, int64_t n, const SegIn& in, const Se
 using HFn = void (*)(const KParams, const int64_t, const SegIn, const SegOut, const int, const int64_t, const int64_t,
                      const int64_t, const int, unsigned long long*);
 HFn pick_helper(const KParams& P);
+// The integrator (propagate_kernel) and tail kernel builds of art_kernels_nolicm.hip: every geometry
+// but flat's (nullptr for a combination no path launches). integ: ART_VERN6 / ART_RK4; geom: the
+// GEOM_* of art_kernels.hip (0 any, 1 flat, 2 GR); don: the donation mode; wps: waves per SIMD.
+using KFn = void (*)(const KParams, const int64_t, const SegIn, const SegOut, const int32_t, unsigned long long*,
+                     unsigned long long*);
+using TFn = void (*)(const KParams, const int64_t, const SegIn, const SegOut, const int32_t, const int32_t,
+                     unsigned long long*);
+KFn nl_propagate(int integ, int geom, bool save, int don, int wps);
+TFn nl_tail(int geom);
 int helper_waves_per_simd(const KParams& P);
 // The batch size up to which launch_propagate runs every ray on a wave of its own (tail_kernel):
 // ART_SMALL_TAIL, default one ray per SIMD of the device; 0 switches it off.

@@ -320,8 +320,8 @@ struct StageTable {
   double e_f, e_A, e_L[LDS_SLOTS], e_k;  // error weights (Vern6): btilde of f, kA(=k8), L, k9
 };
 
-#ifndef ART_HELPER_TU  // (art_helpers.hip compiles the helper kernel alone, see there)
-__constant__ StageTable c_vern6 = {
+// (static: both translation units, art_kernels.hip and art_kernels_nolicm.hip, hold their own copy)
+static __constant__ StageTable c_vern6 = {
     // {cf = a_{s+2,1}, cA (k2 for slots 0..6, k8 for slot 7), ct, lmask, storeA, storeL}
     {{Vern6::a21, 0.0, Vern6::c2, 0x0, 1, -1, 0},
      {Vern6::a31, Vern6::a32, Vern6::c3, 0x0, 0, 0, 0},
@@ -342,7 +342,7 @@ __constant__ StageTable c_vern6 = {
      {0, Vern6::a94, Vern6::a95, Vern6::a96, Vern6::a97}},
     Vern6::e1, Vern6::e8, {0.0, Vern6::e4, Vern6::e5, Vern6::e6, Vern6::e7}, Vern6::e9};
 
-__constant__ StageTable c_rk4 = {
+static __constant__ StageTable c_rk4 = {
     {{0.5, 0.0, 0.5, 0x0, 1, -1, 0},
      {0.0, 0.5, 0.5, 0x0, 0, 0, 0},
      {0.0, 0.0, 1.0, 0x1, 0, 1, 0},
@@ -352,7 +352,6 @@ __constant__ StageTable c_rk4 = {
      {0, 0, 0, 0, 0}, {0, 0, 0, 0, 0}, {0, 0, 0, 0, 0}, {0, 0, 0, 0, 0}},
     0.0, 0.0, {0, 0, 0, 0, 0}, 0.0};
 
-#endif
 enum LaneMode { M_IDLE = 0, M_STEP = 2, M_ROOT = 3 };
 
 // Lanes per block of the persistent integrator. A block retires only when all its waves are
@@ -687,7 +686,6 @@ __device__ inline bool chunk_wait(const SegOut& out, int wnext, int leader) {
   return __shfl(ok, leader) != 0;
 }
 
-#ifndef ART_HELPER_TU
 // DON: the tail-donation instantiations (SegOut::donate / cont_mode honoured); the others
 // carry none of that code, so a lone pass pays nothing for it
 // WPS: waves per SIMD the registers are budgeted for (the default 2; the GR continuation
@@ -1592,7 +1590,7 @@ __global__ __launch_bounds__(BLOCK, WPS) void propagate_kernel(const KParams P_i
 // Everything else is the bulk kernel's arithmetic on the same operands in the same order, so a
 // donated ray's result is bit-identical to its never-donated one (tests/test_gpu_tail_donation.py).
 // Vern6 without saveat only (the other launches keep the packed continuation).
-__constant__ double c_tail_ct[8] = {Vern6::c2, Vern6::c3, Vern6::c4, Vern6::c5, Vern6::c6, Vern6::c7, 1.0, 1.0};
+static __constant__ double c_tail_ct[8] = {Vern6::c2, Vern6::c3, Vern6::c4, Vern6::c5, Vern6::c6, Vern6::c7, 1.0, 1.0};
 
 // a wave-uniform double from lane l (two v_readlane_b32)
 __device__ inline double rdlane(double v, int l) {
@@ -2161,6 +2159,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
   span_stamp(stats, true);
 }
 
+#ifndef ART_NOLICM_TU  // (non-template kernels: this translation unit only)
 // Small batches (SegOut::small_tail): every fresh ray as a CONT_REC record for tail_kernel, the
 // state the persistent integrator gives a ray it takes from the queue (its refill: u0, f0, dt
 // and c0 from init_kernel, the controller's qold power at qoldinit = 1e-4, no b at the step
@@ -2199,7 +2198,7 @@ __global__ __launch_bounds__(256) void pack_fresh_kernel(const int64_t n, const 
   ri[1] = make_int4(0, sprev, photon | 2 /* cprev_ok */, 1 /* save_k */);
 }
 
-#endif  // ART_HELPER_TU
+#endif  // ART_NOLICM_TU
 // Every initialisation and finalization of the library runs in helper_kernel, through ONE call
 // site of init_one and ONE of finalize_one: their arithmetic (the right-hand side's "fast"
 // contraction included) is then the same machine code for every path -- the single launch, the
@@ -2226,7 +2225,7 @@ enum { HK_INIT = 0, HK_FIN = 1, HK_TILES = 2 };
 // VGPRs and no scratch (-disable-machine-licm, build.py); helper_waves_per_simd checks that at
 // run time, because a scratch-spilling persistent helper stalled the next launch on another
 // queue for seconds (the runtime growing that queue's scratch while the helpers held theirs).
-#ifdef ART_HELPER_TU
+#ifdef ART_NOLICM_TU
 template <int GEOM>
 __global__ __launch_bounds__(256, 2) void helper_kernel(
     const KParams P_in, const int64_t n, const SegIn in, const SegOut out, const int mode, const int64_t i0,
@@ -2471,9 +2470,29 @@ int helper_waves_per_simd(const KParams& P) {
   }
   return w;
 }
-#endif  // ART_HELPER_TU
 
-#ifndef ART_HELPER_TU
+// The integrator and tail instantiations compiled here, without MachineLICM (art_kernels_nolicm.hip):
+// every geometry but flat's Vern6/RK4 integrator. GR: the bulk launch 235.2-236.7 -> 227.3-228.7
+// ms per 10^6 rays, the lone tail ray 7.69 -> 7.54 us per attempt (no spills: 256 VGPRs + 60 spilled
+// -> 226), bit-identical (profiles/r06q_gr_licm.jsonl); the flat integrator stays in art_kernels.hip,
+// 3% faster with the pass (profiles/r06o_ab_device_licm_off_everywhere.jsonl).
+KFn nl_propagate(int integ, int geom, bool save, int don, int wps) {
+#define ART_NL(I, G, S, D, W) \
+  if (integ == I && geom == G && save == S && don == D && wps == W) return propagate_kernel<I, G, S, D, W>;
+  ART_NL(ART_VERN6, GEOM_GR, true, 0, 2) ART_NL(ART_VERN6, GEOM_GR, true, 1, 2)
+  ART_NL(ART_VERN6, GEOM_ANY, true, 0, 2) ART_NL(ART_VERN6, GEOM_ANY, true, 1, 2)
+  ART_NL(ART_RK4, GEOM_ANY, true, 0, 2) ART_NL(ART_RK4, GEOM_ANY, true, 1, 2)
+  ART_NL(ART_RK4, GEOM_ANY, false, 0, 2) ART_NL(ART_RK4, GEOM_ANY, false, 1, 2)
+  ART_NL(ART_VERN6, GEOM_GR, false, 0, 2) ART_NL(ART_VERN6, GEOM_GR, false, 1, 2) ART_NL(ART_VERN6, GEOM_GR, false, 3, 2)
+  ART_NL(ART_VERN6, GEOM_ANY, false, 0, 2) ART_NL(ART_VERN6, GEOM_ANY, false, 1, 2) ART_NL(ART_VERN6, GEOM_ANY, false, 3, 2)
+  ART_NL(ART_VERN6, GEOM_GR, false, 0, 1) ART_NL(ART_VERN6, GEOM_GR, false, 1, 1)
+#undef ART_NL
+  return nullptr;
+}
+TFn nl_tail(int geom) { return geom == GEOM_FLAT ? tail_kernel<GEOM_FLAT> : (geom == GEOM_GR ? tail_kernel<GEOM_GR> : tail_kernel<GEOM_ANY>); }
+#endif  // ART_NOLICM_TU
+
+#ifndef ART_NOLICM_TU
 // ---------------------------------------------------------------------------
 // find_samples_new (RayTracer.jl:1480-1653) + main_runner's erg and k_init
 // (MainRunner.jl:511-529): persistent lanes, one ray per lane, one attempt per lane per outer
@@ -3361,20 +3380,16 @@ int persistent_blocks(const void* func, int64_t work, int block, int fallback_pe
   return (int)(need < full ? need : full);
 }
 
-using KFn = void (*)(const KParams, const int64_t, const SegIn, const SegOut, const int32_t, unsigned long long*,
-                     unsigned long long*);
 
+// flat's instantiations live here; every other one comes from art_kernels_nolicm.hip (nl_propagate)
 template <int DON>
 static KFn pick_propagate(bool save, bool rk4, bool flat, bool sch) {
   if (save)  // saveat requested: the saving instantiations
-    return rk4 ? propagate_kernel<ART_RK4, GEOM_ANY, true, DON>
-               : (flat ? propagate_kernel<ART_VERN6, GEOM_FLAT, true, DON>
-                       : (sch ? propagate_kernel<ART_VERN6, GEOM_GR, true, DON>
-                              : propagate_kernel<ART_VERN6, GEOM_ANY, true, DON>));
-  return rk4 ? (flat ? propagate_kernel<ART_RK4, GEOM_FLAT, false, DON> : propagate_kernel<ART_RK4, GEOM_ANY, false, DON>)
-             : (flat ? propagate_kernel<ART_VERN6, GEOM_FLAT, false, DON>
-                     : (sch ? propagate_kernel<ART_VERN6, GEOM_GR, false, DON>
-                            : propagate_kernel<ART_VERN6, GEOM_ANY, false, DON>));
+    return (!rk4 && flat) ? propagate_kernel<ART_VERN6, GEOM_FLAT, true, DON>
+                          : nl_propagate(rk4 ? ART_RK4 : ART_VERN6, (!rk4 && sch) ? GEOM_GR : GEOM_ANY, true, DON,
+                                         ART_WAVES_PER_SIMD);
+  if (flat) return rk4 ? propagate_kernel<ART_RK4, GEOM_FLAT, false, DON> : propagate_kernel<ART_VERN6, GEOM_FLAT, false, DON>;
+  return nl_propagate(rk4 ? ART_RK4 : ART_VERN6, (!rk4 && sch) ? GEOM_GR : GEOM_ANY, false, DON, ART_WAVES_PER_SIMD);
 }
 
 int64_t small_tail_limit() {
@@ -3442,9 +3457,7 @@ hipError_t launch_propagate(const KParams& P, int64_t n, const SegIn& in, const 
     const int waves = (int)(n < (int64_t)ncu * 4 ? n : (int64_t)ncu * 4);
     if (grid_out) *grid_out = waves;
     if (ev0 && (e = hipEventRecord(ev0, s)) != hipSuccess) return e;
-    using TFn = void (*)(const KParams, const int64_t, const SegIn, const SegOut, const int32_t, const int32_t,
-                         unsigned long long*);
-    const TFn tfn = flat ? tail_kernel<GEOM_FLAT> : (sch ? tail_kernel<GEOM_GR> : tail_kernel<GEOM_ANY>);
+    const TFn tfn = nl_tail(flat ? GEOM_FLAT : (sch ? GEOM_GR : GEOM_ANY));
     hipLaunchKernelGGL(tfn, dim3(waves), dim3(64), 0, s, P, n, in, ot, max_crossings, waves, stats);
     ART_DBG("tail_kernel (small batch)")
     if ((e = hipGetLastError()) != hipSuccess) return e;
@@ -3473,7 +3486,7 @@ hipError_t launch_propagate(const KParams& P, int64_t n, const SegIn& in, const 
 #else
     if (true) {  // (dev A/B build: the 1-wave/SIMD integrator for every batch, the occupancy sensitivity)
 #endif
-      fn = flat ? propagate_kernel<ART_VERN6, GEOM_FLAT, false, 0, 1> : propagate_kernel<ART_VERN6, GEOM_GR, false, 0, 1>;
+      fn = flat ? propagate_kernel<ART_VERN6, GEOM_FLAT, false, 0, 1> : nl_propagate(ART_VERN6, GEOM_GR, false, 0, 1);
       w1 = true;
     }
   }
@@ -3502,7 +3515,7 @@ hipError_t launch_propagate(const KParams& P, int64_t n, const SegIn& in, const 
     // GR continuations at 1 wave/SIMD: no spills (68 VGPRs spill to scratch at 2). A/B on the
     // configs[3] bench line: 3.21e8 -> 3.35e8 ray-steps/s, bit-identical
     // (profiles/r02h_continuation_w1_ab.txt); flat stays at 2 (measured -3.5% at 1).
-    const KFn cfn = (w1_builds() && sch && !rk4 && out.ntimes < 2) ? propagate_kernel<ART_VERN6, GEOM_GR, false, 1, 1> : fn;
+    const KFn cfn = (w1_builds() && sch && !rk4 && out.ntimes < 2) ? nl_propagate(ART_VERN6, GEOM_GR, false, 1, 1) : fn;
     hipLaunchKernelGGL(cfn, dim3(cgrid), dim3(BLOCK), 0, s, P, n, in, oc, max_crossings, queue, stats);
     ART_DBG("continuation")
     if ((e = hipGetLastError()) != hipSuccess) return e;
@@ -3519,9 +3532,7 @@ hipError_t launch_propagate(const KParams& P, int64_t n, const SegIn& in, const 
       ot.cont = out.cont2;
       ot.cont_count = out.cont2_count;
       ot.cont_queue = out.cont2_queue;
-      using TFn = void (*)(const KParams, const int64_t, const SegIn, const SegOut, const int32_t, const int32_t,
-                           unsigned long long*);
-      const TFn tfn = flat ? tail_kernel<GEOM_FLAT> : (sch ? tail_kernel<GEOM_GR> : tail_kernel<GEOM_ANY>);
+      const TFn tfn = nl_tail(flat ? GEOM_FLAT : (sch ? GEOM_GR : GEOM_ANY));
       if (tgrid > 0) hipLaunchKernelGGL(tfn, dim3(tgrid), dim3(64), 0, s, P, n, in, ot, max_crossings, waves, stats);
       ART_DBG("tail_kernel")
       if ((e = hipGetLastError()) != hipSuccess) return e;
@@ -3548,7 +3559,7 @@ hipError_t launch_integrator_streamed(const KParams& P, int64_t n, const SegIn& 
   const bool flat = P.rs_eff == 0.0 && !(P.bndry_lyr > 0.0) && !P.isotropic;
   const bool sch = P.rs_eff > 0.0 && !(P.bndry_lyr > 0.0) && !P.isotropic;
   const KFn fn = flat ? propagate_kernel<ART_VERN6, GEOM_FLAT, false, 3>
-                      : (sch ? propagate_kernel<ART_VERN6, GEOM_GR, false, 3> : propagate_kernel<ART_VERN6, GEOM_ANY, false, 3>);
+                      : nl_propagate(ART_VERN6, sch ? GEOM_GR : GEOM_ANY, false, 3, ART_WAVES_PER_SIMD);
   const int64_t need = (n + BLOCK - 1) / BLOCK;
   const int grid = (int)(need < (int64_t)blocks ? need : (int64_t)blocks);
   if (grid_out) *grid_out = grid;
@@ -3640,7 +3651,7 @@ hipError_t launch_eval_condition(const KParams& P, int64_t n, const double* u, c
   return hipGetLastError();
 }
 
-#endif  // ART_HELPER_TU
+#endif  // ART_NOLICM_TU
 
 }  // namespace art
 
