@@ -169,6 +169,11 @@ using TFn = void (*)(const KParams, const int64_t, const SegIn, const SegOut, co
                      unsigned long long*);
 KFn nl_propagate(int integ, int geom, bool save, int don, int wps);
 TFn nl_tail(int geom);
+// the sampler (find_samples_new) builds, also in art_kernels_nolicm.hip: wps 2 or 3 waves per SIMD,
+// blocks: the blocks-of-steps line scan
+using SFn = void (*)(const KParams, const double, const uint64_t, const int64_t, const int64_t, double*, double*,
+                     double*, double*, int32_t*, int32_t*, unsigned long long*);
+SFn nl_sample(int wps, bool blocks);
 int helper_waves_per_simd(const KParams& P);
 // The batch size up to which launch_propagate runs every ray on a wave of its own (tail_kernel):
 // ART_SMALL_TAIL, default one ray per SIMD of the device; 0 switches it off.

@@ -2492,7 +2492,7 @@ KFn nl_propagate(int integ, int geom, bool save, int don, int wps) {
 TFn nl_tail(int geom) { return geom == GEOM_FLAT ? tail_kernel<GEOM_FLAT> : (geom == GEOM_GR ? tail_kernel<GEOM_GR> : tail_kernel<GEOM_ANY>); }
 #endif  // ART_NOLICM_TU
 
-#ifndef ART_NOLICM_TU
+
 // ---------------------------------------------------------------------------
 // find_samples_new (RayTracer.jl:1480-1653) + main_runner's erg and k_init
 // (MainRunner.jl:511-529): persistent lanes, one ray per lane, one attempt per lane per outer
@@ -3198,6 +3198,15 @@ __global__ __launch_bounds__(256, WPS) void sample_kernel(const KParams P, const
 #endif
 }
 
+#ifdef ART_NOLICM_TU
+// the sampler's builds, compiled here without MachineLICM (art_kernels_nolicm.hip)
+SFn nl_sample(int wps, bool blocks) {
+  return wps == 3 ? (blocks ? sample_kernel<3, true> : sample_kernel<3, false>)
+                  : (blocks ? sample_kernel<2, true> : sample_kernel<2, false>);
+}
+#endif  // ART_NOLICM_TU
+
+#ifndef ART_NOLICM_TU
 // ---------------------------------------------------------------------------
 // get_Prob_nonAD over groups; one thread per group (groups are one segment's crossings).
 __global__ __launch_bounds__(256) void prob_kernel(const KParams P, const int64_t nc, const double* __restrict__ pos,
@@ -3588,10 +3597,8 @@ hipError_t launch_sample(const KParams& P, double maxR, uint64_t seed, int64_t r
     if (e[0] == '2' || e[0] == '3') wps = e[0] - '0';
   if (const char* e = std::getenv("ART_SAMPLER_BLOCKS"))
     if (e[0] == '0' || e[0] == '1') blocks = e[0] == '1';
-  using SFn = void (*)(const KParams, const double, const uint64_t, const int64_t, const int64_t, double*, double*,
-                       double*, double*, int32_t*, int32_t*, unsigned long long*);
-  const SFn fn = wps == 3 ? (blocks ? sample_kernel<3, true> : sample_kernel<3, false>)
-                          : (blocks ? sample_kernel<2, true> : sample_kernel<2, false>);
+
+  const SFn fn = nl_sample(wps, blocks);
   const int grid = persistent_blocks((const void*)fn, n, 256, 1);
   hipLaunchKernelGGL(fn, dim3(grid), dim3(256), 0, s, P, maxR, seed, ray_offset, n, x, k, erg, vifty, w, att, queue);
   return hipGetLastError();

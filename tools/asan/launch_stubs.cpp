@@ -20,6 +20,7 @@ int helper_waves_per_simd(const KParams&) { return 2; }
 HFn pick_helper(const KParams&) { return nullptr; }
 KFn nl_propagate(int, int, bool, int, int) { return nullptr; }
 TFn nl_tail(int) { return nullptr; }
+SFn nl_sample(int, bool) { return nullptr; }
 hipError_t launch_sample(const KParams&, double, uint64_t, int64_t, int64_t, double*, double*, double*, double*, int32_t*,
                          int32_t*, unsigned long long*, hipStream_t, int) { return hipErrorNoDevice; }
 hipError_t launch_prob(const KParams&, int64_t, const double*, const double*, const double*, int64_t, const int64_t*,
