@@ -9,8 +9,8 @@
 # Before a call, on the CPU: build the library (python -c "import __graft_entry__ as g; g.build()") and
 # the two section-timing variants the `sections` step loads from the same source (a variant built from
 # older source lacks newer symbols and fails to load):
-#   python adiabatic_raytracer_amd/build.py --variant tools/build/libart_sect.so -DART_SECTION_TIMING
-#   python adiabatic_raytracer_amd/build.py --variant tools/build/libart_ssec.so -DART_SAMPLER_SECTIONS
+#   python adiabatic_raytracer_amd/build.py --variant tools/ab/libart_sect.so -DART_SECTION_TIMING
+#   python adiabatic_raytracer_amd/build.py --variant tools/ab/libart_ssec.so -DART_SAMPLER_SECTIONS
 # Writes gpurun_out/TAG_*; every GPU step has its own time limit; the first failure ends the run.
 TAG=${TAG:-r05fin}
 set -o pipefail
@@ -53,13 +53,13 @@ run_step() {
       timeout -k 10 300 python3 -u tools/exp_events.py flat 1000,10000,100000 0 > ${O}_events_flat.jsonl 2>> ${O}.err &&
       timeout -k 10 300 python3 -u tools/exp_events.py gr 1000,10000 0 > ${O}_events_gr.jsonl 2>> ${O}.err ;;
     sections)
-      ART_LIB=tools/build/libart_sect.so timeout -k 10 200 python3 -u tools/exp_sections.py > ${O}_sections.jsonl 2>> ${O}.err &&
-      ART_LIB=tools/build/libart_ssec.so timeout -k 10 300 python3 -u tools/exp_sampler_time.py > ${O}_sampler_sections.jsonl 2> ${O}_sampler_sections.err ;;
+      ART_LIB=tools/ab/libart_sect.so timeout -k 10 200 python3 -u tools/exp_sections.py > ${O}_sections.jsonl 2>> ${O}.err &&
+      ART_LIB=tools/ab/libart_ssec.so timeout -k 10 300 python3 -u tools/exp_sampler_time.py > ${O}_sampler_sections.jsonl 2> ${O}_sampler_sections.err ;;
     *) echo "unknown step $1"; return 2 ;;
   esac
 }
 steps=("$@")
-[ ${#steps[@]} -gt 0 ] || steps=(pytest smoke pmc bench rocprof rocprof_copies shard gr pmc_gr scan sampler tail host small events sections)
+[ ${#steps[@]} -gt 0 ] || steps=(pytest smoke pmc bench rocprof shard gr pmc_gr scan sampler tail host small events sections)
 for s in "${steps[@]}"; do
   echo "[$(date +%T)] $s"
   run_step "$s" || { echo "[$(date +%T)] $s failed"; exit 1; }
