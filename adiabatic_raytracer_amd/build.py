@@ -37,7 +37,8 @@ def stale():
     if not os.path.exists(LIB):
         return True
     t = os.path.getmtime(LIB)
-    deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS] + [os.path.join(HERE, "..", "include", "art.h")]
+    deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS] + [os.path.join(HERE, "..", "include", "art.h"),
+                                                                  os.path.abspath(__file__)]  # (the flags too)
     return any(os.path.getmtime(d) > t for d in deps)
 
 
