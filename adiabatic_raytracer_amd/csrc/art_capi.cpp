@@ -53,6 +53,7 @@ std::atomic<uint64_t> g_host_cnt[HC_N] = {};
 constexpr int RING = 64;
 struct LaunchRec {
   hipEvent_t ev0 = nullptr, ev1 = nullptr, done = nullptr;
+  hipEvent_t hot_fork = nullptr, hot_join = nullptr;  // the hot rays' side launch (art::HotSide)
   unsigned long long* host_stats = nullptr;  // N_STATS_DEV words (pinned): statistics, then the clock stamps
   int grid = 0;
   hipStream_t stream = nullptr;
@@ -103,6 +104,9 @@ struct DeviceCtx {
   int32_t donate = -1;           // tail donation (art_set_tail_donation): lanes per wave, 0 = off, -1 = by geometry
   int32_t graduate = -1;         // graduation (art_set_graduation): attempts, 0 = off, -1 = the default (2048)
   int32_t sampler_waves = 0;     // art_set_sampler_waves: 0 = by line length, 2 or 3
+  // the side stream of each stream that propagate launches ran on (the hot rays' tail launch,
+  // art::HotSide): one per caller stream, so a launch waits on no other stream's hot rays
+  std::map<hipStream_t, hipStream_t> hot_side;
   std::vector<std::pair<void*, size_t>> pool;  // host-entry staging buffers (grow-only, used under g_mu by the
                                                // synchronous *_host calls only)
   // the chunked host pipeline of art_propagate_host (propagate_host_chunked): its compute
@@ -173,6 +177,8 @@ int current_ctx(DeviceCtx** out) {
       HIP_OK(hipEventCreate(&c.ring[i].ev0));
       HIP_OK(hipEventCreate(&c.ring[i].ev1));
       HIP_OK(hipEventCreateWithFlags(&c.ring[i].done, hipEventDisableTiming));
+      HIP_OK(hipEventCreateWithFlags(&c.ring[i].hot_fork, hipEventDisableTiming));
+      HIP_OK(hipEventCreateWithFlags(&c.ring[i].hot_join, hipEventDisableTiming));
       c.ring[i].host_stats = hs + i * art::N_STATS_DEV;
     }
     // per-launch scratch comes from the stream-ordered allocator: keep what it frees cached
@@ -312,6 +318,11 @@ int env_int(const char* name, int dflt) {
   const char* e = std::getenv(name);
   return (e && *e) ? std::atoi(e) : dflt;
 }
+double env_double(const char* name, double dflt) {
+  const char* e = std::getenv(name);
+  return (e && *e) ? std::atof(e) : dflt;
+}
+constexpr size_t HOT_CAP = 1024;  // early-graduation records of one launch (SegOut::hot)
 
 // (a heap object, not a function-local static: art_shutdown joins its threads before the HIP
 // runtime's own teardown, and no static destructor of libart is left to run after it)
@@ -355,7 +366,10 @@ void release_ctx(DeviceCtx& c) {
     if (L.ev0) (void)hipEventDestroy(L.ev0);
     if (L.ev1) (void)hipEventDestroy(L.ev1);
     if (L.done) (void)hipEventDestroy(L.done);
+    for (hipEvent_t e : {L.hot_fork, L.hot_join})
+      if (e) (void)hipEventDestroy(e);
   }
+  for (auto& e : c.hot_side) (void)hipStreamDestroy(e.second);
   if (c.ring[0].host_stats) (void)hipHostFree(c.ring[0].host_stats);  // one block for the ring
   for (auto& e : c.pool)
     if (e.first) (void)hipFree(e.first);
@@ -509,7 +523,7 @@ bool use_small_tail(const art_params* p, int64_t n, const TrajArgs& tr) {
 // (init_kernel -> the integrator) | END_REC n doubles of end records | X_REC cap n doubles of
 // crossing records (the integrator -> finalize_kernel) | donation records of two levels]
 struct ScratchLayout {
-  size_t head = 256, u0b = 0, recb = 0, xrb = 0, ncont = 0, contb = 0;
+  size_t head = 256, u0b = 0, recb = 0, xrb = 0, ncont = 0, nhot = 0, contb = 0;
   size_t total() const { return head + u0b + recb + xrb + contb; }
 };
 int scratch_layout(DeviceCtx* c, int64_t n, int cap, int32_t donate, ScratchLayout* L, bool small_tail = false) {
@@ -528,8 +542,11 @@ int scratch_layout(DeviceCtx* c, int64_t n, int cap, int32_t donate, ScratchLayo
     L->ncont = std::min(nd, (size_t)ncu * 32 * (size_t)donate);
   }
   // the second level (the packed continuation's own donations, resumed by the tail kernel):
-  // never more than the first level's; then as many graduation records (SegOut::grad)
-  L->contb = (small_tail ? 2 : 3) * L->ncont * art::CONT_REC * sizeof(double);
+  // never more than the first level's; then as many graduation records (SegOut::grad) and the
+  // early-graduation records (SegOut::hot)
+  // early-graduation records (SegOut::hot) and their ready words
+  L->nhot = small_tail ? 0 : std::min(L->ncont, (size_t)HOT_CAP);
+  L->contb = ((small_tail ? 2 : 3) * L->ncont + L->nhot) * art::CONT_REC * sizeof(double) + L->nhot * sizeof(unsigned);
   return ART_OK;
 }
 
@@ -579,6 +596,7 @@ int propagate_device_impl(const art_params* p, int64_t n, const double* x0, cons
     so.traj_n = tr.count;
   }
   so.rec = rec;
+  art::HotSide hot;
   if (ncont) {
     so.cont = (double*)((char*)blk + head + u0b + recb + xrb);
     so.cont_count = words + 16;  // head words 16 .. 19 (zeroed with the head)
@@ -599,13 +617,51 @@ int propagate_device_impl(const art_params* p, int64_t n, const double* x0, cons
       // CUs it would free, profiles/r04al_graduation_in_flight.txt; round 4 decided this per launch
       // from the other streams' events, which made it depend on host timing)
       so.graduate = c->graduate >= 0 ? c->graduate : std::max(0, env_int("ART_GRADUATE", 2048));
+      // early graduation (SegOut::hot), with graduation only: from ART_HOT_AT attempts (default
+      // 128) a ray whose progress in ln t is below ART_HOT_DTAU + ART_HOT_SLOPE log2(attempts /
+      // 256) (defaults 15.95, 0.75): on configs[3] 102 rays, 90 of them past 5000 attempts, among
+      // them every one of the 20 longest (tools/exp_gr_predict.py)
+      // (only on a non-blocking stream: the side stream below is a blocking one, and work on a
+      // blocking stream -- the null stream above all -- would wait for the hot launch, which waits
+      // for this launch's own kernels)
+      unsigned sflags = 0;
+      const bool nonblocking = s != nullptr && hipStreamGetFlags(s, &sflags) == hipSuccess && (sflags & hipStreamNonBlocking);
+      if (SL.nhot && so.graduate > 0 && nonblocking) {
+        so.hot = so.grad + ncont * art::CONT_REC;
+        so.hot_ready = (unsigned*)(so.hot + SL.nhot * art::CONT_REC);
+        so.hot_count = words + 22;
+        so.hot_queue = words + 23;
+        so.hot_done = (unsigned*)(words + 26);
+        so.hot_cap = (int32_t)SL.nhot;
+        so.hot_at = std::max(0, env_int("ART_HOT_AT", 128));
+        so.hot_dtau = env_double("ART_HOT_DTAU", 15.95);
+        so.hot_slope = env_double("ART_HOT_SLOPE", 0.75);
+        auto it = c->hot_side.find(s);
+        if (it == c->hot_side.end()) {
+          // a hardware queue of its own (a stream with a CU mask gets one; the mask holds every CU):
+          // a plain stream may share one with s, and s's kernels would then queue behind the hot
+          // launch that waits for them (lane_setup, profiles/r04p_maskless_hwqueue.txt)
+          int ncu_all = 0;
+          HIP_OK(hipDeviceGetAttribute(&ncu_all, hipDeviceAttributeMultiprocessorCount, c->device));
+          std::vector<uint32_t> all((ncu_all + 31) / 32, 0u);
+          for (int i = 0; i < ncu_all; ++i) all[i / 32] |= 1u << (i % 32);
+          hipStream_t hsd = nullptr;
+          HIP_OK(hipExtStreamCreateWithCUMask(&hsd, (uint32_t)all.size(), all.data()));
+          it = c->hot_side.emplace(s, hsd).first;
+        }
+        hot.stream = it->second;
+        hot.fork = L->hot_fork;
+        hot.join = L->hot_join;
+        hot.zero_word = words + 24;  // (words 22 .. 26: zeroed with the head)
+      }
     }
     so.donate = donate;
     so.small_tail = small_tail ? 1 : 0;
   }
   HIP_OK(hipMemsetAsync(words, 0, head, s));
+  if (so.hot_ready) HIP_OK(hipMemsetAsync(so.hot_ready, 0, SL.nhot * sizeof(unsigned), s));
   HIP_OK(art::launch_propagate(K, n, in, so, max_crossings, words, words + 1, s, &L->grid, L->ev0, L->ev1,
-                               opt.finalize_stream));
+                               opt.finalize_stream, hot));
   HIP_OK(hipMemcpyAsync(L->host_stats, words + 1, sizeof(unsigned long long) * art::N_STATS_DEV, hipMemcpyDeviceToHost, s));
   HIP_OK(hipEventRecord(L->done, s));
   if (!opt.scratch) HIP_OK(hipFreeAsync(blk, s));

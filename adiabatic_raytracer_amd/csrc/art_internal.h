@@ -118,6 +118,21 @@ struct SegOut {
   double* grad;
   unsigned long long *grad_count, *grad_queue;
   int32_t grad_cap, graduate;
+  // Early graduation (DON = 1 launches with tail_kernel, art_capi.cpp): a ray whose progress
+  // in ln t since its start is below hot_dtau + hot_slope log2(attempts / 256) -- tested at every
+  // power-of-two attempt count >= hot_at, and when its drained wave donates it -- leaves for
+  // hot[0, hot_cap) at once: the count in *hot_count (it may pass hot_cap: a ray that finds no
+  // slot stays where it is), each record's hot_ready word raised once it is written.
+  // configs[3]'s longest rays crawl along the star's surface and are singled out this way
+  // (tail_kernel "hot rays"). A tail_kernel launch beside the bulk pass and the
+  // continuation claims them through *hot_queue as they arrive, until *hot_done (raised after
+  // the continuation) and none is left. hot_at 0 = off.
+  double* hot;
+  unsigned long long *hot_count, *hot_queue;
+  unsigned* hot_ready;
+  unsigned* hot_done;
+  int32_t hot_cap, hot_at;
+  double hot_dtau, hot_slope;
 };
 constexpr unsigned long long STREAM_WAIT_TICKS = 200000000ull;  // 2 s at 100 MHz
 constexpr int FLUX_HELPER_BINS = 256;  // flux bins the helpers bin themselves (2 x 256 doubles of LDS)
@@ -142,9 +157,18 @@ int persistent_blocks(const void* func, int64_t work, int block, int fallback_pe
 // integrator kernels alone. With fs (and ev1) given, finalize runs on stream fs after ev1,
 // so s can go on with its next launch while the outputs are written (the chunked host
 // pipeline writes them over PCIe into pinned memory).
+// hs: the side stream of the hot rays' tail launch (SegOut::hot), its fork and join events and two
+// zeroed device words; without them the launch does not graduate early.
+struct HotSide {
+  hipStream_t stream = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr;
+  unsigned long long* zero_word = nullptr;
+};
+constexpr unsigned long long HOT_WAIT_TICKS = 3000000000ull;  // 30 s at 100 MHz: a hot wave's bound on its wait
+constexpr int HOT_BLOCKS = 32;  // the hot rays' tail launch: 32 blocks of 4 waves (one ray a wave)
 hipError_t launch_propagate(const KParams& P, int64_t n, const SegIn& in, const SegOut& out, int32_t max_crossings,
                             unsigned long long* queue, unsigned long long* stats, hipStream_t s, int* grid_out,
-                            hipEvent_t ev0, hipEvent_t ev1, hipStream_t fs = nullptr);
+                            hipEvent_t ev0, hipEvent_t ev1, hipStream_t fs = nullptr, const HotSide& hs = HotSide());
 // The streamed host pipeline's integrator (DON = 3) with at most `blocks` persistent blocks.
 hipError_t launch_integrator_streamed(const KParams& P, int64_t n, const SegIn& in, const SegOut& out,
                                       int32_t max_crossings, unsigned long long* queue, unsigned long long* stats,
@@ -154,7 +178,7 @@ hipError_t launch_integrator_streamed(const KParams& P, int64_t n, const SegIn& 
 // announce counts each block into host_flags[64] as it starts.
 hipError_t launch_helpers(const KParams& P, int64_t n, const SegIn& in, const SegOut& out, int blocks, int64_t init_limit,
                           int announce, unsigned long long* stats, hipStream_t s);
-// The helper kernel (art_helpers.hip, its own translation unit): the instantiation for these
+// The helper kernel (art_kernels_nolicm.hip, its own translation unit): the instantiation for these
 // parameters' geometry, and its waves per SIMD (2: a helper block shares its CU with one
 // integrator block; 1: it takes the whole CU).
 using HFn = void (*)(const KParams, const int64_t, const SegIn, const SegOut, const int, const int64_t, const int64_t,

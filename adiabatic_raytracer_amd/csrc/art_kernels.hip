@@ -686,6 +686,12 @@ __device__ inline bool chunk_wait(const SegOut& out, int wnext, int leader) {
   return __shfl(ok, leader) != 0;
 }
 
+// The hot rule (SegOut::hot): a ray that has advanced less than hot_dtau + hot_slope
+// log2(attempts / 256) in ln t since its start
+__device__ inline bool hot_lags(const SegOut& out, double dtau, double log2_att_256) {
+  return dtau < out.hot_dtau + out.hot_slope * log2_att_256;
+}
+
 // DON: the tail-donation instantiations (SegOut::donate / cont_mode honoured); the others
 // carry none of that code, so a lone pass pays nothing for it
 // WPS: waves per SIMD the registers are budgeted for (the default 2; the GR continuation
@@ -1508,6 +1514,37 @@ __global__ __launch_bounds__(BLOCK, WPS) void propagate_kernel(const KParams P_i
     // for the tail kernel now instead of running on as one lane of this wave until the wave
     // drains; its lane takes the next ray. The record is the donation record, so the ray's
     // arithmetic does not change.
+    // early graduation (SegOut::hot): a ray whose progress in ln t lags the hot rule at a
+    // power-of-two attempt count, or when its drained wave donates it, leaves for the hot
+    // records, which a tail_kernel launch beside this one resumes at once (one wave per ray)
+    auto to_hot = [&](bool h) {
+      const unsigned long long hm = __ballot(h);
+      if (hm == 0ull) return;
+      const int leader = __ffsll((long long)hm) - 1;
+      unsigned long long base = 0;
+      if (lane == leader) base = atomicAdd(out.hot_count, (unsigned long long)__popcll(hm));
+      base = __shfl(base, leader);
+      const int64_t slot = (int64_t)base + __popcll(hm & ((1ull << lane) - 1ull));
+      if (h && slot < (int64_t)out.hot_cap) {  // (no slot left: the ray stays)
+        write_cont_rec(out.hot + slot * CONT_REC, u, f, tau, dt, qpow, cprev, bstart, erg, ray, n_acc, n_rej, ncross,
+                       iter, sprev, photon, cprev_ok, just_evented, save_k);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        __hip_atomic_store(out.hot_ready + slot, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ray = -1;
+        mode = M_IDLE;
+      }
+    };
+    if (DON == 1 && out.hot_at > 0) {
+      bool h = mode == M_STEP && iter >= out.hot_at && (iter & (iter - 1)) == 0;
+      if (__ballot(h) != 0ull) {
+        if (h) h = hot_lags(out, tau - in.lnt0[ray], (double)(__builtin_ctz((unsigned)iter) - 8));
+        to_hot(h);
+      }
+    }
+    // graduation (SegOut::graduate): a ray past `graduate` attempts, at a step boundary, leaves
+    // for the tail kernel now instead of running on as one lane of this wave until the wave
+    // drains; its lane takes the next ray. The record is the donation record, so the ray's
+    // arithmetic does not change.
     if (DON == 1 && out.graduate > 0) {
       const bool g = mode == M_STEP && iter >= out.graduate;
       const unsigned long long gm = __ballot(g);
@@ -1528,18 +1565,28 @@ __global__ __launch_bounds__(BLOCK, WPS) void propagate_kernel(const KParams P_i
     // tail donation (SegOut::donate): the drained wave's last few rays, all at a step
     // boundary, leave for the continuation launch and the wave retires
     if (DON == 1 && exhausted && out.donate > 0) {
-      const unsigned long long live = __ballot(mode != M_IDLE);
+      unsigned long long live = __ballot(mode != M_IDLE);
       if (live != 0ull && __popcll(live) <= out.donate && __ballot(mode == M_ROOT) == 0ull) {
-        const int leader = __ffsll((long long)live) - 1;
-        unsigned long long base = 0;
-        if (lane == leader) base = atomicAdd(out.cont_count, (unsigned long long)__popcll(live));
-        base = __shfl(base, leader);
-        if (mode != M_IDLE) {
-          const int64_t slot = (int64_t)base + __popcll(live & ((1ull << lane) - 1ull));
-          write_cont_rec(out.cont + slot * CONT_REC, u, f, tau, dt, qpow, cprev, bstart, erg, ray, n_acc, n_rej,
-                         ncross, iter, sprev, photon, cprev_ok, just_evented, save_k);
-          ray = -1;
-          mode = M_IDLE;
+        if (out.hot_at > 0) {  // (the lagging ones to the hot records instead)
+          bool h = mode == M_STEP && iter >= out.hot_at;
+          if (__ballot(h) != 0ull) {
+            if (h) h = hot_lags(out, tau - in.lnt0[ray], log2((double)iter) - 8.0);
+            to_hot(h);
+            live = __ballot(mode != M_IDLE);
+          }
+        }
+        if (live != 0ull) {
+          const int leader = __ffsll((long long)live) - 1;
+          unsigned long long base = 0;
+          if (lane == leader) base = atomicAdd(out.cont_count, (unsigned long long)__popcll(live));
+          base = __shfl(base, leader);
+          if (mode != M_IDLE) {
+            const int64_t slot = (int64_t)base + __popcll(live & ((1ull << lane) - 1ull));
+            write_cont_rec(out.cont + slot * CONT_REC, u, f, tau, dt, qpow, cprev, bstart, erg, ray, n_acc, n_rej,
+                           ncross, iter, sprev, photon, cprev_ok, just_evented, save_k);
+            ray = -1;
+            mode = M_IDLE;
+          }
         }
       }
     }
@@ -1641,13 +1688,55 @@ __device__ inline void tail_rhs(const KParams& P, int lane, const double* y, dou
   }
 }
 
+// The next hot record (SegOut::hot) for this wave, -1 once none is left: claimed as the records
+// arrive until *hot_done is raised (then the count is final) or the wait passes HOT_WAIT_TICKS,
+// and read only once its hot_ready word is up.
+__device__ inline int64_t claim_hot(const SegOut& out, int lane) {
+  long long rec = -1;
+  if (lane == 0) {
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    const unsigned long long cap = (unsigned long long)out.hot_cap;
+    while (true) {
+      const bool done = __hip_atomic_load(out.hot_done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
+      unsigned long long q = __hip_atomic_load(out.hot_queue, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      unsigned long long c = __hip_atomic_load(out.hot_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      c = c < cap ? c : cap;
+      if (q < c) {
+        if (__hip_atomic_compare_exchange_strong(out.hot_queue, &q, q + 1ull, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT)) {
+          rec = (long long)q;
+          break;
+        }
+        continue;
+      }
+      if (done || __builtin_amdgcn_s_memrealtime() - t0 > HOT_WAIT_TICKS) break;
+      __builtin_amdgcn_s_sleep(64);
+    }
+    if (rec >= 0) {  // (its producer raises it right after the record; bounded all the same)
+      while (__hip_atomic_load(out.hot_ready + rec, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
+        if (__builtin_amdgcn_s_memrealtime() - t0 > 2ull * HOT_WAIT_TICKS) {
+          rec = -1;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(8);
+      }
+    }
+  }
+  rec = (long long)(((unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)(unsigned)rec, 0)) |
+                    ((unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)((unsigned long long)rec >> 32), 0) << 32));
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  return (int64_t)rec;
+}
+
+// (blocks of up to 4 waves, each wave a ray of its own: the hot rays' launch packs its waves
+// into few CUs, the others launch one wave a block)
 template <int GEOM>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void tail_kernel(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void tail_kernel(
     const KParams P_in, const int64_t n, const SegIn in, const SegOut out, const int32_t max_crossings,
     const int32_t max_rays, unsigned long long* __restrict__ stats) {
   const KParams P = specialize<GEOM>(P_in);
   using V = Vern6;
-  const int lane = threadIdx.x;
+  const int lane = threadIdx.x & 63;
   // Every lane holds the ray's state alike, so its control decisions are wave-uniform: U() makes
   // that visible to the compiler (a scalar branch on lane 0's value instead of an exec-mask
   // branch with its saved masks -- SGPRs the kernel otherwise spills to VGPR lanes); the values
@@ -1668,9 +1757,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
                                                                                    : (int64_t)out.grad_cap)
                               : 0;
   bool grads = ng > 0;
+  bool hots = out.hot != nullptr;
   span_stamp(stats, false);
   while (true) {
     const double* src = nullptr;
+    if (hots) {  // the hot rays first (a launch beside the bulk pass waits for them)
+      const int64_t rec = claim_hot(out, lane);
+      if (rec >= 0) src = out.hot + rec * CONT_REC;
+      else hots = false;
+    }
     while (src == nullptr) {
       unsigned long long* q = grads ? out.grad_queue : out.cont_queue;
       unsigned long long ix = 0;
@@ -3433,9 +3528,17 @@ static bool w1_builds() {
   return on;
 }
 
+// Raises a launch's *hot_done once the kernels that write hot records have ended (stream order).
+__global__ void hot_done_kernel(unsigned* w) {
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __hip_atomic_store(w, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 hipError_t launch_propagate(const KParams& P, int64_t n, const SegIn& in, const SegOut& out_arg, int32_t max_crossings,
                             unsigned long long* queue, unsigned long long* stats, hipStream_t s, int* grid_out,
-                            hipEvent_t ev0, hipEvent_t ev1, hipStream_t fs) {
+                            hipEvent_t ev0, hipEvent_t ev1, hipStream_t fs, const HotSide& hs) {
   const int64_t gr = (n + 255) / 256;
   const unsigned g1 = (unsigned)((n + 255) / 256);
 #define ART_DBG(stage)
@@ -3453,6 +3556,14 @@ hipError_t launch_propagate(const KParams& P, int64_t n, const SegIn& in, const 
   if (out.small_tail || !(out.donate > 0 && tail_rays() != 0 && !rk4 && out.ntimes < 2 && out.cont2)) {
     out.grad = nullptr;
     out.graduate = 0;
+  }
+  // early graduation (SegOut::hot): only with graduation, and with the side stream that the hot
+  // rays' tail launch runs on beside the bulk pass and the continuation
+  const bool hot = out.graduate > 0 && out.hot && out.hot_ready && out.hot_done && out.hot_at > 0 && out.hot_cap > 0 &&
+                   hs.stream && hs.fork && hs.join && hs.zero_word;
+  if (!hot) {
+    out.hot = nullptr;
+    out.hot_at = 0;
   }
   if (out.small_tail) {  // a small Vern6 batch: every ray on a wave of its own (tail_kernel)
     int dev = 0, ncu = 0;
@@ -3500,19 +3611,47 @@ hipError_t launch_propagate(const KParams& P, int64_t n, const SegIn& in, const 
     }
   }
   // (the integrator's blocks per CU by design: its waves per SIMD, 4 waves a block)
-  const int grid = persistent_blocks((const void*)fn, n, BLOCK, w1 ? 1 : ART_WAVES_PER_SIMD * 4 / (BLOCK / 64));
+  int grid = persistent_blocks((const void*)fn, n, BLOCK, w1 ? 1 : ART_WAVES_PER_SIMD * 4 / (BLOCK / 64));
   ART_DBG("persistent_blocks")
+  // the hot rays' launch: HOT_BLOCKS blocks of 4 waves, each beside one integrator block on a CU
+  // (one wave of each per SIMD), so the bulk pass gives up that many of its blocks
+  if (hot) grid = grid > 2 * HOT_BLOCKS ? grid - HOT_BLOCKS : grid;
   if (grid_out) *grid_out = grid;
   if (ev0 && (e = hipEventRecord(ev0, s)) != hipSuccess) return e;
+  if (hot) {
+    // on the side stream from the bulk pass's start: each wave resumes a hot record as soon as
+    // one is written (one wave per ray, the tail kernel's arithmetic) and leaves once *hot_done is
+    // raised after the continuation and none is left
+    if ((e = hipEventRecord(hs.fork, s)) != hipSuccess) return e;
+    if ((e = hipStreamWaitEvent(hs.stream, hs.fork, 0)) != hipSuccess) return e;
+    SegOut oh = out;
+    oh.grad = nullptr;
+    oh.graduate = 0;
+    oh.hot_at = 0;
+    oh.cont_count = hs.zero_word;  // (no drained-wave records: word 0 stays zero, word 1 is its queue)
+    oh.cont_queue = hs.zero_word + 1;
+    hipLaunchKernelGGL(nl_tail(flat ? GEOM_FLAT : (sch ? GEOM_GR : GEOM_ANY)), dim3(HOT_BLOCKS), dim3(256), 0,
+                       hs.stream, P, n, in, oh, max_crossings, 4 * HOT_BLOCKS, stats);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if ((e = hipEventRecord(hs.join, hs.stream)) != hipSuccess) return e;
+  }
+  // (from here on every return raises *hot_done first, so the hot waves never wait past it)
+  auto hot_done = [&](hipError_t err) {
+    if (hot) {
+      hipLaunchKernelGGL(hot_done_kernel, dim3(1), dim3(64), 0, s, out.hot_done);
+      if (err == hipSuccess) err = hipGetLastError();
+    }
+    return err;
+  };
   hipLaunchKernelGGL(fn, dim3(grid), dim3(BLOCK), 0, s, P, n, in, out, max_crossings, queue, stats);
   ART_DBG("propagate_kernel")
-  if ((e = hipGetLastError()) != hipSuccess) return e;
+  if ((e = hipGetLastError()) != hipSuccess) return hot_done(e);
   if (out.donate > 0) {  // the donated tail rays, packed into full waves (at most waves x donate of them)
     // with the tail kernel (ART_TAIL != 0, Vern6 without saveat) the packed continuation donates
     // in its turn: its drained waves' last rays (at most ART_TAIL_DONATE each, default 4) go to
     // the second-level records, and tail_kernel resumes each of those on a wave of its own
     const bool tail = tail_rays() != 0 && !rk4 && out.ntimes < 2 && out.cont2;
-    SegOut oc = out;
+    SegOut oc = out;  // (the continuation sends its lagging rays to the hot records too)
     oc.cont_mode = 1;
     oc.cont_src = out.cont;
     oc.cont_src_count = out.cont_count;
@@ -3527,7 +3666,8 @@ hipError_t launch_propagate(const KParams& P, int64_t n, const SegIn& in, const 
     const KFn cfn = (w1_builds() && sch && !rk4 && out.ntimes < 2) ? nl_propagate(ART_VERN6, GEOM_GR, false, 1, 1) : fn;
     hipLaunchKernelGGL(cfn, dim3(cgrid), dim3(BLOCK), 0, s, P, n, in, oc, max_crossings, queue, stats);
     ART_DBG("continuation")
-    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if ((e = hipGetLastError()) != hipSuccess) return hot_done(e);
+    if ((e = hot_done(hipSuccess)) != hipSuccess) return e;
     if (tail) {
       int dev = 0, ncu = 0;
       (void)hipGetDevice(&dev);
@@ -3546,7 +3686,10 @@ hipError_t launch_propagate(const KParams& P, int64_t n, const SegIn& in, const 
       ART_DBG("tail_kernel")
       if ((e = hipGetLastError()) != hipSuccess) return e;
     }
+  } else if ((e = hot_done(hipSuccess)) != hipSuccess) {
+    return e;
   }
+  if (hot && (e = hipStreamWaitEvent(s, hs.join, 0)) != hipSuccess) return e;
   if (ev1 && (e = hipEventRecord(ev1, s)) != hipSuccess) return e;
   hipStream_t sf = s;
   if (fs && ev1 && fs != s) {

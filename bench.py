@@ -339,11 +339,13 @@ def main():
         def device_run(nstreams, donate_lanes, steps, warmup):
             eng.set_tail_donation(donate_lanes)
             eng.set_graduation(0 if nstreams > 1 else -1)  # (batches in flight: off, include/art.h)
-            streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(nstreams - 1)]
+            # (non-blocking streams, as a host keeping batches in flight uses: the GR batch's
+            # early graduation runs only on one, include/art.h)
+            streams = [torch.cuda.Stream() for _ in range(nstreams)]
             outs = [eng.alloc_out(n, capacity=1) for _ in streams]
             hists = [torch.zeros(2 * args.nbins, dtype=torch.float64, device=eng.device) for _ in streams]
-            for st_ in streams[1:]:
-                st_.wait_stream(streams[0])  # the sampled inputs and the outputs' initialisation
+            for st_ in streams:
+                st_.wait_stream(torch.cuda.current_stream())  # the sampled inputs and the outputs' initialisation
 
             def one_step(i):
                 k = i % len(streams)

@@ -180,7 +180,13 @@ int art_set_tail_donation(int32_t lanes);
  * for their waves to drain (configs[3] as one batch: 260-297 -> 230 ms). 0 switches it off -- for
  * a host that keeps several batches in flight, where each graduated ray would hold a whole tail
  * wave while the other batches fill the CUs it frees; -1 (the default) = 2048 attempts (or
- * ART_GRADUATE). Per device; results are bit-identical either way. */
+ * ART_GRADUATE). Per device; results are bit-identical either way.
+ * With graduation on, a launch on a non-blocking stream also graduates early: from 128 attempts
+ * on, a ray whose progress in ln t lags 15.95 + 0.75 log2(attempts / 256) (ART_HOT_AT,
+ * ART_HOT_DTAU, ART_HOT_SLOPE) -- on configs[3] the rays that crawl along the star's surface,
+ * every one of its 20 longest among them -- leaves at once for a tail-kernel launch that runs on
+ * a side stream beside the bulk pass (configs[3] as one batch: 226 -> 203 ms). Not on the null
+ * stream or another blocking stream, whose work would wait for that side launch. */
 int art_set_graduation(int32_t attempts);
 /* Waves per SIMD of the conversion-point sampler (art_sample_conversion_points*): 0 (the default)
  * chooses by line length -- 3 for lines up to 2.2 x 60 km, walked step by step, else 2 with blocks

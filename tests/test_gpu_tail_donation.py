@@ -17,10 +17,13 @@ def _run(eng, inp, lanes):
     import torch
     import adiabatic_raytracer_amd as A
     eng.set_tail_donation(lanes)
+    torch.cuda.synchronize()
     try:
-        out = eng.propagate(inp, max_crossings=-1)
-        eng.kernel_ms()
-        st = dict(A.raytracer.last_stats())
+        # (a non-blocking stream: early graduation, SegOut::hot, runs only on one)
+        with torch.cuda.stream(torch.cuda.Stream()):
+            out = eng.propagate(inp, max_crossings=-1)
+            eng.kernel_ms()
+            st = dict(A.raytracer.last_stats())
     finally:
         eng.set_tail_donation(-1)
     torch.cuda.synchronize()
@@ -73,6 +76,32 @@ def test_graduation_is_bit_exact(cfg, graduate, monkeypatch):
         assert np.array_equal(a, b, equal_nan=True), (cfg, graduate, k)
     for k in ("attempts", "accepted", "root_steps", "scan_evals", "rays", "cert_steps"):
         assert sref[k] == sgot[k], (cfg, graduate, k, sref[k], sgot[k])
+
+
+@pytest.mark.parametrize("cfg", ["flat", "gr", "gr_oblique"])
+@pytest.mark.parametrize("hot", [("16", "1e9"), ("64", "14"), ("128", "15.95")], ids=["every_ray", "some", "default"])
+def test_early_graduation_is_bit_exact(cfg, hot, monkeypatch):
+    """ART_HOT_AT=a, ART_HOT_DTAU=d (SegOut::hot): from a attempts on, a ray whose progress in ln t
+    lags d + 0.75 log2(attempts / 256) leaves for the hot records at once, and a tail_kernel
+    launch beside the bulk pass resumes it as soon as its record is written. a=16, d=1e9 sends
+    every ray alive at 16 attempts (and overflows the 1024 records, so the rest stay in place);
+    128/15.95 is the default. Outputs and counters equal the undonated run bit for bit."""
+    monkeypatch.setenv("ART_HOT_AT", hot[0])
+    monkeypatch.setenv("ART_HOT_DTAU", hot[1])
+    import adiabatic_raytracer_amd as A
+    from adiabatic_raytracer_amd import Engine
+    eng = Engine(A.Params(**CONFIGS[cfg]))
+    inp = eng.forward_roots(N, seed=1769)
+    ref, sref = _run(eng, inp, 0)
+    has = ref["n_cross"] > 0
+    got, sgot = _run(eng, inp, 16)
+    for k in ref:
+        a, b = ref[k], got[k]
+        if k.startswith("xc_"):
+            a, b = a.reshape(-1, N)[:, has], b.reshape(-1, N)[:, has]
+        assert np.array_equal(a, b, equal_nan=True), (cfg, hot, k)
+    for k in ("attempts", "accepted", "root_steps", "scan_evals", "rays", "cert_steps"):
+        assert sref[k] == sgot[k], (cfg, hot, k, sref[k], sgot[k])
 
 
 def test_tail_donation_rejects_bad_lane_counts():

@@ -17,6 +17,11 @@
 
 #include "../adiabatic_raytracer_amd/csrc/art_core.h"
 
+#ifndef CPU_SAME_ATTEMPT_HOOK  // (tools/exp_gr_predict.cpp: per-attempt probes of the same loop)
+#define CPU_SAME_ATTEMPT_HOOK(attempts, tau, u)
+#define CPU_SAME_RAY_HOOK(ray)
+#endif
+
 using namespace art;
 
 namespace {
@@ -182,6 +187,7 @@ struct Segment {
     for (int64_t iter = 0;; ++iter) {
       if (tau >= tend) return ART_STATUS_SUCCESS;
       if (iter >= P.maxiters) return ART_STATUS_MAXITERS;
+      CPU_SAME_ATTEMPT_HOOK(n_acc + n_rej, tau, u);
       double h = dt;
       bool last = false, forced = false;
       if (tau + h >= tend) { h = tend - tau; last = true; }
@@ -298,6 +304,7 @@ void cpu_same_propagate(const art_params* p, int64_t n, const double* x0, const 
   const KParams P = make_kparams(*p);
 #pragma omp parallel for schedule(dynamic, 16) num_threads(nthreads > 0 ? nthreads : 1)
   for (int64_t i = 0; i < n; ++i) {
+    CPU_SAME_RAY_HOOK(i);
     const double xi[3] = {x0[i], x0[n + i], x0[2 * n + i]}, ki[3] = {k0[i], k0[n + i], k0[2 * n + i]};
     const bool photon = species[i] != ART_AXION;
     double u[7];
