@@ -521,10 +521,11 @@ bool use_small_tail(const art_params* p, int64_t n, const TrajArgs& tr) {
 
 // this launch's scratch: [queue head + statistics (256 B) | u0: U0_REC n doubles of fresh state
 // (init_kernel -> the integrator) | END_REC n doubles of end records | X_REC cap n doubles of
-// crossing records (the integrator -> finalize_kernel) | donation records of two levels]
+// crossing records (the integrator -> finalize_kernel) | donation records of two levels, the
+// graduation and early-graduation records (and the latter's ready words) | the claim order's sort]
 struct ScratchLayout {
-  size_t head = 256, u0b = 0, recb = 0, xrb = 0, ncont = 0, nhot = 0, contb = 0;
-  size_t total() const { return head + u0b + recb + xrb + contb; }
+  size_t head = 256, u0b = 0, recb = 0, xrb = 0, ncont = 0, nhot = 0, contb = 0, ordb = 0;
+  size_t total() const { return head + u0b + recb + xrb + contb + ordb; }
 };
 int scratch_layout(DeviceCtx* c, int64_t n, int cap, int32_t donate, ScratchLayout* L, bool small_tail = false) {
   const size_t nd = (size_t)n;
@@ -547,6 +548,8 @@ int scratch_layout(DeviceCtx* c, int64_t n, int cap, int32_t donate, ScratchLayo
   // early-graduation records (SegOut::hot) and their ready words
   L->nhot = small_tail ? 0 : std::min(L->ncont, (size_t)HOT_CAP);
   L->contb = ((small_tail ? 2 : 3) * L->ncont + L->nhot) * art::CONT_REC * sizeof(double) + L->nhot * sizeof(unsigned);
+  // (then the claim order's sort, SegOut::order)
+  L->ordb = L->nhot ? art::claim_order_bytes(n) + 256 : 0;
   return ART_OK;
 }
 
@@ -636,6 +639,10 @@ int propagate_device_impl(const art_params* p, int64_t n, const double* x0, cons
         so.hot_at = std::max(0, env_int("ART_HOT_AT", 128));
         so.hot_dtau = env_double("ART_HOT_DTAU", 15.95);
         so.hot_slope = env_double("ART_HOT_SLOPE", 0.75);
+        if (SL.ordb && env_int("ART_HOT_ORDER", 1)) {  // (256-byte aligned)
+          const uintptr_t o = (uintptr_t)blk + SL.total() - SL.ordb;
+          so.order_tmp = (void*)((o + 255) & ~(uintptr_t)255);
+        }
         auto it = c->hot_side.find(s);
         if (it == c->hot_side.end()) {
           // a hardware queue of its own (a stream with a CU mask gets one; the mask holds every CU):

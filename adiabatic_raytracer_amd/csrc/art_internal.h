@@ -133,6 +133,12 @@ struct SegOut {
   unsigned* hot_done;
   int32_t hot_cap, hot_at;
   double hot_dtau, hot_slope;
+  // The bulk pass's claim order with early graduation (launch_propagate sorts it; null: ray index
+  // order): the rays by their initial step size, smallest first -- configs[3]'s 20 longest rays
+  // are among the 1066 with the smallest (tools/exp_gr_predict.py), so they start at once and reach
+  // their hot test within the first few milliseconds. order_tmp: claim_order_bytes(n) of scratch.
+  const int32_t* order;
+  void* order_tmp;
 };
 constexpr unsigned long long STREAM_WAIT_TICKS = 200000000ull;  // 2 s at 100 MHz
 constexpr int FLUX_HELPER_BINS = 256;  // flux bins the helpers bin themselves (2 x 256 doubles of LDS)
@@ -164,6 +170,7 @@ struct HotSide {
   hipEvent_t fork = nullptr, join = nullptr;
   unsigned long long* zero_word = nullptr;
 };
+size_t claim_order_bytes(int64_t n);
 constexpr unsigned long long HOT_WAIT_TICKS = 3000000000ull;  // 30 s at 100 MHz: a hot wave's bound on its wait
 constexpr int HOT_BLOCKS = 32;  // the hot rays' tail launch: 32 blocks of 4 waves (one ray a wave)
 hipError_t launch_propagate(const KParams& P, int64_t n, const SegIn& in, const SegOut& out, int32_t max_crossings,

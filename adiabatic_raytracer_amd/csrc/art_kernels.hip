@@ -21,6 +21,9 @@
 #include "art_core.h"
 #include "art_event.h"
 #include "art_internal.h"
+#ifndef ART_NOLICM_TU
+#include <hipcub/hipcub.hpp>
+#endif
 
 namespace art {
 
@@ -842,7 +845,7 @@ __global__ __launch_bounds__(BLOCK, WPS) void propagate_kernel(const KParams P_i
           cprev_ok = (i1.z >> 1) & 1;
           just_evented = (i1.z >> 2) & 1;
         } else if (mode == M_IDLE && rank < take) {
-          ray = wnext + rank;
+          ray = (DON == 1 && out.order) ? out.order[wnext + rank] : wnext + rank;
           mode = M_STEP;
           // fresh segment: u0, f(u0), the initial dt and the initial condition value, all
           // precomputed by the init pass, with erg, ln t0 and the species: one 160-byte record
@@ -3528,6 +3531,37 @@ static bool w1_builds() {
   return on;
 }
 
+// The claim order (SegOut::order): 32-bit keys of the rays' initial step sizes (positive floats sort
+// as their bits), the ray ids beside them, one stable radix sort.
+__global__ void order_keys_kernel(int64_t n, const double* __restrict__ u0, unsigned* __restrict__ keys,
+                                  int32_t* __restrict__ ids) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) {
+    keys[i] = __float_as_uint((float)u0[i * U0_REC + 14]);
+    ids[i] = (int32_t)i;
+  }
+}
+struct OrderLayout {
+  size_t keys_in, keys_out, ids_in, ids_out, tmp, tmp_bytes, total;
+};
+static OrderLayout order_layout(int64_t n) {
+  auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+  OrderLayout L{};
+  size_t tb = 0;
+  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, tb, (const unsigned*)nullptr, (unsigned*)nullptr,
+                                           (const int32_t*)nullptr, (int32_t*)nullptr, (int)n);
+  const size_t k = al((size_t)n * 4);
+  L.keys_in = 0;
+  L.keys_out = k;
+  L.ids_in = 2 * k;
+  L.ids_out = 3 * k;
+  L.tmp = 4 * k;
+  L.tmp_bytes = tb;
+  L.total = 4 * k + al(tb);
+  return L;
+}
+size_t claim_order_bytes(int64_t n) { return n > 0 && n < INT32_MAX ? order_layout(n).total : 0; }
+
 // Raises a launch's *hot_done once the kernels that write hot records have ended (stream order).
 __global__ void hot_done_kernel(unsigned* w) {
   if (threadIdx.x == 0) {
@@ -3564,6 +3598,21 @@ hipError_t launch_propagate(const KParams& P, int64_t n, const SegIn& in, const 
   if (!hot) {
     out.hot = nullptr;
     out.hot_at = 0;
+  }
+  out.order = nullptr;
+  if (hot && out.order_tmp && !out.small_tail && n < INT32_MAX) {
+    // the bulk pass claims the rays smallest initial step first (SegOut::order)
+    const OrderLayout L = order_layout(n);
+    char* b = (char*)out.order_tmp;
+    hipLaunchKernelGGL(order_keys_kernel, dim3(g1), dim3(256), 0, s, n, in.u0, (unsigned*)(b + L.keys_in),
+                       (int32_t*)(b + L.ids_in));
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    size_t tb = L.tmp_bytes;
+    if ((e = hipcub::DeviceRadixSort::SortPairs(b + L.tmp, tb, (const unsigned*)(b + L.keys_in),
+                                                (unsigned*)(b + L.keys_out), (const int32_t*)(b + L.ids_in),
+                                                (int32_t*)(b + L.ids_out), (int)n, 0, 32, s)) != hipSuccess)
+      return e;
+    out.order = (const int32_t*)(b + L.ids_out);
   }
   if (out.small_tail) {  // a small Vern6 batch: every ray on a wave of its own (tail_kernel)
     int dev = 0, ncu = 0;

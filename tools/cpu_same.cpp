@@ -18,7 +18,7 @@
 #include "../adiabatic_raytracer_amd/csrc/art_core.h"
 
 #ifndef CPU_SAME_ATTEMPT_HOOK  // (tools/exp_gr_predict.cpp: per-attempt probes of the same loop)
-#define CPU_SAME_ATTEMPT_HOOK(attempts, tau, u)
+#define CPU_SAME_ATTEMPT_HOOK(attempts, tau, u, dt)
 #define CPU_SAME_RAY_HOOK(ray)
 #endif
 
@@ -187,7 +187,7 @@ struct Segment {
     for (int64_t iter = 0;; ++iter) {
       if (tau >= tend) return ART_STATUS_SUCCESS;
       if (iter >= P.maxiters) return ART_STATUS_MAXITERS;
-      CPU_SAME_ATTEMPT_HOOK(n_acc + n_rej, tau, u);
+      CPU_SAME_ATTEMPT_HOOK(n_acc + n_rej, tau, u, dt);
       double h = dt;
       bool last = false, forced = false;
       if (tau + h >= tend) { h = tend - tau; last = true; }

@@ -36,7 +36,7 @@ if __name__ == "__main__":
     erg = inp["erg"].cpu().numpy()
     lib = C.CDLL(LIB)
     cpu_same._lib = lib
-    probe = np.full((N, 8, 2), np.nan, np.float32)
+    probe = np.full((N, 9, 2), np.nan, np.float32)
     lib.exp_set_probe(probe.ctypes.data_as(C.c_void_p))
     p = O.make_params(theta_m=0.0, mass_a=1e-6, flat=False)
     t = time.time()
@@ -44,6 +44,7 @@ if __name__ == "__main__":
     print("cpu", time.time() - t, flush=True)
     att = r["n_accept"] + r["n_reject"]
     keep = np.nonzero(att > 128)[0]
+    np.savez_compressed("gpurun_out/gr_predict_all.npz", att=att.astype(np.int32), dt0=probe[:, 8, 0], r0=probe[:, 8, 1])
     os.makedirs("gpurun_out", exist_ok=True)
     np.savez_compressed("gpurun_out/gr_predict.npz", ray=keep, att=att[keep], status=r["status"][keep],
                         tau_end=r["tau_end"][keep], probe=probe[keep], att_hist=np.bincount(np.minimum(att, 100000)))
