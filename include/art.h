@@ -185,8 +185,9 @@ int art_set_tail_donation(int32_t lanes);
  * on, a ray whose progress in ln t lags 15.95 + 0.75 log2(attempts / 256) (ART_HOT_AT,
  * ART_HOT_DTAU, ART_HOT_SLOPE) -- on configs[3] the rays that crawl along the star's surface,
  * every one of its 20 longest among them -- leaves at once for a tail-kernel launch that runs on
- * a side stream beside the bulk pass (configs[3] as one batch: 226 -> 203 ms). Not on the null
- * stream or another blocking stream, whose work would wait for that side launch. */
+ * a side stream beside the bulk pass, and the bulk pass claims its rays smallest initial step
+ * first (configs[3] as one batch: 226 -> 188 ms). Not on the null stream or another blocking
+ * stream, whose work would wait for that side launch. */
 int art_set_graduation(int32_t attempts);
 /* Waves per SIMD of the conversion-point sampler (art_sample_conversion_points*): 0 (the default)
  * chooses by line length -- 3 for lines up to 2.2 x 60 km, walked step by step, else 2 with blocks

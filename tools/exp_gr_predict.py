@@ -17,6 +17,9 @@ import cpu_same  # noqa: E402
 
 N = int(sys.argv[1]) if len(sys.argv) > 1 and sys.argv[1].isdigit() else 1000000
 THREADS = int(os.environ.get("THREADS", "16"))
+CFG = {"gr": dict(theta_m=0.0, mass_a=1e-6, flat=False), "flat": dict(theta_m=0.2, mass_a=1e-5, flat=True)}[
+    os.environ.get("CONFIG", "gr")]  # (bench.py's configs; CONFIG=flat: the headline's)
+TAG = "" if os.environ.get("CONFIG", "gr") == "gr" else "_" + os.environ["CONFIG"]
 LIB = os.path.join(HERE, "build", "libexp_gr_predict.so")
 
 if __name__ == "__main__":
@@ -29,7 +32,7 @@ if __name__ == "__main__":
     import adiabatic_raytracer_amd as A
     from adiabatic_raytracer_amd import Engine
     import oracle as O
-    eng = Engine(A.Params(theta_m=0.0, mass_a=1e-6, flat=False))
+    eng = Engine(A.Params(**CFG))
     inp = eng.forward_roots(N, seed=1769)
     x0 = inp["x0"].cpu().numpy()
     k0 = inp["k0"].cpu().numpy()
@@ -38,14 +41,14 @@ if __name__ == "__main__":
     cpu_same._lib = lib
     probe = np.full((N, 9, 2), np.nan, np.float32)
     lib.exp_set_probe(probe.ctypes.data_as(C.c_void_p))
-    p = O.make_params(theta_m=0.0, mass_a=1e-6, flat=False)
+    p = O.make_params(**CFG)
     t = time.time()
     r = cpu_same.propagate(p, x0, k0, erg, -1.0, -30.0, 1, max_crossings=-1, nthreads=THREADS)
     print("cpu", time.time() - t, flush=True)
     att = r["n_accept"] + r["n_reject"]
     keep = np.nonzero(att > 128)[0]
-    np.savez_compressed("gpurun_out/gr_predict_all.npz", att=att.astype(np.int32), dt0=probe[:, 8, 0], r0=probe[:, 8, 1])
+    np.savez_compressed(f"gpurun_out/gr_predict_all{TAG}.npz", att=att.astype(np.int32), dt0=probe[:, 8, 0], r0=probe[:, 8, 1])
     os.makedirs("gpurun_out", exist_ok=True)
-    np.savez_compressed("gpurun_out/gr_predict.npz", ray=keep, att=att[keep], status=r["status"][keep],
+    np.savez_compressed(f"gpurun_out/gr_predict{TAG}.npz", ray=keep, att=att[keep], status=r["status"][keep],
                         tau_end=r["tau_end"][keep], probe=probe[keep], att_hist=np.bincount(np.minimum(att, 100000)))
     print("rays past 128 attempts", keep.size, "max", att.max(), "argmax", att.argmax(), flush=True)
