@@ -5,6 +5,7 @@
 
 namespace art {
 int persistent_blocks(const void*, int64_t, int, int) { return 1; }
+size_t claim_order_bytes(int64_t) { return 0; }
 hipError_t launch_propagate(const KParams&, int64_t, const SegIn&, const SegOut&, int32_t, unsigned long long*,
                             unsigned long long*, hipStream_t, int*, hipEvent_t, hipEvent_t, hipStream_t, const HotSide&) {
   return hipErrorNoDevice;
