@@ -635,7 +635,6 @@ int propagate_device_impl(const art_params* p, int64_t n, const double* x0, cons
         so.hot_count = words + 22;
         so.hot_queue = words + 23;
         so.hot_done = (unsigned*)(words + 26);
-        so.hot_started = (unsigned*)(words + 27);
         so.hot_cap = (int32_t)SL.nhot;
         so.hot_at = std::max(0, env_int("ART_HOT_AT", 128));
         so.hot_dtau = env_double("ART_HOT_DTAU", 15.95);
@@ -660,7 +659,7 @@ int propagate_device_impl(const art_params* p, int64_t n, const double* x0, cons
         hot.stream = it->second;
         hot.fork = L->hot_fork;
         hot.join = L->hot_join;
-        hot.zero_word = words + 24;  // (words 22 .. 27: zeroed with the head)
+        hot.zero_word = words + 24;  // (words 22 .. 26: zeroed with the head)
       }
     }
     so.donate = donate;

@@ -131,7 +131,6 @@ struct SegOut {
   unsigned long long *hot_count, *hot_queue;
   unsigned* hot_ready;
   unsigned* hot_done;
-  unsigned* hot_started;  // raised by the integrator's waves as they start (see claim_hot)
   int32_t hot_cap, hot_at;
   double hot_dtau, hot_slope;
   // The bulk pass's claim order with early graduation (launch_propagate sorts it; null: ray index
@@ -172,11 +171,11 @@ struct HotSide {
   unsigned long long* zero_word = nullptr;
 };
 size_t claim_order_bytes(int64_t n);
-constexpr unsigned long long HOT_WAIT_TICKS = 3000000000ull;  // 30 s at 100 MHz: a hot wave's bound on its wait
-// 50 ms: a hot wave that has seen no integrator wave start by then leaves (a profiler that
-// serialises kernels runs the launch's integrator only after it; its hot rays then go to the
-// tail launch after the continuation)
-constexpr unsigned long long HOT_START_TICKS = 5000000ull;
+// 200 ms at 100 MHz: a hot wave that has waited this long for a record leaves (the records still
+// to come, if any, go to the tail launch after the continuation). In a 10^6-ray GR launch the
+// hot records arrive within the first ~70 ms; a profiler that serialises kernels runs the
+// continuation, and so the raising of *hot_done, only after this launch has ended.
+constexpr unsigned long long HOT_WAIT_TICKS = 20000000ull;
 constexpr int HOT_BLOCKS = 32;  // the hot rays' tail launch: 32 blocks of 4 waves (one ray a wave)
 hipError_t launch_propagate(const KParams& P, int64_t n, const SegIn& in, const SegOut& out, int32_t max_crossings,
                             unsigned long long* queue, unsigned long long* stats, hipStream_t s, int* grid_out,

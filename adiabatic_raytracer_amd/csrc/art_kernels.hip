@@ -777,8 +777,6 @@ __global__ __launch_bounds__(BLOCK, WPS) void propagate_kernel(const KParams P_i
 #endif
 #pragma unroll
   for (int i = 0; i < 7; ++i) { u[i] = 0.0; f[i] = 0.0; }
-  if (DON == 1 && out.hot_at > 0 && lane == 0)  // (the hot launch beside this one waits for it, claim_hot)
-    __hip_atomic_store(out.hot_started, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 
   while (true) {
     // ---- refill idle lanes from the wave's chunk (one atomicAdd per 64 rays) ----
@@ -1714,11 +1712,7 @@ __device__ inline int64_t claim_hot(const SegOut& out, int lane) {
         }
         continue;
       }
-      const unsigned long long waited = __builtin_amdgcn_s_memrealtime() - t0;
-      if (done || waited > HOT_WAIT_TICKS) break;
-      if (waited > HOT_START_TICKS &&
-          __hip_atomic_load(out.hot_started, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u)
-        break;
+      if (done || __builtin_amdgcn_s_memrealtime() - t0 > HOT_WAIT_TICKS) break;
       __builtin_amdgcn_s_sleep(64);
     }
     if (rec >= 0) {  // (its producer raises it right after the record; bounded all the same)
@@ -3599,7 +3593,7 @@ hipError_t launch_propagate(const KParams& P, int64_t n, const SegIn& in, const 
   }
   // early graduation (SegOut::hot): only with graduation, and with the side stream that the hot
   // rays' tail launch runs on beside the bulk pass and the continuation
-  const bool hot = out.graduate > 0 && out.hot && out.hot_ready && out.hot_done && out.hot_started && out.hot_at > 0 &&
+  const bool hot = out.graduate > 0 && out.hot && out.hot_ready && out.hot_done && out.hot_at > 0 &&
                    out.hot_cap > 0 &&
                    hs.stream && hs.fork && hs.join && hs.zero_word;
   if (!hot) {
