@@ -104,6 +104,29 @@ def test_early_graduation_is_bit_exact(cfg, hot, monkeypatch):
         assert sref[k] == sgot[k], (cfg, hot, k, sref[k], sgot[k])
 
 
+def test_early_graduation_default_on_a_large_gr_batch(monkeypatch):
+    """The default rule and the claim order on 2*10^5 configs[3] rays (rays long enough to be hot
+    by it, as in the 10^6-ray batch): every output and counter equals the launch with both off
+    (ART_HOT_AT=0), which claims rays in index order and never graduates early."""
+    import adiabatic_raytracer_amd as A
+    from adiabatic_raytracer_amd import Engine
+    n = 200000
+    eng = Engine(A.Params(**CONFIGS["gr"]))
+    inp = eng.forward_roots(n, seed=1769)
+    got, sgot = _run(eng, inp, -1)
+    monkeypatch.setenv("ART_HOT_AT", "0")
+    ref, sref = _run(eng, inp, -1)
+    assert int((ref["n_accept"] + ref["n_reject"]).max()) > 4096  # (the batch has long rays)
+    has = ref["n_cross"] > 0
+    for k in ref:
+        a, b = ref[k], got[k]
+        if k.startswith("xc_"):
+            a, b = a.reshape(-1, n)[:, has], b.reshape(-1, n)[:, has]
+        assert np.array_equal(a, b, equal_nan=True), k
+    for k in ("attempts", "accepted", "root_steps", "scan_evals", "rays", "cert_steps"):
+        assert sref[k] == sgot[k], (k, sref[k], sgot[k])
+
+
 def test_tail_donation_rejects_bad_lane_counts():
     import adiabatic_raytracer_amd as A
     from adiabatic_raytracer_amd import Engine
