@@ -39,3 +39,26 @@ def test_engine_within_stated_tolerance(case, mode):
     assert np.all(g["flux"][0] == 0.0)
     assert np.array_equal(g["flux"][1], T.flux_of(g["status"], g["x_end"], g["k_end"], p.rNS))
     T.check(rep, mode)
+
+
+@pytest.mark.parametrize("mode", ["reference", "tight"])
+@pytest.mark.parametrize("case", ("flat", "gr"))
+def test_saved_points_within_stated_tolerance(case, mode):
+    """saveat (RayTracer.jl:176,383,427-444, art_propagate_traj_*): the interior saved positions of
+    the truth rays that reach ln t_end against the converged dense output at the same times
+    (tests/golden/truth_saveat_*.npz), within truth_compare.SAVED_TOL."""
+    import adiabatic_raytracer_amd as A
+    z, zs = T.load(case), T.load_saved(case)
+    n = z["n"]
+    p = A.Params(**T.NUMERICS[mode], **z["params"])
+    g = A.propagate_batch(p, z["x0"], z["k0"], z["erg"], -np.ones(n), np.full(n, -30.0), np.ones(n, np.int8),
+                          max_crossings=-1, ntimes=int(zs["ntimes"]))
+    rep = T.compare_saved(zs, g, n)
+    rep.update(case=case, mode=mode, what="saved points")
+    line = json.dumps(rep)
+    print(line)
+    if os.environ.get("ART_TRUTH_REPORT"):
+        with open(os.environ["ART_TRUTH_REPORT"], "a") as fh:
+            fh.write(line + "\n")
+    assert rep["compared"]["rays"] >= 0.95 * rep["compared"]["fixture rays"]
+    T.check_saved(rep, mode)

@@ -60,3 +60,18 @@ def test_truth_flux_is_the_fixture_histogram():
         z = T.load(case)
         f = T.flux_of(z["status"], z["x_end"], z["k_end"], z["params"].get("rNS", 10.0))
         assert np.array_equal(f, z["flux"]) and f.sum() > 0.15 * z["n"]
+
+
+@pytest.mark.parametrize("case", ("flat", "gr"))
+def test_truth_saveat_fixture_reproduced(case, oracle_lib):
+    """The committed saved points are what make_truth_saveat_fixture.py computes now (4 rays)."""
+    sys.path.insert(0, os.path.join(HERE, "golden"))
+    import make_truth_saveat_fixture as MS
+    z, zs = T.load(case), T.load_saved(case)
+    n = z["n"]
+    x0, k0 = z["x0"].reshape(3, n), z["k0"].reshape(3, n)
+    assert np.all(z["status"][zs["rays"]] == T.ST_SUCCESS)
+    for j in np.linspace(0, zs["rays"].size - 1, 4).astype(int):
+        i = int(zs["rays"][j])
+        pts = MS.saved_points((z["params"], x0[:, i].copy(), k0[:, i].copy(), float(z["erg"][i]), zs["times"]))
+        assert np.allclose(pts, zs["pos"][:, :, j], rtol=1e-10, atol=0)

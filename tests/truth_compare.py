@@ -50,6 +50,13 @@ TOL = {
     },
 }
 NUMERICS = {"reference": dict(abstol=1e-6, reltol=1e-7), "tight": dict(abstol=1e-10, reltol=1e-11)}
+# saved points (saveat, RayTracer.jl:176,383,427-444) at the interior times of the truth_saveat
+# fixtures (tests/golden/make_truth_saveat_fixture.py): the same 50th / 90th / 99th percentile
+# bounds on the relative position error. They carry the engine's cubic Hermite interpolant
+# between steps where the reference interpolates with Vern6's own dense output:
+# measured p99 2.0e-5 / 4.2e-8 (reference / tight, the larger of flat and GR; the errors fall
+# ~500x per 10^4x tighter tolerance, the cubic interpolant's h^4), bounds with a 5-7x margin.
+SAVED_TOL = {"reference": (3e-6, 3e-5, 1e-4), "tight": (1e-8, 1e-7, 3e-7)}
 # segment status and crossing detection (REFERENCE measured at most 1 of 1024 rays per
 # configuration, a near-tangent ray whose true condition stays within 4e-9 of zero; TIGHT none)
 MAX_STATUS_MISMATCH = {"reference": 0.01, "tight": 0.002}  # fraction of rays (truth not singular)
@@ -123,6 +130,31 @@ def compare(z, out):
     rep["flux_l1"] = float(np.abs(f_run - f_truth).sum() / max(1.0, f_truth.sum()))
     rep["flux_max_bin_diff"] = float(np.abs(f_run - f_truth).max())
     return rep
+
+
+def load_saved(case):
+    z = np.load(os.path.join(GOLDEN, f"truth_saveat_{case}.npz"))
+    return {k: z[k] for k in z.files}
+
+
+def compare_saved(zs, out, n):
+    """The run's interior saved positions (out["traj"], (3, ntimes, n)) against the truth's, on
+    the fixture's rays that the run also ends without a crossing."""
+    rays = zs["rays"]
+    ok = (np.asarray(out["status"])[rays] == ST_SUCCESS) & (np.asarray(out["traj_n"])[rays] == int(zs["ntimes"]))
+    r = rays[ok]
+    assert np.allclose(np.asarray(out["traj_t"])[1:-1, r], zs["times"][:, None], rtol=0, atol=1e-12)
+    got = np.asarray(out["traj"])[:, 1:-1, r]  # (3, ntimes - 2, rays)
+    want = zs["pos"][:, :, ok]
+    e = (np.abs(got - want).max(0) / np.linalg.norm(want, axis=0)).reshape(-1)
+    return {"saved position": _pct(e), "compared": {"saved points": int(e.size), "rays": int(ok.sum()),
+                                                     "fixture rays": int(rays.size)}}
+
+
+def check_saved(rep, mode="reference"):
+    b50, b90, b99 = SAVED_TOL[mode]
+    p50, p90, p99, _ = rep["saved position"]
+    assert p50 <= b50 and p90 <= b90 and p99 <= b99, (mode, rep["saved position"], SAVED_TOL[mode])
 
 
 def check(rep, mode="reference"):
