@@ -11,6 +11,7 @@
 # older source lacks newer symbols and fails to load):
 #   python adiabatic_raytracer_amd/build.py --variant tools/ab/libart_sect.so -DART_SECTION_TIMING
 #   python adiabatic_raytracer_amd/build.py --variant tools/ab/libart_ssec.so -DART_SAMPLER_SECTIONS
+# (.gpurunignore keeps tools/ab/*.so off other pushes: drop that line for a call with `sections`)
 # Writes gpurun_out/TAG_*; every GPU step has its own time limit; the first failure ends the run.
 TAG=${TAG:-r05fin}
 set -o pipefail
